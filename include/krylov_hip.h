@@ -1,0 +1,177 @@
+/*
+ * krylov_hip.h — C-ABI of libkrylov_hip.so, the MI355X (gfx950) inner loop of
+ * the Krylov solvers cg / gmres / minres.
+ *
+ * The reference (ju-liu/krylov 0.0.3) is pure Python: its hot path ends in
+ * SciPy/OpenBLAS/LAPACK calls made from the solver loops. Each entry point
+ * below replaces one of those call sites (cited per function) and is bound
+ * from Python through ctypes (krylov_amd/_lib.py; INTEGRATION.md shows the
+ * stub). Plain pointers and sizes only; no C++ exceptions cross this boundary.
+ *
+ * Conventions
+ *  - Every function returns an int status: KRY_OK (0) or a negative KRY_E*
+ *    code; kry_last_error() returns the message of the calling thread's last
+ *    failure.
+ *  - Handles are opaque and owned by the caller (create/destroy pairs).
+ *  - A vector is an n x k block stored row-major (the reference's "blocked"
+ *    right-hand sides, b.shape == (n, k)); k = 1 is a plain vector.
+ *  - One kry_ctx = one device + one HIP stream; a context is not thread-safe.
+ *  - Host buffers are C-contiguous arrays of the stated dtype.
+ *  - Device-resident state: per-iteration scalars never leave the GPU; the
+ *    solver "run" calls return the residual-norm history of the steps they
+ *    executed (the only mandatory device-to-host traffic).
+ */
+#ifndef KRYLOV_HIP_H
+#define KRYLOV_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct kry_ctx kry_ctx;
+typedef struct kry_csr kry_csr;
+typedef struct kry_vec kry_vec;
+typedef struct kry_cg kry_cg;
+typedef struct kry_gmres kry_gmres;
+typedef struct kry_minres kry_minres;
+typedef struct kry_comm kry_comm;
+
+/* value / index types */
+enum { KRY_F32 = 1, KRY_F64 = 2 };
+enum { KRY_I32 = 1, KRY_I64 = 2 };
+
+/* status codes */
+enum {
+  KRY_OK = 0,
+  KRY_EINVAL = -1,       /* bad argument (shape, dtype, null handle)   -> ValueError      */
+  KRY_ENOMEM = -2,       /* device allocation failed                   -> MemoryError     */
+  KRY_EDEVICE = -3,      /* HIP runtime / no device                    -> RuntimeError    */
+  KRY_EINVARIANT = -4,   /* Krylov space invariant (arnoldi.py:168-171) -> ArgumentError  */
+  KRY_EUNSUPPORTED = -5, /* outside the device path's scope            -> NotImplementedError */
+  KRY_ESINGULAR = -6,    /* singular triangular factor (gmres.py:36)   -> LinAlgError     */
+  KRY_ENONFINITE = -7,   /* NaN/inf handed to solve_triangular         -> ValueError      */
+  KRY_ECOMM = -8         /* RCCL failure                               -> RuntimeError    */
+};
+
+/* ---- library / context ------------------------------------------------ */
+int kry_version(void);
+const char *kry_last_error(void);
+int kry_device_count(int *count);
+int kry_ctx_create(int device, kry_ctx **out);
+int kry_ctx_destroy(kry_ctx *ctx);
+int kry_ctx_synchronize(kry_ctx *ctx);
+
+/* ---- CSR operator ------------------------------------------------------
+ * Replaces the scipy.sparse matrix the reference multiplies with `A @ x`
+ * (_helpers.py:44-48 Product.__matmul__, cg.py:86, gmres.py:106,
+ * minres.py:111,121). Uploads once; the library owns the device copy.
+ * Indices may be unsorted and contain duplicates; they are honoured in stored
+ * order (SciPy csr_matvec semantics). */
+int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr,
+                   const void *indices, const void *data, int dtype, int itype,
+                   kry_csr **out);
+int kry_csr_destroy(kry_csr *A);
+/* Host-only (no GPU needed): the row-tile partition the streaming SpMV kernel
+ * uses. Tiles hold <= tile_nnz nonzeros and <= tile_rows rows, except a single
+ * row longer than tile_nnz which gets a tile of its own. Returns the tile
+ * count; if row_starts != NULL it receives ntiles + 1 row offsets. */
+int kry_csr_partition(int64_t n, const void *indptr, int itype, int64_t tile_nnz,
+                      int64_t tile_rows, int64_t *ntiles, int64_t *row_starts);
+
+/* ---- vectors (n x k row-major blocks) ---------------------------------- */
+int kry_vec_create(kry_ctx *ctx, int64_t n, int32_t k, int dtype, kry_vec **out);
+int kry_vec_destroy(kry_vec *v);
+int kry_vec_upload(kry_vec *v, const void *host);
+int kry_vec_download(kry_vec *v, void *host);
+
+/* ---- primitives --------------------------------------------------------
+ * y = A @ x. Replaces SciPy csr_matvec / csr_matvecs (SURVEY §2 kernel
+ * table); bitwise equal to them (sequential per-row sum, no FMA). */
+int kry_spmv(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y);
+/* out[c] = sum_i x[i,c] * (w[i] * y[i,c])  (w == NULL: plain). Replaces
+ * get_default_inner (_helpers.py:101-110) and the weighted inner of
+ * tests/test_solvers.py:157-161. Deterministic two-stage reduction. */
+int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out);
+/* y = alpha[c] * x + y  (the reference's `y += alpha * x`, e.g. cg.py:196). */
+int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y);
+/* Batched LAPACK >= 3.10 ?lartg on device (givens.py:35-40); host arrays of
+ * `count` values of `dtype`. Bitwise equal to scipy.linalg.lapack ?lartg. */
+int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void *g,
+              void *c, void *s, void *r);
+
+/* ---- CG (cg.py:16-259, M = Ml = I) --------------------------------------
+ * start: r0 = b - A x0, rho0 = <r0, r0>_w; rho0 (k values) returned.
+ * run:   executes up to max_steps iterations of cg.py:175-217 on device; stops
+ *        early after the first iteration whose residual norms all satisfy
+ *        resnorm <= criterion (the test at cg.py:156). Writes the new residual
+ *        norms (steps_done x k) to resnorms.
+ * residual: explicit ||b - A xk||_w with xk = x0 + yk (cg.py:158-160).
+ * get:   download xk (which = 0) or the updated residual r (which = 1). */
+int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out);
+int kry_cg_destroy(kry_cg *s);
+int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0);
+int kry_cg_set_criterion(kry_cg *s, const double *criterion);
+int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnorms);
+int kry_cg_residual(kry_cg *s, double *resnorm);
+int kry_cg_get(kry_cg *s, int which, void *host);
+
+/* ---- GMRES (gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200, M = I) -------
+ * create: workspace for up to `maxiter` Arnoldi steps with `sweeps` MGS
+ *         passes per step ("mgs" = 1, "mgsK" = K).
+ * start:  r0 = b - A x0, ||r0||, V0 = r0 / ||r0|| (guarded), y[0] = ||r0||.
+ * run:    up to max_steps Arnoldi + Givens steps; stops early after a step
+ *         whose |y[k+1]| all satisfy the criterion or that found the space
+ *         invariant (*invariant = 1). Returns KRY_EINVARIANT if called after
+ *         an invariant step (arnoldi.py:168-171).
+ * solution: xk = x0 + sum_i yy_i V_i with yy = R^-1 y (gmres.py:89-99),
+ *         left on device; residual: explicit ||b - A xk||. */
+int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t maxiter,
+                     int32_t sweeps, kry_gmres **out);
+int kry_gmres_destroy(kry_gmres *s);
+int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm);
+int kry_gmres_set_criterion(kry_gmres *s, const double *criterion);
+int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done,
+                  double *resnorms, int32_t *invariant);
+int kry_gmres_solution(kry_gmres *s);
+int kry_gmres_residual(kry_gmres *s, double *resnorm);
+int kry_gmres_get(kry_gmres *s, int which, void *host);
+
+/* ---- MINRES (minres.py:28-253, ArnoldiLanczos arnoldi.py:203-281, M = I) --
+ * Same run protocol as CG; R, rotations, y, z and W are float64 as in the
+ * reference under NumPy-2 promotion (minres.py:195,219). */
+int kry_minres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_minres **out);
+int kry_minres_destroy(kry_minres *s);
+int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm);
+int kry_minres_set_criterion(kry_minres *s, const double *criterion);
+int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done,
+                   double *resnorms, int32_t *invariant);
+int kry_minres_residual(kry_minres *s, double *resnorm);
+int kry_minres_get(kry_minres *s, int which, void *host);
+
+/* ---- multi-GPU: RHS columns sharded one block per GPU ----
+ * One RCCL communicator per process/GPU. After attaching, each CG iteration
+ * performs exactly one ncclAllReduce(sum, f64, count = total_k) on the
+ * zero-padded residual-norm vector so every rank applies the reference's
+ * global stop rule np.all(resnorms[-1] <= criterion) (cg.py:156). */
+int kry_comm_unique_id(void *id128);
+int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id128,
+                    kry_comm **out);
+int kry_comm_destroy(kry_comm *c);
+/* in-place sum over ranks of `count` host doubles (setup-time exchanges) */
+int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);
+int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k);
+
+/* ---- timing: HIP events on the context stream --------------------------- */
+int kry_timer_start(kry_ctx *ctx);
+int kry_timer_stop(kry_ctx *ctx, double *ms);
+/* average device time of the most recent SpMV launches made by CG runs,
+ * measured with HIP events around each SpMV launch when enabled */
+int kry_profile_enable(kry_ctx *ctx, int enable);
+int kry_profile_read(kry_ctx *ctx, int kernel_id, int64_t *count, double *total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRYLOV_HIP_H */

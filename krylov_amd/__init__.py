@@ -1,0 +1,36 @@
+"""krylov_amd — MI355X-native inner loop for the Krylov solvers of
+``ju-liu/krylov`` (cg / gmres / minres with the reference call signatures).
+
+The per-iteration work (CSR SpMV, AXPY/scale updates, inner products and
+norms, GMRES modified Gram-Schmidt + Givens, the MINRES Lanczos/QR
+recurrences) runs as hand-written gfx950 HIP kernels in ``libkrylov_hip.so``
+reached through a ctypes C-ABI (``include/krylov_hip.h``). There is no CPU
+fallback: importing this package without the built library raises.
+"""
+from ._helpers import Identity, Info, WeightedInner, aslinearoperator, get_default_inner
+from .cg import cg
+from .errors import ArgumentError
+from .givens import givens, lartg
+from .gmres import gmres, gmres_restarted
+from .minres import minres
+from .sparse import CsrOperator, as_device_operator
+
+__version__ = "0.1.0"
+
+__all__ = [
+    "cg",
+    "gmres",
+    "gmres_restarted",
+    "minres",
+    "givens",
+    "lartg",
+    "CsrOperator",
+    "as_device_operator",
+    "WeightedInner",
+    "Identity",
+    "Info",
+    "aslinearoperator",
+    "get_default_inner",
+    "ArgumentError",
+    "__version__",
+]

@@ -1,0 +1,160 @@
+"""ctypes binding of ``libkrylov_hip.so`` (declared in ``include/krylov_hip.h``).
+
+The shared library is the only compute path of this package. If it is missing
+the import fails loudly; there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .errors import ArgumentError
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
+
+KRY_F32, KRY_F64 = 1, 2
+KRY_I32, KRY_I64 = 1, 2
+
+KRY_OK = 0
+KRY_EINVAL = -1
+KRY_ENOMEM = -2
+KRY_EDEVICE = -3
+KRY_EINVARIANT = -4
+KRY_EUNSUPPORTED = -5
+KRY_ESINGULAR = -6
+KRY_ENONFINITE = -7
+KRY_ECOMM = -8
+
+PROF_SPMV, PROF_UPDATE, PROF_MGS, PROF_OTHER = 0, 1, 2, 3
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "or `make -C krylov_amd/csrc` (hipcc, gfx950). krylov_amd has no CPU fallback."
+    )
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_vp = ctypes.c_void_p
+_pvp = ctypes.POINTER(ctypes.c_void_p)
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip32 = ctypes.POINTER(ctypes.c_int32)
+_ip64 = ctypes.POINTER(ctypes.c_int64)
+
+# name: argtypes (all return int status except kry_version / kry_last_error)
+_SIGNATURES = {
+    "kry_device_count": [ctypes.POINTER(_int)],
+    "kry_ctx_create": [_int, _pvp],
+    "kry_ctx_destroy": [_vp],
+    "kry_ctx_synchronize": [_vp],
+    "kry_csr_create": [_vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
+    "kry_csr_destroy": [_vp],
+    "kry_csr_partition": [_i64, _vp, _int, _i64, _i64, _ip64, _ip64],
+    "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
+    "kry_vec_destroy": [_vp],
+    "kry_vec_upload": [_vp, _vp],
+    "kry_vec_download": [_vp, _vp],
+    "kry_spmv": [_vp, _vp, _vp, _vp],
+    "kry_dot": [_vp, _vp, _vp, _vp, _dp],
+    "kry_axpy": [_vp, _dp, _vp, _vp],
+    "kry_lartg": [_vp, _i64, _int, _vp, _vp, _vp, _vp, _vp],
+    "kry_cg_create": [_vp, _vp, _i32, _int, _pvp],
+    "kry_cg_destroy": [_vp],
+    "kry_cg_start": [_vp, _vp, _vp, _vp, _dp],
+    "kry_cg_set_criterion": [_vp, _dp],
+    "kry_cg_run": [_vp, _i32, _ip32, _dp],
+    "kry_cg_residual": [_vp, _dp],
+    "kry_cg_get": [_vp, _int, _vp],
+    "kry_gmres_create": [_vp, _vp, _i32, _int, _i32, _i32, _pvp],
+    "kry_gmres_destroy": [_vp],
+    "kry_gmres_start": [_vp, _vp, _vp, _vp, _dp],
+    "kry_gmres_set_criterion": [_vp, _dp],
+    "kry_gmres_run": [_vp, _i32, _ip32, _dp, _ip32],
+    "kry_gmres_solution": [_vp],
+    "kry_gmres_residual": [_vp, _dp],
+    "kry_gmres_get": [_vp, _int, _vp],
+    "kry_minres_create": [_vp, _vp, _i32, _int, _pvp],
+    "kry_minres_destroy": [_vp],
+    "kry_minres_start": [_vp, _vp, _vp, _vp, _dp],
+    "kry_minres_set_criterion": [_vp, _dp],
+    "kry_minres_run": [_vp, _i32, _ip32, _dp, _ip32],
+    "kry_minres_residual": [_vp, _dp],
+    "kry_minres_get": [_vp, _int, _vp],
+    "kry_comm_unique_id": [_vp],
+    "kry_comm_create": [_vp, _i32, _i32, _vp, _pvp],
+    "kry_comm_destroy": [_vp],
+    "kry_comm_allreduce": [_vp, _dp, _i32],
+    "kry_cg_attach_comm": [_vp, _vp, _i32, _i32],
+    "kry_timer_start": [_vp],
+    "kry_timer_stop": [_vp, _dp],
+    "kry_profile_enable": [_vp, _int],
+    "kry_profile_read": [_vp, _int, _ip64, _dp],
+}
+
+for _name, _args in _SIGNATURES.items():
+    _f = getattr(lib, _name)
+    _f.argtypes = _args
+    _f.restype = _int
+lib.kry_version.argtypes = []
+lib.kry_version.restype = _int
+lib.kry_last_error.argtypes = []
+lib.kry_last_error.restype = ctypes.c_char_p
+
+EXPORTED = sorted(list(_SIGNATURES) + ["kry_version", "kry_last_error"])
+
+
+def check(rc):
+    """Map a C-ABI status to the exception the reference would raise."""
+    if rc == KRY_OK:
+        return
+    msg = (lib.kry_last_error() or b"").decode(errors="replace")
+    if rc == KRY_EINVARIANT:
+        raise ArgumentError(msg)
+    if rc == KRY_ENOMEM:
+        raise MemoryError(msg)
+    if rc in (KRY_EINVAL, KRY_ENONFINITE):
+        raise ValueError(msg)
+    if rc == KRY_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    if rc == KRY_ESINGULAR:
+        raise np.linalg.LinAlgError(msg)
+    raise RuntimeError(f"libkrylov_hip error {rc}: {msg}")
+
+
+def dtype_code(dt):
+    dt = np.dtype(dt)
+    if dt == np.float64:
+        return KRY_F64
+    if dt == np.float32:
+        return KRY_F32
+    raise TypeError(f"the MI355X path computes in float32/float64, not {dt}")
+
+
+def itype_code(dt):
+    dt = np.dtype(dt)
+    if dt == np.int32:
+        return KRY_I32
+    if dt == np.int64:
+        return KRY_I64
+    raise TypeError(f"CSR index arrays must be int32 or int64, not {dt}")
+
+
+def ptr(a):
+    """Data pointer of a C-contiguous numpy array (as a c_void_p)."""
+    assert a.flags.c_contiguous
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def dptr(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def device_count():
+    c = _int(0)
+    check(lib.kry_device_count(ctypes.byref(c)))
+    return c.value

@@ -1,0 +1,115 @@
+"""Preconditioned CG driver (reference ``cg.py:16-259``) over the device loop.
+
+The loop structure, stop rule, explicit-residual recheck and ``Info`` record
+are the reference's; every iteration's arithmetic (SpMV, inner products, the
+x/r/p updates and the scalar recurrences) runs on the GPU through
+``kry_cg_run`` in chunks of up to ``CHUNK`` iterations with one host sync per
+chunk. The device stops a chunk right after the first iteration whose
+residual norms satisfy the criterion, so the host sees exactly the
+iterations the reference performs.
+"""
+import ctypes
+import weakref
+
+import numpy as np
+
+from . import _helpers, _lib
+from ._helpers import Info, Problem
+from ._lib import check, lib
+
+
+class _CGState:
+    def __init__(self, prob):
+        self.prob = prob
+        h = ctypes.c_void_p()
+        check(lib.kry_cg_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype), ctypes.byref(h)))
+        self.h = h
+        self._fin = weakref.finalize(self, lib.kry_cg_destroy, h)
+
+    def start(self):
+        p = self.prob
+        rho = np.zeros(p.kpad)
+        check(lib.kry_cg_start(self.h, p.b_dev.handle, p.x0_dev.handle if p.x0_dev else None,
+                               p.w_dev.handle if p.w_dev else None, _lib.dptr(rho)))
+        return rho
+
+    def set_criterion(self, crit):
+        crit = np.ascontiguousarray(crit, dtype=np.float64)
+        check(lib.kry_cg_set_criterion(self.h, _lib.dptr(crit)))
+
+    def run(self, steps, ncols=None):
+        ncols = self.prob.kpad if ncols is None else ncols
+        out = np.zeros((max(steps, 1), ncols))
+        done = ctypes.c_int32()
+        check(lib.kry_cg_run(self.h, int(steps), ctypes.byref(done), _lib.dptr(out)))
+        return out[: done.value]
+
+    def residual_norm2(self):
+        out = np.zeros(self.prob.kpad)
+        check(lib.kry_cg_residual(self.h, _lib.dptr(out)))
+        return out
+
+    def get(self, which):
+        p = self.prob
+        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        check(lib.kry_cg_get(self.h, which, _lib.ptr(out)))
+        return out
+
+
+def _norm_from_sq(prob, sq):
+    return np.sqrt(np.asarray(sq[: prob.kc]).astype(prob.inner_dtype))
+
+
+def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None,
+       return_arnoldi=False, callback=None):
+    """Preconditioned CG, reference signature (``cg.py:16-28``).
+
+    ``A``: ``krylov_amd.CsrOperator``, scipy.sparse matrix or dense ndarray
+    (uploaded once as CSR). ``inner``: ``None`` or ``WeightedInner``.
+    ``M``/``Ml``: ``None`` or ``Identity`` on the device path.
+    """
+    if return_arnoldi:
+        raise NotImplementedError("return_arnoldi is not on the MI355X path yet")
+    prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
+    N = prob.A.shape[0]
+    maxiter = N if maxiter is None else maxiter
+    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
+
+    st = _CGState(prob)
+    rho0 = st.start()
+    rn0 = _norm_from_sq(prob, rho0)
+    if callback is not None:
+        callback(x0_host, prob.unpad_vec(st.get(1), prob.r0_dtype))
+    resnorms = [prob.colvals(rn0)]
+    criterion = np.maximum(tol * resnorms[0], atol)
+    st.set_criterion(prob.pad_cols(criterion, np.inf))
+
+    k = 0
+    success = False
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            # the reference's explicit residual recheck (cg.py:156-164)
+            resnorms[-1] = prob.colvals(_norm_from_sq(prob, st.residual_norm2()))
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        steps = 1 if callback is not None else min(_helpers.CHUNK, maxiter - k)
+        hist = st.run(steps)
+        for row in hist:
+            resnorms.append(prob.colvals(row))
+            k += 1
+        if callback is not None and len(hist):
+            callback(prob.unpad_vec(st.get(0), prob.r0_dtype), prob.unpad_vec(st.get(1), prob.r0_dtype))
+
+    xk = prob.unpad_vec(st.get(0), prob.r0_dtype)
+    num_operations = {
+        "A": 1 + k,
+        "M": 2 + k,
+        "Ml": 2 + k,
+        "Mr": 1 + k,
+        "inner": 2 + 2 * k,
+        "axpy": 2 + 2 * k,
+    }
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)

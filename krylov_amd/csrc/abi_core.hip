@@ -1,0 +1,485 @@
+// C-ABI: library, context, CSR operator, vectors, primitives, timers.
+#include <algorithm>
+#include <cstring>
+
+#include "device.hpp"
+
+using namespace kry;
+
+namespace kry {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+void *dev_alloc(size_t bytes) {
+  void *p = nullptr;
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess)
+    throw Error{e == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE,
+                std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e)};
+  return p;
+}
+
+void dev_free(void *p) {
+  if (p) (void)hipFree(p);
+}
+
+ProfScope::ProfScope(kry_ctx *c, int kernel_id) : ctx(c), id(kernel_id) {
+  if (!ctx->profile) return;
+  if (ctx->ev_used == ctx->ev_pool.size()) {
+    hipEvent_t a, b;
+    KRY_HIP(hipEventCreate(&a));
+    KRY_HIP(hipEventCreate(&b));
+    ctx->ev_pool.emplace_back(a, b);
+    ctx->ev_ids.push_back(0);
+  }
+  auto &pr = ctx->ev_pool[ctx->ev_used];
+  ctx->ev_ids[ctx->ev_used] = id;
+  KRY_HIP(hipEventRecord(pr.first, ctx->stream));
+  e1 = pr.second;
+}
+
+ProfScope::~ProfScope() {
+  if (!e1) return;
+  (void)hipEventRecord(e1, ctx->stream);
+  ctx->ev_used++;
+}
+
+// Tile partition for the streaming SpMV kernel (see krylov_hip.h).
+template <typename I>
+static int64_t partition_rows(int64_t n, const I *ip, int64_t tile_nnz, int64_t tile_rows,
+                              std::vector<int64_t> *out) {
+  int64_t count = 0;
+  if (out) out->push_back(0);
+  int64_t r = 0;
+  while (r < n) {
+    const int64_t start = r, e_start = (int64_t)ip[r];
+    if ((int64_t)ip[r + 1] - e_start > tile_nnz) {
+      r += 1;
+    } else {
+      while (r < n && r - start < tile_rows && (int64_t)ip[r + 1] - e_start <= tile_nnz) ++r;
+    }
+    ++count;
+    if (out) out->push_back(r);
+  }
+  return count;
+}
+
+template <typename V>
+struct OpDot {
+  const V *x, *y;
+  const double *w;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V a[W], b[W];
+    VIO<V>::load(x, e, N, a);
+    VIO<V>::load(y, e, N, b);
+#pragma unroll
+    for (int v = 0; v < W; ++v)
+      if (e + v < N)
+        acc[v] += w ? dterm_w((double)a[v], w[(e + v) / k], (double)b[v]) : dterm((double)a[v], (double)b[v]);
+  }
+};
+
+template <typename V>
+struct OpAxpy {
+  const V *x;
+  V *y;
+  const double *alpha;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V a[W], b[W];
+    VIO<V>::load(x, e, N, a);
+    VIO<V>::load(y, e, N, b);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V t = (V)alpha[(e + v) & (k - 1)] * a[v];
+      b[v] = b[v] + t;
+    }
+    VIO<V>::store(y, e, N, b);
+  }
+};
+
+template <typename T>
+__global__ void lartg_kernel(int64_t count, const T *f, const T *g, T *c, T *s, T *r) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) lartg<T>(f[i], g[i], c[i], s[i], r[i]);
+}
+
+}  // namespace kry
+
+#define KRY_API_BEGIN try {
+#define KRY_API_END                                                    \
+  return KRY_OK;                                                       \
+  }                                                                    \
+  catch (const kry::Error &e) {                                        \
+    kry::set_error(e.msg);                                             \
+    return e.code;                                                     \
+  }                                                                    \
+  catch (const std::exception &e) {                                    \
+    kry::set_error(e.what());                                          \
+    return KRY_EDEVICE;                                                \
+  }
+
+extern "C" {
+
+int kry_version(void) { return 100; }
+
+const char *kry_last_error(void) { return kry::g_last_error.c_str(); }
+
+int kry_device_count(int *count) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(count, KRY_EINVAL, "null count");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  *count = (e == hipSuccess) ? c : 0;
+  KRY_API_END
+}
+
+int kry_ctx_create(int device, kry_ctx **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(out, KRY_EINVAL, "null out");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  KRY_REQUIRE(e == hipSuccess && c > 0, KRY_EDEVICE, "no HIP device available");
+  KRY_REQUIRE(device >= 0 && device < c, KRY_EINVAL, "device index out of range");
+  KRY_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  KRY_HIP(hipGetDeviceProperties(&prop, device));
+  KRY_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, KRY_EDEVICE,
+              std::string("libkrylov_hip is built for gfx950 only; found ") + prop.gcnArchName);
+  auto *ctx = new kry_ctx();
+  ctx->device = device;
+  KRY_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  KRY_HIP(hipEventCreate(&ctx->t0));
+  KRY_HIP(hipEventCreate(&ctx->t1));
+  *out = ctx;
+  KRY_API_END
+}
+
+int kry_ctx_destroy(kry_ctx *ctx) {
+  KRY_API_BEGIN
+  if (!ctx) return KRY_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &p : ctx->ev_pool) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  (void)hipEventDestroy(ctx->t0);
+  (void)hipEventDestroy(ctx->t1);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  KRY_API_END
+}
+
+int kry_ctx_synchronize(kry_ctx *ctx) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx, KRY_EINVAL, "null ctx");
+  KRY_HIP(hipStreamSynchronize(ctx->stream));
+  KRY_API_END
+}
+
+int kry_csr_partition(int64_t n, const void *indptr, int itype, int64_t tile_nnz, int64_t tile_rows,
+                      int64_t *ntiles, int64_t *row_starts) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(indptr && ntiles && n >= 0 && tile_nnz > 0 && tile_rows > 0, KRY_EINVAL,
+              "bad partition arguments");
+  std::vector<int64_t> rs;
+  int64_t cnt;
+  if (itype == KRY_I32)
+    cnt = partition_rows(n, static_cast<const int32_t *>(indptr), tile_nnz, tile_rows, row_starts ? &rs : nullptr);
+  else if (itype == KRY_I64)
+    cnt = partition_rows(n, static_cast<const int64_t *>(indptr), tile_nnz, tile_rows, row_starts ? &rs : nullptr);
+  else
+    throw Error{KRY_EINVAL, "bad itype"};
+  *ntiles = cnt;
+  if (row_starts) std::copy(rs.begin(), rs.end(), row_starts);
+  KRY_API_END
+}
+
+int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
+                   const void *data, int dtype, int itype, kry_csr **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && out && indptr && (nnz == 0 || (indices && data)), KRY_EINVAL, "null argument");
+  KRY_REQUIRE(n >= 0 && nnz >= 0, KRY_EINVAL, "negative size");
+  KRY_REQUIRE(dtype == KRY_F32 || dtype == KRY_F64, KRY_EINVAL, "dtype must be f32 or f64");
+  KRY_REQUIRE(itype == KRY_I32 || itype == KRY_I64, KRY_EINVAL, "itype must be i32 or i64");
+  if (itype == KRY_I32) KRY_REQUIRE(nnz < (int64_t(1) << 31) && n < (int64_t(1) << 31), KRY_EINVAL,
+                                    "int32 indices cannot address this matrix");
+  KRY_HIP(hipSetDevice(ctx->device));
+  auto *A = new kry_csr();
+  try {
+    A->ctx = ctx;
+    A->n = n;
+    A->nnz = nnz;
+    A->dtype = dtype;
+    A->itype = itype;
+    const size_t is = isize(itype), vs = dsize(dtype);
+    const int64_t nnz_pad = (nnz + 7) / 4 * 4;  // 16-byte loads may run 3 past the end
+    A->indptr = dev_alloc((n + 1) * is);
+    A->indices = dev_alloc(nnz_pad * is);
+    A->data = dev_alloc(nnz_pad * vs);
+    KRY_HIP(hipMemcpyAsync(A->indptr, indptr, (n + 1) * is, hipMemcpyHostToDevice, ctx->stream));
+    KRY_HIP(hipMemsetAsync(A->indices, 0, nnz_pad * is, ctx->stream));
+    KRY_HIP(hipMemsetAsync(A->data, 0, nnz_pad * vs, ctx->stream));
+    if (nnz) {
+      KRY_HIP(hipMemcpyAsync(A->indices, indices, nnz * is, hipMemcpyHostToDevice, ctx->stream));
+      KRY_HIP(hipMemcpyAsync(A->data, data, nnz * vs, hipMemcpyHostToDevice, ctx->stream));
+    }
+    std::vector<int64_t> rs;
+    if (itype == KRY_I32) {
+      const int32_t *ip = static_cast<const int32_t *>(indptr);
+      KRY_REQUIRE(ip[0] == 0 && ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
+      A->ntiles = partition_rows(n, ip, kTileNnz, kTileRows, &rs);
+      std::vector<int32_t> t(rs.begin(), rs.end());
+      A->tiles = dev_alloc(t.size() * 4);
+      KRY_HIP(hipMemcpyAsync(A->tiles, t.data(), t.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+      KRY_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+      const int64_t *ip = static_cast<const int64_t *>(indptr);
+      KRY_REQUIRE(ip[0] == 0 && ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
+      A->ntiles = partition_rows(n, ip, kTileNnz, kTileRows, &rs);
+      A->tiles = dev_alloc(rs.size() * 8);
+      KRY_HIP(hipMemcpyAsync(A->tiles, rs.data(), rs.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      KRY_HIP(hipStreamSynchronize(ctx->stream));
+    }
+  } catch (...) {
+    dev_free(A->indptr);
+    dev_free(A->indices);
+    dev_free(A->data);
+    dev_free(A->tiles);
+    delete A;
+    throw;
+  }
+  *out = A;
+  KRY_API_END
+}
+
+int kry_csr_destroy(kry_csr *A) {
+  KRY_API_BEGIN
+  if (!A) return KRY_OK;
+  (void)hipSetDevice(A->ctx->device);
+  (void)hipStreamSynchronize(A->ctx->stream);
+  dev_free(A->indptr);
+  dev_free(A->indices);
+  dev_free(A->data);
+  dev_free(A->tiles);
+  delete A;
+  KRY_API_END
+}
+
+int kry_vec_create(kry_ctx *ctx, int64_t n, int32_t k, int dtype, kry_vec **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(n >= 0 && k >= 1, KRY_EINVAL, "bad vector shape");
+  KRY_REQUIRE(dtype == KRY_F32 || dtype == KRY_F64, KRY_EINVAL, "dtype must be f32 or f64");
+  KRY_HIP(hipSetDevice(ctx->device));
+  auto *v = new kry_vec();
+  v->ctx = ctx;
+  v->n = n;
+  v->k = k;
+  v->dtype = dtype;
+  const size_t elems = ((size_t)n * k + 15) / 16 * 16;
+  try {
+    v->d = dev_alloc(elems * dsize(dtype));
+    KRY_HIP(hipMemsetAsync(v->d, 0, elems * dsize(dtype), ctx->stream));
+  } catch (...) {
+    delete v;
+    throw;
+  }
+  *out = v;
+  KRY_API_END
+}
+
+int kry_vec_destroy(kry_vec *v) {
+  KRY_API_BEGIN
+  if (!v) return KRY_OK;
+  (void)hipSetDevice(v->ctx->device);
+  (void)hipStreamSynchronize(v->ctx->stream);
+  dev_free(v->d);
+  delete v;
+  KRY_API_END
+}
+
+int kry_vec_upload(kry_vec *v, const void *host) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(v && host, KRY_EINVAL, "null argument");
+  KRY_HIP(hipMemcpyAsync(v->d, host, v->bytes(), hipMemcpyHostToDevice, v->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(v->ctx->stream));
+  KRY_API_END
+}
+
+int kry_vec_download(kry_vec *v, void *host) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(v && host, KRY_EINVAL, "null argument");
+  KRY_HIP(hipMemcpyAsync(host, v->d, v->bytes(), hipMemcpyDeviceToHost, v->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(v->ctx->stream));
+  KRY_API_END
+}
+
+int kry_spmv(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && x && y, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(x->n == A->n && y->n == A->n && x->k == y->k, KRY_EINVAL, "shape mismatch");
+  KRY_REQUIRE(x->dtype == y->dtype, KRY_EINVAL, "dtype mismatch");
+  KRY_REQUIRE(is_pow2(x->k) && x->k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_HIP(hipSetDevice(ctx->device));
+  const int k = x->k;
+  dispatch_vmi(x->dtype, A->dtype, A->itype, [&](auto v0, auto m0, auto i0) {
+    using V = decltype(v0);
+    using MV = decltype(m0);
+    using I = decltype(i0);
+    ProfScope ps(ctx, PROF_SPMV);
+    launch_spmv<V, MV, I>(A, k, SrcPlain<V>{static_cast<const V *>(x->d), k},
+                      EpiStore<V>{static_cast<V *>(y->d), k}, nullptr, nullptr, nullptr, 0, ctx->stream);
+  });
+  KRY_HIP(hipStreamSynchronize(ctx->stream));
+  KRY_API_END
+}
+
+int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && x && y && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(x->n == y->n && x->k == y->k && x->dtype == y->dtype, KRY_EINVAL, "shape mismatch");
+  KRY_REQUIRE(!w || (w->n == x->n && w->k == 1 && w->dtype == KRY_F64), KRY_EINVAL,
+              "weights must be an (n,) float64 vector");
+  KRY_REQUIRE(is_pow2(x->k) && x->k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_HIP(hipSetDevice(ctx->device));
+  const int k = x->k;
+  const int64_t N = x->n * (int64_t)k;
+  double *part = static_cast<double *>(dev_alloc((kMaxGrid + 1) * (size_t)k * 8));
+  try {
+    int P;
+    const double *wd = w ? static_cast<const double *>(w->d) : nullptr;
+    if (x->dtype == KRY_F64)
+      P = launch_elementwise<double>(N, k, OpDot<double>{static_cast<const double *>(x->d), static_cast<const double *>(y->d), wd, k},
+                                     part, nullptr, 0, ctx->stream);
+    else
+      P = launch_elementwise<float>(N, k, OpDot<float>{static_cast<const float *>(x->d), static_cast<const float *>(y->d), wd, k},
+                                    part, nullptr, 0, ctx->stream);
+    double *res = part + (size_t)kMaxGrid * k;
+    hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, ctx->stream, part, P, k, res);
+    KRY_HIP(hipGetLastError());
+    KRY_HIP(hipMemcpyAsync(out, res, k * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    dev_free(part);
+    throw;
+  }
+  dev_free(part);
+  KRY_API_END
+}
+
+int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && alpha && x && y, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(x->n == y->n && x->k == y->k && x->dtype == y->dtype, KRY_EINVAL, "shape mismatch");
+  KRY_REQUIRE(is_pow2(x->k) && x->k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_HIP(hipSetDevice(ctx->device));
+  const int k = x->k;
+  const int64_t N = x->n * (int64_t)k;
+  double *a = static_cast<double *>(dev_alloc(k * 8));
+  try {
+    KRY_HIP(hipMemcpyAsync(a, alpha, k * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (x->dtype == KRY_F64)
+      launch_elementwise<double>(N, k, OpAxpy<double>{static_cast<const double *>(x->d), static_cast<double *>(y->d), a, k},
+                                 nullptr, nullptr, 0, ctx->stream);
+    else
+      launch_elementwise<float>(N, k, OpAxpy<float>{static_cast<const float *>(x->d), static_cast<float *>(y->d), a, k},
+                                nullptr, nullptr, 0, ctx->stream);
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    dev_free(a);
+    throw;
+  }
+  dev_free(a);
+  KRY_API_END
+}
+
+int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void *g, void *c, void *s,
+              void *r) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && f && g && c && s && r && count >= 0, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(dtype == KRY_F32 || dtype == KRY_F64, KRY_EINVAL, "bad dtype");
+  if (count == 0) return KRY_OK;
+  KRY_HIP(hipSetDevice(ctx->device));
+  const size_t vs = dsize(dtype), bytes = count * vs;
+  char *buf = static_cast<char *>(dev_alloc(5 * bytes));
+  try {
+    KRY_HIP(hipMemcpyAsync(buf, f, bytes, hipMemcpyHostToDevice, ctx->stream));
+    KRY_HIP(hipMemcpyAsync(buf + bytes, g, bytes, hipMemcpyHostToDevice, ctx->stream));
+    const int grid = (int)((count + kBlock - 1) / kBlock);
+    if (dtype == KRY_F64) {
+      double *b = reinterpret_cast<double *>(buf);
+      hipLaunchKernelGGL(lartg_kernel<double>, dim3(grid), dim3(kBlock), 0, ctx->stream, count, b, b + count,
+                         b + 2 * count, b + 3 * count, b + 4 * count);
+    } else {
+      float *b = reinterpret_cast<float *>(buf);
+      hipLaunchKernelGGL(lartg_kernel<float>, dim3(grid), dim3(kBlock), 0, ctx->stream, count, b, b + count,
+                         b + 2 * count, b + 3 * count, b + 4 * count);
+    }
+    KRY_HIP(hipGetLastError());
+    KRY_HIP(hipMemcpyAsync(c, buf + 2 * bytes, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    KRY_HIP(hipMemcpyAsync(s, buf + 3 * bytes, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    KRY_HIP(hipMemcpyAsync(r, buf + 4 * bytes, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    dev_free(buf);
+    throw;
+  }
+  dev_free(buf);
+  KRY_API_END
+}
+
+int kry_timer_start(kry_ctx *ctx) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx, KRY_EINVAL, "null ctx");
+  KRY_HIP(hipEventRecord(ctx->t0, ctx->stream));
+  KRY_API_END
+}
+
+int kry_timer_stop(kry_ctx *ctx, double *ms) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && ms, KRY_EINVAL, "null argument");
+  KRY_HIP(hipEventRecord(ctx->t1, ctx->stream));
+  KRY_HIP(hipEventSynchronize(ctx->t1));
+  float f = 0;
+  KRY_HIP(hipEventElapsedTime(&f, ctx->t0, ctx->t1));
+  *ms = f;
+  KRY_API_END
+}
+
+int kry_profile_enable(kry_ctx *ctx, int enable) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx, KRY_EINVAL, "null ctx");
+  KRY_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->profile = enable != 0;
+  ctx->ev_used = 0;
+  for (int i = 0; i < 4; ++i) {
+    ctx->prof_count[i] = 0;
+    ctx->prof_ms[i] = 0;
+  }
+  KRY_API_END
+}
+
+int kry_profile_read(kry_ctx *ctx, int kernel_id, int64_t *count, double *total_ms) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && count && total_ms && kernel_id >= 0 && kernel_id < 4, KRY_EINVAL, "bad argument");
+  KRY_HIP(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < ctx->ev_used; ++i) {
+    float f = 0;
+    KRY_HIP(hipEventElapsedTime(&f, ctx->ev_pool[i].first, ctx->ev_pool[i].second));
+    ctx->prof_count[ctx->ev_ids[i]] += 1;
+    ctx->prof_ms[ctx->ev_ids[i]] += f;
+  }
+  ctx->ev_used = 0;
+  *count = ctx->prof_count[kernel_id];
+  *total_ms = ctx->prof_ms[kernel_id];
+  KRY_API_END
+}
+
+}  // extern "C"

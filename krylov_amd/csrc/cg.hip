@@ -1,0 +1,431 @@
+// CG device loop (reference cg.py:16-259 with M = Ml = I).
+//
+// One iteration = four launches on the context stream, no host sync:
+//   1. SpMV   p = r + omega p_old (materialised in the gather), Ap = A p,
+//             partial <p, Ap>                          cg.py:175-183
+//   2. tiny   alpha = rho / guard(<p, Ap>)             cg.py:185
+//   3. update y += alpha p, r -= alpha Ap, partial <r, r>   cg.py:196-209
+//   4. tiny   rho shift, omega, resnorm = sqrt(rho) -> history, stop test
+//             np.all(resnorm <= criterion) -> ctrl.stop_at  cg.py:156,214-217
+// (+ with an attached communicator: one ncclAllReduce of the zero-padded
+//  residual-norm vector and a tiny global stop test.)
+#include "solver_common.hpp"
+
+using namespace kry;
+
+struct kry_cg {
+  kry_ctx *ctx = nullptr;
+  kry_csr *A = nullptr;
+  int64_t n = 0;
+  int k = 1;
+  int dtype = 0;
+  bool scalar_f32 = false;
+  void *b = nullptr, *x0 = nullptr, *y = nullptr, *r = nullptr, *p[2] = {nullptr, nullptr};
+  void *Ap = nullptr, *xk = nullptr, *rt = nullptr;
+  double *w = nullptr;
+  double *part = nullptr;  // 2 * kMaxGrid * k
+  double *scal = nullptr;  // scalar slots, see S_* below
+  double *hist = nullptr;  // chunk_cap * hist_k
+  Ctrl *ctrl = nullptr;
+  int chunk_cap = 0;
+  int64_t it = 0;
+  bool started = false;
+  // multi-GPU
+  kry_comm *comm = nullptr;
+  int col_offset = 0, total_k = 0;
+  double *gbuf = nullptr;  // total_k (allreduced residual norms)
+  double *gcrit = nullptr; // total_k
+};
+
+namespace {
+
+enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_COUNT = 6 };
+
+template <typename V>
+struct OpCgUpdate {
+  V *y, *r;
+  const V *p, *Ap;
+  const double *alpha;
+  const double *w;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V yv[W], rv[W], pv[W], av[W];
+    VIO<V>::load(y, e, N, yv);
+    VIO<V>::load(r, e, N, rv);
+    VIO<V>::load(p, e, N, pv);
+    VIO<V>::load(Ap, e, N, av);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V a = (V)alpha[(e + v) & (k - 1)];
+      const V t1 = a * pv[v];
+      yv[v] = yv[v] + t1;        // yk += alpha * p        (cg.py:196)
+      const V t2 = a * av[v];
+      rv[v] = rv[v] - t2;        // Ml_rk -= alpha * Ap    (cg.py:200)
+      if (e + v < N) {
+        const double rd = (double)rv[v];
+        acc[v] += w ? dterm_w(rd, w[(e + v) / k], rd) : dterm(rd, rd);
+      }
+    }
+    VIO<V>::store(y, e, N, yv);
+    VIO<V>::store(r, e, N, rv);
+  }
+};
+
+// rho0 = <r0, r0> -> rho slot (cg.py:116, 131).
+template <typename S>
+__global__ void cg_start_finalize(const double *part, int P, int k, double *scal) {
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S rho = (S)red[c];
+    scal[S_RHO * k + c] = (double)rho;
+    scal[S_RHO_PREV * k + c] = 0.0;
+    scal[S_OMEGA * k + c] = 0.0;
+    scal[S_TMP * k + c] = (double)rho;
+  }
+}
+
+// alpha = rhos[-1] / np.where(pAp != 0, pAp, 1.0)  (cg.py:183-185)
+template <typename S>
+__global__ void cg_alpha_kernel(const double *part, int P, int k, double *scal, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S pAp = (S)red[c];
+    const S rho = (S)scal[S_RHO * k + c];
+    scal[S_ALPHA * k + c] = (double)(rho / safe<S>(pAp));
+  }
+}
+
+// rhos = [rhos[-1], <r, r>]; omega for the next p-update; resnorm =
+// sqrt(<r, r>); global stop test (cg.py:209-217, 156, 177).
+template <typename S>
+__global__ void cg_rho_kernel(const double *part, int P, int k, double *scal, double *hist, Ctrl *ctrl,
+                              int step, double *gbuf, int col_offset, int total_k) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  __shared__ double rn[kMaxCols];
+  __shared__ int flag;
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S rr = (S)red[c];
+    const S old = (S)scal[S_RHO * k + c];
+    scal[S_RHO_PREV * k + c] = (double)old;
+    scal[S_RHO * k + c] = (double)rr;
+    scal[S_OMEGA * k + c] = (double)(rr / safe<S>(old));
+    const S nrm = sqrt(rr);
+    rn[c] = (double)nrm;
+    if (!gbuf) hist[(int64_t)step * k + c] = (double)nrm;
+  }
+  __syncthreads();
+  if (gbuf) {
+    // zero-padded residual-norm vector for the RCCL allreduce
+    for (int t = threadIdx.x; t < total_k; t += blockDim.x) {
+      const int lc = t - col_offset;
+      gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
+    }
+    return;
+  }
+  if (all_le(rn, scal + S_CRIT * k, k, &flag) && threadIdx.x == 0) ctrl->stop_at = step + 1;
+}
+
+// global stop test on the allreduced residual norms
+__global__ void cg_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
+                                int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ int flag;
+  for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
+  if (all_le(gbuf, gcrit, total_k, &flag) && threadIdx.x == 0) ctrl->stop_at = step + 1;
+}
+
+template <typename V, typename MV, typename I>
+void cg_start_impl(kry_cg *s) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const V *x0 = static_cast<const V *>(s->x0);
+  const int64_t N = s->n * (int64_t)k;
+  // r0 = b - A x0 (x0 = 0: r0 = b - A 0 evaluated the same way)
+  const V *src = x0;
+  if (!src) src = static_cast<const V *>(s->xk);  // zero-filled scratch
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->r), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  if (s->scalar_f32)
+    hipLaunchKernelGGL(cg_start_finalize<float>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
+  else
+    hipLaunchKernelGGL(cg_start_finalize<double>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
+  KRY_HIP(hipGetLastError());
+  (void)N;
+}
+
+template <typename V, typename MV, typename I>
+void cg_run_impl(kry_cg *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
+  for (int step = 0; step < max_steps; ++step) {
+    const int64_t i = s->it + step;
+    V *pcur = static_cast<V *>(s->p[i & 1]);
+    const V *pold = static_cast<const V *>(s->p[(i + 1) & 1]);
+    SrcCgP<V> src{static_cast<const V *>(s->r), pold, s->scal + S_OMEGA * k, k, i == 0 ? 1 : 0};
+    int PA, PB;
+    {
+      ProfScope ps(s->ctx, PROF_SPMV);
+      launch_spmv<V, MV, I>(s->A, k, src, EpiCgAp<V>{static_cast<V *>(s->Ap), pcur, src, s->w, k}, partA, &PA,
+                        s->ctrl, step, st);
+    }
+    if (s->scalar_f32)
+      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+    else
+      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+    {
+      ProfScope ps(s->ctx, PROF_UPDATE);
+      PB = launch_elementwise<V>(N, k,
+                                 OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), pcur,
+                                               static_cast<const V *>(s->Ap), s->scal + S_ALPHA * k, s->w, k},
+                                 partB, s->ctrl, step, st);
+    }
+    double *gb = s->comm ? s->gbuf : nullptr;
+    if (s->scalar_f32)
+      hipLaunchKernelGGL(cg_rho_kernel<float>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
+                         s->ctrl, step, gb, s->col_offset, s->total_k);
+    else
+      hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
+                         s->ctrl, step, gb, s->col_offset, s->total_k);
+    KRY_HIP(hipGetLastError());
+    if (s->comm) {
+      // exactly one collective per iteration: the residual-norm vector
+      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k, ncclDouble, ncclSum, s->comm->comm, st);
+      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      hipLaunchKernelGGL(cg_global_check, dim3(1), dim3(kBlock), 0, st, s->gbuf, s->gcrit, s->total_k, s->hist,
+                         s->ctrl, step);
+      KRY_HIP(hipGetLastError());
+    }
+  }
+}
+
+template <typename V, typename MV, typename I>
+void cg_residual_impl(kry_cg *s, double *norm2) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  launch_elementwise<V>(N, k, OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->y), static_cast<V *>(s->xk)},
+                        nullptr, nullptr, 0, st);
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  double *out = s->scal + S_TMP * k;
+  hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
+  KRY_HIP(hipGetLastError());
+  KRY_HIP(hipMemcpyAsync(norm2, out, k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+}
+
+}  // namespace
+
+#define KRY_API_BEGIN try {
+#define KRY_API_END                  \
+  return KRY_OK;                     \
+  }                                  \
+  catch (const kry::Error &e) {      \
+    kry::set_error(e.msg);           \
+    return e.code;                   \
+  }                                  \
+  catch (const std::exception &e) {  \
+    kry::set_error(e.what());        \
+    return KRY_EDEVICE;              \
+  }
+
+static void cg_free(kry_cg *s) {
+  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p[0], s->p[1], s->Ap, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
+                  s->ctrl, s->gbuf, s->gcrit};
+  for (void *b : bufs) dev_free(b);
+}
+
+extern "C" {
+
+int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(is_pow2(k) && k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_REQUIRE(dtype == A->dtype || (dtype == KRY_F64 && A->dtype == KRY_F32), KRY_EINVAL,
+              "vectors must have the operator dtype (or float64 over a float32 operator)");
+  KRY_HIP(hipSetDevice(ctx->device));
+  auto *s = new kry_cg();
+  try {
+    s->ctx = ctx;
+    s->A = A;
+    s->n = A->n;
+    s->k = k;
+    s->dtype = dtype;
+    const size_t vb = ((size_t)A->n * k + 15) / 16 * 16 * dsize(dtype);
+    void **vecs[] = {&s->b, &s->y, &s->r, &s->p[0], &s->p[1], &s->Ap, &s->xk, &s->rt};
+    for (void **v : vecs) {
+      *v = dev_alloc(vb);
+      KRY_HIP(hipMemsetAsync(*v, 0, vb, ctx->stream));
+    }
+    s->part = static_cast<double *>(dev_alloc(2 * (size_t)kMaxGrid * k * 8));
+    s->scal = static_cast<double *>(dev_alloc(S_COUNT * (size_t)k * 8));
+    KRY_HIP(hipMemsetAsync(s->scal, 0, S_COUNT * (size_t)k * 8, ctx->stream));
+    s->chunk_cap = 64;
+    s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * k * 8));
+    s->ctrl = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
+    reset_ctrl(s->ctrl, ctx->stream);
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    cg_free(s);
+    delete s;
+    throw;
+  }
+  *out = s;
+  KRY_API_END
+}
+
+int kry_cg_destroy(kry_cg *s) {
+  KRY_API_BEGIN
+  if (!s) return KRY_OK;
+  (void)hipSetDevice(s->ctx->device);
+  (void)hipStreamSynchronize(s->ctx->stream);
+  cg_free(s);
+  delete s;
+  KRY_API_END
+}
+
+int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && rho0, KRY_EINVAL, "null argument");
+  check_vec(b, s->n, s->k, s->dtype, "b");
+  if (x0) check_vec(x0, s->n, s->k, s->dtype, "x0");
+  check_weights(w, s->n);
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const size_t vb = b->bytes();
+  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  dev_free(s->x0);
+  s->x0 = nullptr;
+  if (x0) {
+    s->x0 = dev_alloc(((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype));
+    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+  }
+  dev_free(s->w);
+  s->w = nullptr;
+  if (w) {
+    s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
+    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+  }
+  // the inner product's dtype: float32 for an unweighted fp32 solve (np.dot of
+  // float32), float64 otherwise (weights are float64)
+  s->scalar_f32 = (s->dtype == KRY_F32 && !w);
+  KRY_HIP(hipMemsetAsync(s->y, 0, vb, st));
+  KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
+  s->it = 0;
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
+  // p0 = r0 is materialised by the first iteration's gather (first = 1)
+  KRY_HIP(hipMemcpyAsync(rho0, s->scal + S_TMP * s->k, s->k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  s->started = true;
+  KRY_API_END
+}
+
+int kry_cg_set_criterion(kry_cg *s, const double *criterion) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && criterion, KRY_EINVAL, "null argument");
+  hipStream_t st = s->ctx->stream;
+  if (s->comm) {
+    KRY_HIP(hipMemcpyAsync(s->gcrit, criterion, s->total_k * 8, hipMemcpyHostToDevice, st));
+  } else {
+    KRY_HIP(hipMemcpyAsync(s->scal + S_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, st));
+  }
+  KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnorms) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && steps_done && resnorms && max_steps >= 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_cg_start has not been called");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const int hk = s->comm ? s->total_k : s->k;
+  if (max_steps > s->chunk_cap) {
+    dev_free(s->hist);
+    s->hist = nullptr;
+    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * hk * 8));
+    s->chunk_cap = max_steps;
+  }
+  reset_ctrl(s->ctrl, st);
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  Ctrl c;
+  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
+  if (done > 0) {
+    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  }
+  s->it += done;
+  *steps_done = done;
+  KRY_API_END
+}
+
+int kry_cg_residual(kry_cg *s, double *norm2) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && norm2, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_cg_start has not been called");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_residual_impl<decltype(v0), decltype(m0), decltype(i0)>(s, norm2); });
+  KRY_API_END
+}
+
+int kry_cg_get(kry_cg *s, int which, void *host) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && host && (which == 0 || which == 1), KRY_EINVAL, "bad argument");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const size_t vb = (size_t)s->n * s->k * dsize(s->dtype);
+  const int64_t N = s->n * (int64_t)s->k;
+  if (which == 0) {
+    if (s->dtype == KRY_F64)
+      launch_elementwise<double>(N, s->k, OpXk<double>{static_cast<const double *>(s->x0), static_cast<const double *>(s->y), static_cast<double *>(s->xk)},
+                                 nullptr, nullptr, 0, st);
+    else
+      launch_elementwise<float>(N, s->k, OpXk<float>{static_cast<const float *>(s->x0), static_cast<const float *>(s->y), static_cast<float *>(s->xk)},
+                                nullptr, nullptr, 0, st);
+    KRY_HIP(hipMemcpyAsync(host, s->xk, vb, hipMemcpyDeviceToHost, st));
+  } else {
+    KRY_HIP(hipMemcpyAsync(host, s->r, vb, hipMemcpyDeviceToHost, st));
+  }
+  KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && c, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(col_offset >= 0 && total_k >= col_offset + s->k && total_k <= 4096, KRY_EINVAL,
+              "bad column range");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dev_free(s->gbuf);
+  dev_free(s->gcrit);
+  s->gbuf = nullptr;
+  s->gcrit = nullptr;
+  s->gbuf = static_cast<double *>(dev_alloc((size_t)total_k * 8));
+  s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
+  dev_free(s->hist);
+  s->hist = nullptr;
+  s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * total_k * 8));
+  s->comm = c;
+  s->col_offset = col_offset;
+  s->total_k = total_k;
+  KRY_API_END
+}
+
+}  // extern "C"

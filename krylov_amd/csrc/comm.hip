@@ -1,0 +1,92 @@
+// RCCL communicator for RHS-column sharding (one process per GPU over xGMI).
+#include <cstring>
+
+#include "solver_common.hpp"
+
+using namespace kry;
+
+#define KRY_API_BEGIN try {
+#define KRY_API_END                  \
+  return KRY_OK;                     \
+  }                                  \
+  catch (const kry::Error &e) {      \
+    kry::set_error(e.msg);           \
+    return e.code;                   \
+  }                                  \
+  catch (const std::exception &e) {  \
+    kry::set_error(e.what());        \
+    return KRY_EDEVICE;              \
+  }
+
+#define KRY_NCCL(call)                                                                         \
+  do {                                                                                         \
+    ncclResult_t r_ = (call);                                                                  \
+    if (r_ != ncclSuccess) throw Error{KRY_ECOMM, std::string(#call) + ": " + ncclGetErrorString(r_)}; \
+  } while (0)
+
+static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+
+extern "C" {
+
+int kry_comm_unique_id(void *id128) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(id128, KRY_EINVAL, "null id");
+  ncclUniqueId id;
+  KRY_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(id128, &id, sizeof(id));
+  KRY_API_END
+}
+
+int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id128, kry_comm **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && id128 && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, KRY_EINVAL, "bad rank / nranks");
+  KRY_HIP(hipSetDevice(ctx->device));
+  ncclUniqueId id;
+  std::memcpy(&id, id128, sizeof(id));
+  auto *c = new kry_comm();
+  c->ctx = ctx;
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    throw Error{KRY_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+  }
+  *out = c;
+  KRY_API_END
+}
+
+int kry_comm_destroy(kry_comm *c) {
+  KRY_API_BEGIN
+  if (!c) return KRY_OK;
+  (void)hipSetDevice(c->ctx->device);
+  (void)hipStreamSynchronize(c->ctx->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  dev_free(c->dbuf);
+  delete c;
+  KRY_API_END
+}
+
+// Host-side convenience: in-place sum over ranks of `count` doubles (setup-time
+// exchanges such as the initial residual norms; not used inside iterations).
+int kry_comm_allreduce(kry_comm *c, double *host, int32_t count) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(c && host && count >= 0, KRY_EINVAL, "bad argument");
+  if (count == 0) return KRY_OK;
+  KRY_HIP(hipSetDevice(c->ctx->device));
+  hipStream_t st = c->ctx->stream;
+  if (c->dbuf_len < count) {
+    dev_free(c->dbuf);
+    c->dbuf = nullptr;
+    c->dbuf = static_cast<double *>(dev_alloc((size_t)count * 8));
+    c->dbuf_len = count;
+  }
+  KRY_HIP(hipMemcpyAsync(c->dbuf, host, (size_t)count * 8, hipMemcpyHostToDevice, st));
+  KRY_NCCL(ncclAllReduce(c->dbuf, c->dbuf, count, ncclDouble, ncclSum, c->comm, st));
+  KRY_HIP(hipMemcpyAsync(host, c->dbuf, (size_t)count * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+}  // extern "C"

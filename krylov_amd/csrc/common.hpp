@@ -1,0 +1,98 @@
+// Shared device/host plumbing for libkrylov_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/krylov_hip.h"
+
+namespace kry {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kWave = 64;            // CDNA wavefront
+constexpr int kMaxGrid = 2048;       // persistent grid cap: 256 CUs x 8 blocks
+constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
+constexpr int kTileNnz = 2048;       // LDS product slots per SpMV tile
+constexpr int kTileRows = kBlock;    // rows per SpMV tile (one per thread)
+constexpr int kNumXcd = 8;
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string &msg);
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define KRY_HIP(call)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      throw ::kry::Error{e_ == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE, \
+                         std::string(#call) + ": " + hipGetErrorString(e_)};   \
+  } while (0)
+
+#define KRY_REQUIRE(cond, code, msg)                                           \
+  do {                                                                         \
+    if (!(cond)) throw ::kry::Error{(code), (msg)};                            \
+  } while (0)
+
+// ------------------------------------------------------------- scalars
+// Per-solve control word shared by every kernel of a chunk. Kernels of chunk
+// step s run only while s < stop_at; the finalize kernel that detects
+// convergence (or an invariant Krylov space) at step s sets stop_at = s + 1,
+// so the rest of step s completes and every later launch returns at its first
+// instruction (same stream => kernel boundaries order the stores).
+struct Ctrl {
+  int32_t stop_at;     // first chunk step that must not run (INT32_MAX = none)
+  int32_t invariant;   // Arnoldi / Lanczos invariant flag
+  int32_t status;      // device-detected error (KRY_ESINGULAR, ...)
+  int32_t pad;
+};
+
+// ---------------------------------------------------------- device utils
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  // Blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
+  // range of logical blocks so neighbouring tiles share one L2 (speed only).
+  const int q = nb / kNumXcd, r = nb % kNumXcd;
+  const int xcd = b % kNumXcd, idx = b / kNumXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// Deterministic in-block reduction of `vals` laid out as slots[p], p < nslot,
+// where slot p belongs to column (p % k) (k a power of two <= nslot). Leaves
+// column sums in slots[0..k). Fixed tree => bitwise reproducible.
+__device__ __forceinline__ void block_tree_reduce(double *slots, int nslot, int k) {
+  for (int s = nslot >> 1; s >= k; s >>= 1) {
+    __syncthreads();
+    for (int p = threadIdx.x; p < s; p += blockDim.x) slots[p] = slots[p] + slots[p + s];
+  }
+  __syncthreads();
+}
+
+template <typename V>
+struct Vec16;
+template <>
+struct Vec16<double> {
+  using T = double2;
+  static constexpr int W = 2;
+};
+template <>
+struct Vec16<float> {
+  using T = float4;
+  static constexpr int W = 4;
+};
+
+inline int grid_for(int64_t work_items, int per_block) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return (int)g;
+}
+
+inline bool is_pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
+
+}  // namespace kry

@@ -1,0 +1,599 @@
+// GMRES device loop (reference gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200,
+// M = Ml = Mr = I, which makes the P and V bases identical).
+//
+// One Arnoldi step k (sweeps = 1 for "mgs", K for "mgsK"):
+//   SpMV      w = A V_k, partial <V_0, w>                      arnoldi.py:176
+//   per sweep, per j = 0..k:
+//     tiny    alpha_j = reduce, h[j] += alpha_j                 arnoldi.py:160-161
+//     MGS     w -= alpha_j V_j, partial of the next inner product
+//             (<V_{j+1}, w>, or <V_0, w> for the next sweep, or <w, w>)
+//   tiny      h[k+1] = sqrt(<w, w>), invariant test, Givens QR update of the
+//             Hessenberg column, y update, resnorm = |y[k+1]|, stop test
+//             (arnoldi.py:185-189, gmres.py:206-221)
+//   normalise V_{k+1} = w / guard(h[k+1])                       arnoldi.py:191-196
+// All scalars stay on the device; the host sees the residual-norm history.
+#include "solver_common.hpp"
+
+using namespace kry;
+
+struct kry_gmres {
+  kry_ctx *ctx = nullptr;
+  kry_csr *A = nullptr;
+  int64_t n = 0;
+  int k = 1;
+  int dtype = 0;
+  int maxiter = 0;
+  int sweeps = 1;
+  size_t vstride = 0;  // elements per basis vector (padded)
+  void *b = nullptr, *x0 = nullptr, *V = nullptr, *wv = nullptr, *xk = nullptr, *rt = nullptr;
+  double *w = nullptr;
+  double *part = nullptr;
+  double *scal = nullptr;  // alpha[k], hsafe[k], crit[k], tmp[k]
+  double *h = nullptr;     // (maxiter + 2) x k, current Arnoldi column
+  double *R = nullptr;     // (maxiter + 1) x maxiter x k
+  double *y = nullptr;     // (maxiter + 1) x k
+  double *Gc = nullptr, *Gs = nullptr;  // maxiter x k rotations
+  double *yy = nullptr;    // maxiter x k triangular-solve result
+  double *hist = nullptr;
+  Ctrl *ctrl = nullptr;
+  int chunk_cap = 0;
+  int steps = 0;           // Arnoldi iterations done (arnoldi.iter)
+  bool invariant = false;
+  bool started = false;
+  bool have_solution = false;
+};
+
+namespace {
+
+enum { G_ALPHA = 0, G_HSAFE = 1, G_CRIT = 2, G_TMP = 3, G_COUNT = 4 };
+
+template <typename V>
+__host__ __device__ __forceinline__ V *basis(void *Vb, size_t stride, int i) {
+  return static_cast<V *>(Vb) + stride * (size_t)i;
+}
+
+template <typename V>
+struct OpMgs {
+  V *w;
+  const V *Vj;
+  const V *q;  // next inner-product partner, or null for <w, w>
+  const double *alpha;
+  const double *wt;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V wv[W], vj[W], qv[W];
+    VIO<V>::load(w, e, N, wv);
+    VIO<V>::load(Vj, e, N, vj);
+    if (q) VIO<V>::load(q, e, N, qv);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V t = (V)alpha[(e + v) & (k - 1)] * vj[v];
+      wv[v] = wv[v] - t;  // Av -= alpha * P[j]   (arnoldi.py:162)
+      if (e + v < N) {
+        const double a = q ? (double)qv[v] : (double)wv[v];
+        const double b = (double)wv[v];
+        acc[v] += wt ? dterm_w(a, wt[(e + v) / k], b) : dterm(a, b);
+      }
+    }
+    VIO<V>::store(w, e, N, wv);
+  }
+};
+
+// out = src / hsafe  (arnoldi.py:193-195, the guarded normalisation)
+template <typename V>
+struct OpScaleDiv {
+  const V *src;
+  V *dst;
+  const double *hsafe;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V a[W];
+    VIO<V>::load(src, e, N, a);
+#pragma unroll
+    for (int v = 0; v < W; ++v) a[v] = a[v] / (V)hsafe[(e + v) & (k - 1)];
+    VIO<V>::store(dst, e, N, a);
+  }
+};
+
+// xk = x0 + sum_i yy_i V_i, summed left to right from 0 (gmres.py:97-98)
+template <typename V>
+struct OpBasisCombo {
+  const V *Vb;
+  size_t stride;
+  int m;
+  const double *yy;
+  const V *x0;
+  V *xk;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V acc[W], t[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc[v] = V(0);
+    for (int i = 0; i < m; ++i) {
+      VIO<V>::load(Vb + stride * (size_t)i, e, N, t);
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V p = (V)yy[(int64_t)i * k + ((e + v) & (k - 1))] * t[v];
+        acc[v] = acc[v] + p;
+      }
+    }
+    if (x0) {
+      VIO<V>::load(x0, e, N, t);
+    } else {
+#pragma unroll
+      for (int v = 0; v < W; ++v) t[v] = V(0);
+    }
+#pragma unroll
+    for (int v = 0; v < W; ++v) t[v] = t[v] + acc[v];
+    VIO<V>::store(xk, e, N, t);
+  }
+};
+
+// ||r0|| -> y[0], hsafe (for V_0 = r0 / guard(||r0||)), tmp (host copy)
+template <typename S>
+__global__ void gm_start_finalize(const double *part, int P, int k, double *scal, double *y) {
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S nrm = sqrt((S)red[c]);
+    y[c] = (double)nrm;
+    scal[G_HSAFE * k + c] = (double)safe<S>(nrm);
+    scal[G_TMP * k + c] = (double)nrm;
+  }
+}
+
+// alpha_j = <V_j, w>; h[j] += alpha_j   (h[j] starts at 0.0 each step)
+template <typename S>
+__global__ void gm_coef_kernel(const double *part, int P, int k, double *scal, double *h, int j, int first_sweep,
+                               const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S a = (S)red[c];
+    scal[G_ALPHA * k + c] = (double)a;
+    const S prev = first_sweep ? S(0) : (S)h[(int64_t)j * k + c];
+    h[(int64_t)j * k + c] = (double)(prev + a);
+  }
+}
+
+// h[k+1] = sqrt(<w, w>); invariance; Givens update of column `col`
+// (gmres.py:206-221); resnorm |y[col+1]|; stop test.
+template <typename S>
+__global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, double *h, double *R, double *y,
+                             double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  __shared__ double rn[kMaxCols];
+  __shared__ int flag;
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  const int64_t ld = (int64_t)maxiter * k;  // R row stride
+  if (c < k) {
+    const S hk1 = sqrt((S)red[c]);
+    h[(int64_t)(col + 1) * k + c] = (double)hk1;
+    red[c] = (double)hk1;
+  }
+  __syncthreads();
+  // np.all(h[k+1] <= 1e-14) over the columns (arnoldi.py:187)
+  if (threadIdx.x == 0) flag = 1;
+  __syncthreads();
+  if (c < k && !(red[c] <= 1.0e-14)) flag = 0;
+  __syncthreads();
+  const bool inv = flag != 0;
+  __syncthreads();
+  if (c < k) {
+    const S hk1 = (S)red[c];
+    scal[G_HSAFE * k + c] = (double)safe<S>(hk1);
+    // R[:col+2, col] = h[:col+2]
+    for (int i = 0; i < col + 2; ++i) R[i * ld + (int64_t)col * k + c] = h[(int64_t)i * k + c];
+    // apply the previous rotations
+    for (int i = 0; i < col; ++i) {
+      const S cc = (S)Gc[(int64_t)i * k + c], ss = (S)Gs[(int64_t)i * k + c];
+      const S r0 = (S)R[i * ld + (int64_t)col * k + c], r1 = (S)R[(i + 1) * ld + (int64_t)col * k + c];
+      const S a0 = cc * r0, a1 = ss * r1;
+      const S b0 = -ss * r0, b1 = cc * r1;
+      R[i * ld + (int64_t)col * k + c] = (double)(a0 + a1);
+      R[(i + 1) * ld + (int64_t)col * k + c] = (double)(b0 + b1);
+    }
+    S cs, sn, rr;
+    lartg<S>((S)R[col * ld + (int64_t)col * k + c], (S)R[(col + 1) * ld + (int64_t)col * k + c], cs, sn, rr);
+    Gc[(int64_t)col * k + c] = (double)cs;
+    Gs[(int64_t)col * k + c] = (double)sn;
+    R[col * ld + (int64_t)col * k + c] = (double)rr;
+    R[(col + 1) * ld + (int64_t)col * k + c] = 0.0;
+    const S y0 = (S)y[(int64_t)col * k + c], y1 = (S)y[(int64_t)(col + 1) * k + c];
+    const S a0 = cs * y0, a1 = sn * y1;
+    const S b0 = -sn * y0, b1 = cs * y1;
+    const S ny1 = b0 + b1;
+    y[(int64_t)col * k + c] = (double)(a0 + a1);
+    y[(int64_t)(col + 1) * k + c] = (double)ny1;
+    rn[c] = (double)fabs(ny1);
+    hist[(int64_t)step * k + c] = rn[c];
+  }
+  __syncthreads();
+  const bool conv = all_le(rn, scal + G_CRIT * k, k, &flag);
+  if (threadIdx.x == 0) {
+    if (inv) ctrl->invariant = 1;
+    if (inv || conv) ctrl->stop_at = step + 1;
+  }
+}
+
+// yy = R[:m,:m]^-1 y[:m] per column (gmres.py:24-38; LAPACK ?trtrs semantics:
+// zero rhs -> 0, non-finite input -> error, zero diagonal -> singular).
+template <typename S>
+__global__ void gm_trsv_kernel(const double *R, const double *y, double *yy, int m, int k, int maxiter,
+                               Ctrl *ctrl) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k) return;
+  const int64_t ld = (int64_t)maxiter * k;
+  bool allzero = true;
+  for (int i = 0; i < m; ++i) allzero = allzero && (y[(int64_t)i * k + c] == 0.0);
+  if (allzero) {
+    for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = 0.0;
+    return;
+  }
+  bool finite = true;
+  for (int i = 0; i < m; ++i) {
+    finite = finite && isfinite(y[(int64_t)i * k + c]);
+    for (int j = 0; j < m; ++j) finite = finite && isfinite(R[i * ld + (int64_t)j * k + c]);
+  }
+  if (!finite) {
+    ctrl->status = KRY_ENONFINITE;
+    return;
+  }
+  for (int i = 0; i < m; ++i)
+    if (R[i * ld + (int64_t)i * k + c] == 0.0) {
+      ctrl->status = KRY_ESINGULAR;
+      return;
+    }
+  S x[64];
+  // column-oriented back substitution (reference BLAS xTRSV 'U','N','N')
+  for (int i = 0; i < m; ++i) x[i] = (S)y[(int64_t)i * k + c];
+  for (int j = m - 1; j >= 0; --j) {
+    if (x[j] != S(0)) {
+      x[j] = x[j] / (S)R[j * ld + (int64_t)j * k + c];
+      const S t = x[j];
+      for (int i = j - 1; i >= 0; --i) {
+        const S p = t * (S)R[i * ld + (int64_t)j * k + c];
+        x[i] = x[i] - p;
+      }
+    }
+  }
+  for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = (double)x[i];
+}
+
+// Larger triangular systems: same algorithm, solution kept in global memory.
+template <typename S>
+__global__ void gm_trsv_big_kernel(const double *R, const double *y, double *yy, int m, int k, int maxiter,
+                                   Ctrl *ctrl) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k) return;
+  const int64_t ld = (int64_t)maxiter * k;
+  bool allzero = true;
+  for (int i = 0; i < m; ++i) allzero = allzero && (y[(int64_t)i * k + c] == 0.0);
+  if (allzero) {
+    for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = 0.0;
+    return;
+  }
+  bool finite = true;
+  for (int i = 0; i < m; ++i) {
+    finite = finite && isfinite(y[(int64_t)i * k + c]);
+    for (int j = 0; j < m; ++j) finite = finite && isfinite(R[i * ld + (int64_t)j * k + c]);
+  }
+  if (!finite) {
+    ctrl->status = KRY_ENONFINITE;
+    return;
+  }
+  for (int i = 0; i < m; ++i)
+    if (R[i * ld + (int64_t)i * k + c] == 0.0) {
+      ctrl->status = KRY_ESINGULAR;
+      return;
+    }
+  for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = (double)(S)y[(int64_t)i * k + c];
+  for (int j = m - 1; j >= 0; --j) {
+    S xj = (S)yy[(int64_t)j * k + c];
+    if (xj != S(0)) {
+      xj = xj / (S)R[j * ld + (int64_t)j * k + c];
+      yy[(int64_t)j * k + c] = (double)xj;
+      for (int i = j - 1; i >= 0; --i) {
+        const S p = xj * (S)R[i * ld + (int64_t)j * k + c];
+        yy[(int64_t)i * k + c] = (double)((S)yy[(int64_t)i * k + c] - p);
+      }
+    }
+  }
+}
+
+template <typename V, typename MV, typename I>
+void gm_start_impl(kry_gmres *s) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  const V *src = s->x0 ? static_cast<const V *>(s->x0) : static_cast<const V *>(s->xk);  // xk zero-filled
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->wv), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  hipLaunchKernelGGL(gm_start_finalize<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->y);
+  KRY_HIP(hipGetLastError());
+  launch_elementwise<V>(N, k,
+                        OpScaleDiv<V>{static_cast<const V *>(s->wv), static_cast<V *>(s->V), s->scal + G_HSAFE * k, k},
+                        nullptr, nullptr, 0, st);
+}
+
+template <typename V, typename MV, typename I>
+void gm_run_impl(kry_gmres *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  V *w = static_cast<V *>(s->wv);
+  for (int step = 0; step < max_steps; ++step) {
+    const int col = s->steps + step;
+    if (col >= s->maxiter) break;
+    const V *Vk = basis<V>(s->V, s->vstride, col);
+    const V *V0 = basis<V>(s->V, s->vstride, 0);
+    int P;
+    {
+      ProfScope ps(s->ctx, PROF_SPMV);
+      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{Vk, k}, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step, st);
+    }
+    for (int sw = 0; sw < s->sweeps; ++sw) {
+      for (int j = 0; j <= col; ++j) {
+        hipLaunchKernelGGL(gm_coef_kernel<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->h, j,
+                           sw == 0 ? 1 : 0, s->ctrl, step);
+        const V *Vj = basis<V>(s->V, s->vstride, j);
+        const V *q = j < col ? basis<V>(s->V, s->vstride, j + 1) : (sw + 1 < s->sweeps ? V0 : nullptr);
+        ProfScope ps(s->ctx, PROF_MGS);
+        P = launch_elementwise<V>(N, k, OpMgs<V>{w, Vj, q, s->scal + G_ALPHA * k, s->w, k}, s->part, s->ctrl, step,
+                                  st);
+      }
+    }
+    hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->h, s->R, s->y,
+                       s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
+    KRY_HIP(hipGetLastError());
+    // V_{col+1} = w / guard(h[col+1]) unless invariant; the kernel runs for
+    // this step even when the QR kernel just raised stop_at to step + 1.
+    launch_elementwise<V>(N, k,
+                          OpScaleDiv<V>{w, basis<V>(s->V, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
+                          nullptr, s->ctrl, step, st);
+  }
+}
+
+template <typename V, typename MV, typename I>
+void gm_solution_impl(kry_gmres *s) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k, m = s->steps;
+  const int64_t N = s->n * (int64_t)k;
+  if (m > 0) {
+    const int g = (k + kBlock - 1) / kBlock;
+    if (m <= 64)
+      hipLaunchKernelGGL(gm_trsv_kernel<V>, dim3(g), dim3(kBlock), 0, st, s->R, s->y, s->yy, m, k, s->maxiter, s->ctrl);
+    else
+      hipLaunchKernelGGL(gm_trsv_big_kernel<V>, dim3(g), dim3(kBlock), 0, st, s->R, s->y, s->yy, m, k, s->maxiter,
+                         s->ctrl);
+    KRY_HIP(hipGetLastError());
+  }
+  launch_elementwise<V>(N, k,
+                        OpBasisCombo<V>{static_cast<const V *>(s->V), s->vstride, m, s->yy,
+                                        static_cast<const V *>(s->x0), static_cast<V *>(s->xk), k},
+                        nullptr, nullptr, 0, st);
+}
+
+template <typename V, typename MV, typename I>
+void gm_residual_impl(kry_gmres *s, double *norm2) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  double *out = s->scal + G_TMP * k;
+  hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
+  KRY_HIP(hipGetLastError());
+  KRY_HIP(hipMemcpyAsync(norm2, out, k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+}
+
+void gm_free(kry_gmres *s) {
+  void *bufs[] = {s->b, s->x0, s->V, s->wv, s->xk, s->rt, s->w, s->part, s->scal, s->h, s->R, s->y,
+                  s->Gc, s->Gs, s->yy, s->hist, s->ctrl};
+  for (void *b : bufs) dev_free(b);
+}
+
+}  // namespace
+
+#define KRY_API_BEGIN try {
+#define KRY_API_END                  \
+  return KRY_OK;                     \
+  }                                  \
+  catch (const kry::Error &e) {      \
+    kry::set_error(e.msg);           \
+    return e.code;                   \
+  }                                  \
+  catch (const std::exception &e) {  \
+    kry::set_error(e.what());        \
+    return KRY_EDEVICE;              \
+  }
+
+extern "C" {
+
+int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t maxiter, int32_t sweeps,
+                     kry_gmres **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(is_pow2(k) && k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_REQUIRE(dtype == A->dtype || (dtype == KRY_F64 && A->dtype == KRY_F32), KRY_EINVAL,
+              "vectors must have the operator dtype (or float64 over a float32 operator)");
+  KRY_REQUIRE(maxiter >= 0 && sweeps >= 1, KRY_EINVAL, "bad maxiter / sweeps");
+  KRY_HIP(hipSetDevice(ctx->device));
+  auto *s = new kry_gmres();
+  try {
+    s->ctx = ctx;
+    s->A = A;
+    s->n = A->n;
+    s->k = k;
+    s->dtype = dtype;
+    s->maxiter = maxiter;
+    s->sweeps = sweeps;
+    s->vstride = ((size_t)A->n * k + 15) / 16 * 16;
+    const size_t vb = s->vstride * dsize(dtype);
+    s->b = dev_alloc(vb);
+    s->wv = dev_alloc(vb);
+    s->xk = dev_alloc(vb);
+    s->rt = dev_alloc(vb);
+    s->V = dev_alloc(vb * ((size_t)maxiter + 1));
+    KRY_HIP(hipMemsetAsync(s->xk, 0, vb, ctx->stream));
+    KRY_HIP(hipMemsetAsync(s->wv, 0, vb, ctx->stream));
+    s->part = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
+    s->scal = static_cast<double *>(dev_alloc(G_COUNT * (size_t)k * 8));
+    s->h = static_cast<double *>(dev_alloc(((size_t)maxiter + 2) * k * 8));
+    s->R = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8));
+    s->y = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
+    s->Gc = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
+    s->Gs = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
+    s->yy = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
+    s->chunk_cap = 64;
+    s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * k * 8));
+    s->ctrl = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    gm_free(s);
+    delete s;
+    throw;
+  }
+  *out = s;
+  KRY_API_END
+}
+
+int kry_gmres_destroy(kry_gmres *s) {
+  KRY_API_BEGIN
+  if (!s) return KRY_OK;
+  (void)hipSetDevice(s->ctx->device);
+  (void)hipStreamSynchronize(s->ctx->stream);
+  gm_free(s);
+  delete s;
+  KRY_API_END
+}
+
+int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && r0norm, KRY_EINVAL, "null argument");
+  check_vec(b, s->n, s->k, s->dtype, "b");
+  if (x0) check_vec(x0, s->n, s->k, s->dtype, "x0");
+  check_weights(w, s->n);
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const size_t vb = b->bytes();
+  const int k = s->k;
+  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  dev_free(s->x0);
+  s->x0 = nullptr;
+  if (x0) {
+    s->x0 = dev_alloc(s->vstride * dsize(s->dtype));
+    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+  }
+  dev_free(s->w);
+  s->w = nullptr;
+  if (w) {
+    s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
+    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+  }
+  const size_t m1 = (size_t)s->maxiter + 1;
+  KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
+  KRY_HIP(hipMemsetAsync(s->R, 0, m1 * (s->maxiter > 0 ? s->maxiter : 1) * k * 8, st));
+  KRY_HIP(hipMemsetAsync(s->y, 0, m1 * k * 8, st));
+  KRY_HIP(hipMemsetAsync(s->h, 0, (m1 + 1) * k * 8, st));
+  KRY_HIP(hipMemsetAsync(s->yy, 0, m1 * k * 8, st));
+  reset_ctrl(s->ctrl, st);
+  s->steps = 0;
+  s->invariant = false;
+  s->have_solution = false;
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
+  KRY_HIP(hipMemcpyAsync(r0norm, s->scal + G_TMP * k, k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  s->started = true;
+  KRY_API_END
+}
+
+int kry_gmres_set_criterion(kry_gmres *s, const double *criterion) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && criterion, KRY_EINVAL, "null argument");
+  KRY_HIP(hipMemcpyAsync(s->scal + G_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  KRY_API_END
+}
+
+int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *resnorms, int32_t *invariant) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && steps_done && resnorms && invariant && max_steps >= 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_gmres_start has not been called");
+  if (s->invariant)
+    throw Error{KRY_EINVARIANT, "Krylov subspace was found to be invariant in the previous iteration."};
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  if (max_steps > s->maxiter - s->steps) max_steps = s->maxiter - s->steps;
+  if (max_steps > s->chunk_cap) {
+    dev_free(s->hist);
+    s->hist = nullptr;
+    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
+    s->chunk_cap = max_steps;
+  }
+  reset_ctrl(s->ctrl, st);
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  Ctrl c;
+  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
+  if (done > 0) {
+    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * s->k * 8, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  }
+  s->steps += done;
+  s->invariant = c.invariant != 0;
+  s->have_solution = false;
+  *steps_done = done;
+  *invariant = s->invariant ? 1 : 0;
+  KRY_API_END
+}
+
+int kry_gmres_solution(kry_gmres *s) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && s->started, KRY_EINVAL, "solver not started");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  reset_ctrl(s->ctrl, st);
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_solution_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
+  Ctrl c;
+  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  if (c.status == KRY_ESINGULAR) throw Error{KRY_ESINGULAR, "singular matrix: resolution failed at a zero diagonal"};
+  if (c.status == KRY_ENONFINITE) throw Error{KRY_ENONFINITE, "array must not contain infs or NaNs"};
+  s->have_solution = true;
+  KRY_API_END
+}
+
+int kry_gmres_residual(kry_gmres *s, double *norm2) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && norm2, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_residual_impl<decltype(v0), decltype(m0), decltype(i0)>(s, norm2); });
+  KRY_API_END
+}
+
+int kry_gmres_get(kry_gmres *s, int which, void *host) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && host && which == 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)s->n * s->k * dsize(s->dtype), hipMemcpyDeviceToHost, s->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  KRY_API_END
+}
+
+}  // extern "C"

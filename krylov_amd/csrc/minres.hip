@@ -1,0 +1,485 @@
+// MINRES device loop (reference minres.py:28-253 with the Lanczos process of
+// arnoldi.py:203-281, M = Ml = Mr = I).
+//
+// One iteration = five launches, no host sync:
+//   SpMV   w = A v - h0 p_old, partial <v, w>             arnoldi.py:244-252
+//   tiny   alpha = <v, w>, h[1] = alpha                   arnoldi.py:252-264
+//   ortho  w -= alpha p, partial <w, w>                   arnoldi.py:264-267
+//   tiny   h[2] = sqrt(<w, w>), invariance, the two old rotations and the new
+//          one on R (float64), y update, resnorm = |y1|, stop test
+//                                                        minres.py:193-228
+//   update z = (v - R0 W0 - R1 W1) / guard(R2), W shift, yk += y0 z,
+//          p_old <- p, p = v = w / guard(h[2])           minres.py:219-221,
+//                                                        arnoldi.py:274-277
+// Precision follows the reference under NumPy-2 promotion: Lanczos scalars
+// in the vector dtype, the inner products in the inner's dtype, R / rotations
+// / y / z / W in float64 (minres.py:195, 219).
+#include "solver_common.hpp"
+
+using namespace kry;
+
+struct kry_minres {
+  kry_ctx *ctx = nullptr;
+  kry_csr *A = nullptr;
+  int64_t n = 0;
+  int k = 1;
+  int dtype = 0;
+  bool inner_f32 = false;  // inner products in float32 (unweighted fp32)
+  void *b = nullptr, *x0 = nullptr, *yk = nullptr, *wv = nullptr, *xk = nullptr, *rt = nullptr;
+  void *P[3] = {nullptr, nullptr, nullptr};  // ring: p_old, p (= v), p_new
+  double *W[2] = {nullptr, nullptr};         // float64 W ring
+  double *w = nullptr;
+  double *part = nullptr;
+  double *scal = nullptr;
+  double *hist = nullptr;
+  Ctrl *ctrl = nullptr;
+  int chunk_cap = 0;
+  int64_t it = 0;
+  int wflip = 0;
+  bool invariant = false;
+  bool started = false;
+};
+
+namespace {
+
+// scalar slots (x k each)
+enum {
+  M_H0 = 0, M_H1, M_H2, M_HSAFE, M_ALPHA, M_Y0, M_Y1, M_G0C, M_G0S, M_G1C, M_G1S,
+  M_Z0, M_Z1, M_Z2, M_ZY, M_CRIT, M_TMP, M_COUNT
+};
+
+template <typename V, typename S>
+struct OpLanczosOrtho {
+  V *w;
+  const V *p;
+  const double *alpha;
+  const double *wt;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V wv[W], pv[W];
+    VIO<V>::load(w, e, N, wv);
+    VIO<V>::load(p, e, N, pv);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const S a = (S)alpha[(e + v) & (k - 1)];
+      const S t = a * (S)pv[v];
+      wv[v] = (V)((S)wv[v] - t);  // Av -= alpha * p   (arnoldi.py:264)
+      if (e + v < N) {
+        const double d = (double)wv[v];
+        acc[v] += wt ? dterm_w(d, wt[(e + v) / k], d) : dterm(d, d);
+      }
+    }
+    VIO<V>::store(w, e, N, wv);
+  }
+};
+
+template <typename V>
+struct OpMinresUpdate {
+  const V *vold;   // the v this step multiplied (minres.py:187)
+  const double *W0;
+  double *W1z;     // holds W[0] on entry; receives z (becomes the new W[1])
+  const double *W1;
+  V *yk;
+  const V *wv;
+  V *pnew;         // null when the space is invariant
+  const double *scal;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V va[W], ya[W], wa[W];
+    VIO<V>::load(vold, e, N, va);
+    VIO<V>::load(yk, e, N, ya);
+    if (pnew) VIO<V>::load(wv, e, N, wa);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      if (e + v >= N) continue;
+      const int c = (int)((e + v) & (k - 1));
+      const double r0 = scal[M_Z0 * k + c], r1 = scal[M_Z1 * k + c], r2 = scal[M_Z2 * k + c];
+      const double y0 = scal[M_ZY * k + c];
+      const double t0 = r0 * W0[e + v];
+      const double t1 = r1 * W1[e + v];
+      const double z = (((double)va[v] - t0) - t1) / r2;  // minres.py:219
+      W1z[e + v] = z;
+      const double dy = y0 * z;
+      ya[v] = (V)((double)ya[v] + dy);                     // minres.py:221
+      if (pnew) wa[v] = wa[v] / (V)scal[M_HSAFE * k + c]; // arnoldi.py:276-277
+    }
+    VIO<V>::store(yk, e, N, ya);
+    if (pnew) VIO<V>::store(pnew, e, N, wa);
+  }
+};
+
+template <typename V>
+struct OpDivInto {
+  const V *src;
+  V *dst;
+  const double *den;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V a[W];
+    VIO<V>::load(src, e, N, a);
+#pragma unroll
+    for (int v = 0; v < W; ++v) a[v] = a[v] / (V)den[(e + v) & (k - 1)];
+    VIO<V>::store(dst, e, N, a);
+  }
+};
+
+// ||r0|| (inner dtype S), y = [||r0||, 0], Lanczos scale guard.
+template <typename V, typename S>
+__global__ void mr_start_finalize(const double *part, int P, int k, double *scal) {
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S nrm = sqrt((S)red[c]);
+    scal[M_TMP * k + c] = (double)nrm;
+    scal[M_Y0 * k + c] = (double)nrm;
+    scal[M_Y1 * k + c] = 0.0;
+    scal[M_HSAFE * k + c] = (double)(nrm != S(0) ? nrm : S(1));
+    for (int s = M_H0; s <= M_H2; ++s) scal[s * k + c] = 0.0;
+  }
+}
+
+template <typename V, typename S>
+__global__ void mr_alpha_kernel(const double *part, int P, int k, double *scal, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const S a = (S)red[c];
+    scal[M_ALPHA * k + c] = (double)a;
+    scal[M_H1 * k + c] = (double)(V)a;  // h stored in the Lanczos dtype
+  }
+}
+
+template <typename V, typename S>
+__global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int have_g0, int have_g1, double *hist,
+                             Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  __shared__ double rn[kMaxCols];
+  __shared__ int flag;
+  reduce_partials(part, P, k, red);
+  const int c = threadIdx.x;
+  if (c < k) {
+    const V h2 = (V)sqrt((S)red[c]);
+    scal[M_H2 * k + c] = (double)h2;
+    red[c] = (double)h2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flag = 1;
+  __syncthreads();
+  if (c < k && !(red[c] <= 1.0e-14)) flag = 0;  // np.all(h[2] <= 1e-14)
+  __syncthreads();
+  const bool inv = flag != 0;
+  __syncthreads();
+  if (c < k) {
+    const V h2 = (V)scal[M_H2 * k + c];
+    scal[M_HSAFE * k + c] = (double)(h2 != V(0) ? h2 : V(1));
+    double R0 = 0.0, R1 = scal[M_H0 * k + c], R2, R3;
+    if (have_g1) {
+      const double cc = scal[M_G1C * k + c], ss = scal[M_G1S * k + c];
+      const double a0 = cc * R0, a1 = ss * R1, b0 = -ss * R0, b1 = cc * R1;
+      R0 = a0 + a1;
+      R1 = b0 + b1;
+    }
+    R2 = scal[M_H1 * k + c];
+    R3 = (double)h2;
+    if (have_g0) {
+      const double cc = scal[M_G0C * k + c], ss = scal[M_G0S * k + c];
+      const double a0 = cc * R1, a1 = ss * R2, b0 = -ss * R1, b1 = cc * R2;
+      R1 = a0 + a1;
+      R2 = b0 + b1;
+      scal[M_G1C * k + c] = cc;
+      scal[M_G1S * k + c] = ss;
+    }
+    double cs, sn, rr;
+    lartg<double>(R2, R3, cs, sn, rr);
+    scal[M_G0C * k + c] = cs;
+    scal[M_G0S * k + c] = sn;
+    R2 = rr;
+    const double y0 = scal[M_Y0 * k + c], y1 = scal[M_Y1 * k + c];
+    const double a0 = cs * y0, a1 = sn * y1, b0 = -sn * y0, b1 = cs * y1;
+    const double ny0 = a0 + a1, ny1 = b0 + b1;
+    scal[M_Z0 * k + c] = R0;
+    scal[M_Z1 * k + c] = R1;
+    scal[M_Z2 * k + c] = R2 != 0.0 ? R2 : 1.0;
+    scal[M_ZY * k + c] = ny0;
+    scal[M_Y0 * k + c] = ny1;  // y = [y[1], 0]
+    scal[M_Y1 * k + c] = 0.0;
+    // next step's h[0] = this step's h[2] (arnoldi.py:246-247)
+    scal[M_H0 * k + c] = (double)h2;
+    rn[c] = fabs(ny1);
+    hist[(int64_t)step * k + c] = rn[c];
+  }
+  __syncthreads();
+  const bool conv = all_le(rn, scal + M_CRIT * k, k, &flag);
+  if (threadIdx.x == 0) {
+    if (inv) ctrl->invariant = 1;
+    if (inv || conv) ctrl->stop_at = step + 1;
+  }
+}
+
+template <typename V, typename MV, typename I>
+void mr_start_impl(kry_minres *s) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  const V *src = s->x0 ? static_cast<const V *>(s->x0) : static_cast<const V *>(s->xk);
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->wv), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  if (s->inner_f32)
+    hipLaunchKernelGGL((mr_start_finalize<V, float>), dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
+  else
+    hipLaunchKernelGGL((mr_start_finalize<V, double>), dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
+  KRY_HIP(hipGetLastError());
+  // p = v = r0 / guard(||r0||) (arnoldi.py:480-481 analogue, ArnoldiLanczos.__init__)
+  launch_elementwise<V>(N, k, OpDivInto<V>{static_cast<const V *>(s->wv), static_cast<V *>(s->P[0]), s->scal + M_HSAFE * k, k},
+                        nullptr, nullptr, 0, st);
+}
+
+template <typename V, typename S, typename MV, typename I>
+void mr_run_typed(kry_minres *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  V *w = static_cast<V *>(s->wv);
+  double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
+  for (int step = 0; step < max_steps; ++step) {
+    const int64_t i = s->it + step;
+    const V *v = static_cast<const V *>(s->P[i % 3]);
+    const V *pold = i > 0 ? static_cast<const V *>(s->P[(i + 2) % 3]) : nullptr;
+    V *pnew = static_cast<V *>(s->P[(i + 1) % 3]);
+    int PA, PB;
+    {
+      ProfScope ps(s->ctx, PROF_SPMV);
+      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{v, k}, EpiLanczos<V>{w, v, pold, s->scal + M_H0 * k, s->w, k}, partA,
+                        &PA, s->ctrl, step, st);
+    }
+    hipLaunchKernelGGL((mr_alpha_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+    PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, v, s->scal + M_ALPHA * k, s->w, k}, partB, s->ctrl,
+                               step, st);
+    hipLaunchKernelGGL((mr_qr_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, i >= 1 ? 1 : 0,
+                       i >= 2 ? 1 : 0, s->hist, s->ctrl, step);
+    KRY_HIP(hipGetLastError());
+    const int f = (s->wflip + step) & 1;
+    {
+      ProfScope ps(s->ctx, PROF_UPDATE);
+      launch_elementwise<V>(N, k,
+                            OpMinresUpdate<V>{v, s->W[f], s->W[f], s->W[f ^ 1], static_cast<V *>(s->yk), w, pnew,
+                                              s->scal, k},
+                            nullptr, s->ctrl, step, st);
+    }
+  }
+}
+
+template <typename V, typename MV, typename I>
+void mr_run_impl(kry_minres *s, int max_steps) {
+  if (s->inner_f32)
+    mr_run_typed<V, float, MV, I>(s, max_steps);
+  else
+    mr_run_typed<V, double, MV, I>(s, max_steps);
+}
+
+template <typename V, typename MV, typename I>
+void mr_residual_impl(kry_minres *s, double *norm2) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  launch_elementwise<V>(N, k, OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->yk), static_cast<V *>(s->xk)},
+                        nullptr, nullptr, 0, st);
+  int P;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
+                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
+                    nullptr, 0, st);
+  double *out = s->scal + M_TMP * k;
+  hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
+  KRY_HIP(hipGetLastError());
+  KRY_HIP(hipMemcpyAsync(norm2, out, k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+}
+
+void mr_free(kry_minres *s) {
+  void *bufs[] = {s->b, s->x0, s->yk, s->wv, s->xk, s->rt, s->P[0], s->P[1], s->P[2], s->W[0], s->W[1],
+                  s->w, s->part, s->scal, s->hist, s->ctrl};
+  for (void *b : bufs) dev_free(b);
+}
+
+}  // namespace
+
+#define KRY_API_BEGIN try {
+#define KRY_API_END                  \
+  return KRY_OK;                     \
+  }                                  \
+  catch (const kry::Error &e) {      \
+    kry::set_error(e.msg);           \
+    return e.code;                   \
+  }                                  \
+  catch (const std::exception &e) {  \
+    kry::set_error(e.what());        \
+    return KRY_EDEVICE;              \
+  }
+
+extern "C" {
+
+int kry_minres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_minres **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && out, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(is_pow2(k) && k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_REQUIRE(dtype == A->dtype || (dtype == KRY_F64 && A->dtype == KRY_F32), KRY_EINVAL,
+              "vectors must have the operator dtype (or float64 over a float32 operator)");
+  KRY_HIP(hipSetDevice(ctx->device));
+  auto *s = new kry_minres();
+  try {
+    s->ctx = ctx;
+    s->A = A;
+    s->n = A->n;
+    s->k = k;
+    s->dtype = dtype;
+    const size_t elems = ((size_t)A->n * k + 15) / 16 * 16;
+    const size_t vb = elems * dsize(dtype);
+    void **vecs[] = {&s->b, &s->yk, &s->wv, &s->xk, &s->rt, &s->P[0], &s->P[1], &s->P[2]};
+    for (void **v : vecs) {
+      *v = dev_alloc(vb);
+      KRY_HIP(hipMemsetAsync(*v, 0, vb, ctx->stream));
+    }
+    for (int i = 0; i < 2; ++i) {
+      s->W[i] = static_cast<double *>(dev_alloc(elems * 8));
+      KRY_HIP(hipMemsetAsync(s->W[i], 0, elems * 8, ctx->stream));
+    }
+    s->part = static_cast<double *>(dev_alloc(2 * (size_t)kMaxGrid * k * 8));
+    s->scal = static_cast<double *>(dev_alloc(M_COUNT * (size_t)k * 8));
+    KRY_HIP(hipMemsetAsync(s->scal, 0, M_COUNT * (size_t)k * 8, ctx->stream));
+    s->chunk_cap = 64;
+    s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * k * 8));
+    s->ctrl = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
+    KRY_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    mr_free(s);
+    delete s;
+    throw;
+  }
+  *out = s;
+  KRY_API_END
+}
+
+int kry_minres_destroy(kry_minres *s) {
+  KRY_API_BEGIN
+  if (!s) return KRY_OK;
+  (void)hipSetDevice(s->ctx->device);
+  (void)hipStreamSynchronize(s->ctx->stream);
+  mr_free(s);
+  delete s;
+  KRY_API_END
+}
+
+int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && r0norm, KRY_EINVAL, "null argument");
+  check_vec(b, s->n, s->k, s->dtype, "b");
+  if (x0) check_vec(x0, s->n, s->k, s->dtype, "x0");
+  check_weights(w, s->n);
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const size_t elems = ((size_t)s->n * s->k + 15) / 16 * 16;
+  const size_t vb = b->bytes();
+  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  dev_free(s->x0);
+  s->x0 = nullptr;
+  if (x0) {
+    s->x0 = dev_alloc(elems * dsize(s->dtype));
+    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+  }
+  dev_free(s->w);
+  s->w = nullptr;
+  if (w) {
+    s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
+    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+  }
+  s->inner_f32 = (s->dtype == KRY_F32 && !w);
+  KRY_HIP(hipMemsetAsync(s->yk, 0, vb, st));
+  KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
+  for (int i = 0; i < 2; ++i) KRY_HIP(hipMemsetAsync(s->W[i], 0, elems * 8, st));
+  KRY_HIP(hipMemsetAsync(s->scal, 0, M_COUNT * (size_t)s->k * 8, st));
+  s->it = 0;
+  s->wflip = 0;
+  s->invariant = false;
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
+  KRY_HIP(hipMemcpyAsync(r0norm, s->scal + M_TMP * s->k, s->k * 8, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  s->started = true;
+  KRY_API_END
+}
+
+int kry_minres_set_criterion(kry_minres *s, const double *criterion) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && criterion, KRY_EINVAL, "null argument");
+  KRY_HIP(hipMemcpyAsync(s->scal + M_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  KRY_API_END
+}
+
+int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double *resnorms, int32_t *invariant) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && steps_done && resnorms && invariant && max_steps >= 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_minres_start has not been called");
+  if (s->invariant)
+    throw Error{KRY_EINVARIANT, "Krylov subspace was found to be invariant in the previous iteration."};
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  if (max_steps > s->chunk_cap) {
+    dev_free(s->hist);
+    s->hist = nullptr;
+    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
+    s->chunk_cap = max_steps;
+  }
+  reset_ctrl(s->ctrl, st);
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  Ctrl c;
+  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
+  if (done > 0) {
+    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * s->k * 8, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  }
+  s->it += done;
+  s->wflip = (s->wflip + done) & 1;
+  s->invariant = c.invariant != 0;
+  *steps_done = done;
+  *invariant = s->invariant ? 1 : 0;
+  KRY_API_END
+}
+
+int kry_minres_residual(kry_minres *s, double *norm2) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && norm2, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_minres_start has not been called");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_residual_impl<decltype(v0), decltype(m0), decltype(i0)>(s, norm2); });
+  KRY_API_END
+}
+
+int kry_minres_get(kry_minres *s, int which, void *host) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && host && which == 0, KRY_EINVAL, "bad argument");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  const int64_t N = s->n * (int64_t)s->k;
+  if (s->dtype == KRY_F64)
+    launch_elementwise<double>(N, s->k, OpXk<double>{static_cast<const double *>(s->x0), static_cast<const double *>(s->yk), static_cast<double *>(s->xk)},
+                               nullptr, nullptr, 0, st);
+  else
+    launch_elementwise<float>(N, s->k, OpXk<float>{static_cast<const float *>(s->x0), static_cast<const float *>(s->yk), static_cast<float *>(s->xk)},
+                              nullptr, nullptr, 0, st);
+  KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// Host-side objects behind the opaque C-ABI handles.
+#pragma once
+
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+
+struct kry_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  // per-kernel HIP-event profiling (bench.py's live roofline measurement)
+  bool profile = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
+  int ev_kernel_id = 0;  // which kernel family the pool currently records
+  // accumulated {count, ms} per kernel id, folded in at kry_profile_read
+  int64_t prof_count[4] = {0, 0, 0, 0};
+  double prof_ms[4] = {0, 0, 0, 0};
+  std::vector<int> ev_ids;
+};
+
+struct kry_csr {
+  kry_ctx *ctx = nullptr;
+  int64_t n = 0, nnz = 0;
+  int dtype = 0, itype = 0;
+  void *indptr = nullptr;   // itype, n + 1
+  void *indices = nullptr;  // itype, nnz padded to a multiple of 4 (zeros)
+  void *data = nullptr;     // dtype, nnz padded to a multiple of 4 (zeros)
+  void *tiles = nullptr;    // itype, ntiles + 1 row starts (streaming kernel)
+  int64_t ntiles = 0;
+};
+
+struct kry_vec {
+  kry_ctx *ctx = nullptr;
+  int64_t n = 0;
+  int32_t k = 1;
+  int dtype = 0;
+  void *d = nullptr;  // n*k elements, allocation padded to 16 elements
+  size_t bytes() const { return (size_t)n * k * (dtype == KRY_F64 ? 8 : 4); }
+};
+
+namespace kry {
+
+inline size_t dsize(int dtype) { return dtype == KRY_F64 ? 8 : 4; }
+inline size_t isize(int itype) { return itype == KRY_I64 ? 8 : 4; }
+
+void *dev_alloc(size_t bytes);
+void dev_free(void *p);
+
+// Event-timed launch bracket used by the solvers around their SpMV launches.
+struct ProfScope {
+  kry_ctx *ctx;
+  int id;
+  hipEvent_t e1 = nullptr;
+  ProfScope(kry_ctx *c, int kernel_id);
+  ~ProfScope();
+};
+
+enum { PROF_SPMV = 0, PROF_UPDATE = 1, PROF_MGS = 2, PROF_OTHER = 3 };
+
+}  // namespace kry

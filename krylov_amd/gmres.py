@@ -1,0 +1,155 @@
+"""Preconditioned GMRES driver (reference ``gmres.py:41-251``) over the device
+loop: Arnoldi with modified Gram-Schmidt (``ortho="mgs"`` / ``"mgsK"``,
+arnoldi.py:107-200), the Givens QR update of the Hessenberg matrix, and the
+solution ``x0 + V R^-1 y`` all run on the GPU (``kry_gmres_*``).
+
+Like the reference there is no restart parameter: ``maxiter`` bounds the
+Arnoldi basis, and restarted GMRES(m) is ``gmres(..., maxiter=m)`` chained
+through ``x0`` (see ``gmres_restarted``).
+"""
+import ctypes
+import weakref
+
+import numpy as np
+
+from . import _helpers, _lib
+from ._helpers import Info, Problem
+from ._lib import check, lib
+
+
+class _GmresState:
+    def __init__(self, prob, maxiter, sweeps):
+        self.prob = prob
+        h = ctypes.c_void_p()
+        check(lib.kry_gmres_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype),
+                                   int(maxiter), int(sweeps), ctypes.byref(h)))
+        self.h = h
+        self._fin = weakref.finalize(self, lib.kry_gmres_destroy, h)
+
+    def start(self):
+        p = self.prob
+        out = np.zeros(p.kpad)
+        check(lib.kry_gmres_start(self.h, p.b_dev.handle, p.x0_dev.handle if p.x0_dev else None,
+                                  p.w_dev.handle if p.w_dev else None, _lib.dptr(out)))
+        return out
+
+    def set_criterion(self, crit):
+        crit = np.ascontiguousarray(crit, dtype=np.float64)
+        check(lib.kry_gmres_set_criterion(self.h, _lib.dptr(crit)))
+
+    def run(self, steps):
+        out = np.zeros((max(steps, 1), self.prob.kpad))
+        done = ctypes.c_int32()
+        inv = ctypes.c_int32()
+        check(lib.kry_gmres_run(self.h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
+        return out[: done.value], bool(inv.value)
+
+    def solution(self):
+        check(lib.kry_gmres_solution(self.h))
+
+    def residual_norm2(self):
+        out = np.zeros(self.prob.kpad)
+        check(lib.kry_gmres_residual(self.h, _lib.dptr(out)))
+        return out
+
+    def xk(self):
+        p = self.prob
+        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        check(lib.kry_gmres_get(self.h, 0, _lib.ptr(out)))
+        return p.unpad_vec(out, p.r0_dtype)
+
+
+def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1.0e-15,
+          maxiter=None, callback=None):
+    """Preconditioned GMRES, reference signature (``gmres.py:41-54``)."""
+    if not ortho.startswith("mgs"):
+        if ortho == "householder":
+            raise NotImplementedError("ortho='householder' is not on the MI355X path yet (SURVEY §8(f) rank 2)")
+        raise ValueError(f"unknown ortho {ortho!r}")
+    sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
+    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
+
+    st = _GmresState(prob, maxiter, sweeps)
+    rn0 = st.start()
+    resnorms = [prob.colvals(rn0)]
+    if callback is not None:
+        # the reference passes Ml_r0 = b - A x0 here (gmres.py:143-144)
+        callback(x0_host, prob.b - prob.A @ x0_host)
+    criterion = np.maximum(tol * resnorms[0], atol)
+    st.set_criterion(prob.pad_cols(criterion, np.inf))
+
+    steps_done = 0
+    xk = None
+    k = 0
+    success = False
+
+    def current_x():
+        if steps_done == 0:
+            return x0_host  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
+        st.solution()
+        return st.xk()
+
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            if xk is None:
+                xk = current_x()
+            if steps_done == 0:
+                st.solution()
+            resnorms[-1] = prob.colvals(np.sqrt(np.asarray(st.residual_norm2()[: prob.kc]).astype(prob.inner_dtype)))
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        steps = 1 if callback is not None else min(_helpers.CHUNK, maxiter - k)
+        hist, _ = st.run(steps)
+        xk = None
+        for row in hist:
+            resnorms.append(prob.colvals(row))
+            k += 1
+            steps_done += 1
+        if callback is not None and len(hist):
+            xk = current_x()
+            callback(xk, np.array(resnorms[-1]))
+
+    if xk is None:
+        xk = current_x()
+    num_operations = {
+        "A": 1 + k,
+        "M": 2 + k,
+        "Ml": 2 + k,
+        "Mr": 1 + k,
+        "inner": 2 + k + k * (k + 1) / 2,
+        "axpy": 4 + 2 * k + k * (k + 1) / 2,
+    }
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)
+
+
+def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycles=100, ortho="mgs", inner=None):
+    """Restarted GMRES(restart): the reference's x0-chaining of ``gmres`` with
+    ``maxiter=restart`` (SURVEY §5 checkpoint/resume). The matrix is uploaded
+    once. Returns ``(x, infos)`` with one ``Info`` per cycle; the stop test of
+    every cycle uses ``tol`` relative to the residual at the start of the run.
+    """
+    from .sparse import as_device_operator
+
+    Aop = as_device_operator(A)
+    b = np.asarray(b)
+    x = np.zeros_like(b) if x0 is None else np.asarray(x0)
+    infos = []
+    r0 = None
+    for _ in range(max_cycles):
+        if r0 is None:
+            _, info0 = gmres(Aop, b, x0=x, maxiter=0, tol=0.0, atol=0.0, ortho=ortho, inner=inner)
+            r0 = info0.resnorms[0]
+        cur = None
+        _, info = gmres(Aop, b, x0=x, maxiter=restart, tol=0.0, atol=np.maximum(tol * r0, atol), ortho=ortho,
+                        inner=inner)
+        infos.append(info)
+        x = info.xk
+        cur = info.resnorms[-1]
+        if info.success or np.all(cur <= np.maximum(tol * r0, atol)):
+            break
+    return x, infos

@@ -1,0 +1,100 @@
+"""Preconditioned MINRES driver (reference ``minres.py:28-253``) over the
+device loop: Lanczos (arnoldi.py:203-281), the two-rotation QR update, the
+three-term direction recurrence and the x update run on the GPU
+(``kry_minres_*``), in chunks with one host sync per chunk.
+"""
+import ctypes
+import weakref
+
+import numpy as np
+
+from . import _helpers, _lib
+from ._helpers import Info, Problem
+from ._lib import check, lib
+
+
+class _MinresState:
+    def __init__(self, prob):
+        self.prob = prob
+        h = ctypes.c_void_p()
+        check(lib.kry_minres_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype),
+                                    ctypes.byref(h)))
+        self.h = h
+        self._fin = weakref.finalize(self, lib.kry_minres_destroy, h)
+
+    def start(self):
+        p = self.prob
+        out = np.zeros(p.kpad)
+        check(lib.kry_minres_start(self.h, p.b_dev.handle, p.x0_dev.handle if p.x0_dev else None,
+                                   p.w_dev.handle if p.w_dev else None, _lib.dptr(out)))
+        return out
+
+    def set_criterion(self, crit):
+        crit = np.ascontiguousarray(crit, dtype=np.float64)
+        check(lib.kry_minres_set_criterion(self.h, _lib.dptr(crit)))
+
+    def run(self, steps):
+        out = np.zeros((max(steps, 1), self.prob.kpad))
+        done = ctypes.c_int32()
+        inv = ctypes.c_int32()
+        check(lib.kry_minres_run(self.h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
+        return out[: done.value], bool(inv.value)
+
+    def residual_norm2(self):
+        out = np.zeros(self.prob.kpad)
+        check(lib.kry_minres_residual(self.h, _lib.dptr(out)))
+        return out
+
+    def xk(self):
+        p = self.prob
+        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        check(lib.kry_minres_get(self.h, 0, _lib.ptr(out)))
+        return p.unpad_vec(out, p.r0_dtype)
+
+
+def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None,
+           callback=None):
+    """Preconditioned MINRES, reference signature (``minres.py:28-40``)."""
+    prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
+    N = prob.A.shape[0]
+    maxiter = N if maxiter is None else maxiter
+    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
+
+    st = _MinresState(prob)
+    rn0 = st.start()
+    first = prob.colvals(rn0)
+    if callback is not None:
+        callback(x0_host, np.array(first))
+    resnorms = [first]
+    criterion = np.maximum(tol * resnorms[0], atol)
+    st.set_criterion(prob.pad_cols(criterion, np.inf))
+
+    k = 0
+    success = False
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            sq = st.residual_norm2()
+            resnorms[-1] = prob.colvals(np.sqrt(np.asarray(sq[: prob.kc]).astype(prob.inner_dtype)))
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        steps = 1 if callback is not None else min(_helpers.CHUNK, maxiter - k)
+        hist, _ = st.run(steps)
+        for row in hist:
+            resnorms.append(prob.colvals(row))
+            k += 1
+        if callback is not None and len(hist):
+            callback(st.xk(), np.array(resnorms[-1]))
+
+    xk = st.xk()
+    num_operations = {
+        "A": 1 + k,
+        "M": 2 + k,
+        "Ml": 2 + k,
+        "Mr": 1 + k,
+        "inner": 2 + 2 * k,
+        "axpy": 4 + 8 * k,
+    }
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)

@@ -1,0 +1,109 @@
+"""``CsrOperator``: a device-resident CSR matrix behind the reference's
+operator protocol (``.shape``, ``.dtype``, ``__matmul__``; _helpers.py:14-24,
+tests/test_solvers.py:229-237).
+
+The matrix is uploaded once. ``A @ x`` runs the gfx950 SpMV kernel (bitwise
+SciPy ``csr_matvec``/``csr_matvecs``); the solvers use the device copy
+directly and never move A again.
+"""
+import ctypes
+import weakref
+
+import numpy as np
+import scipy.sparse
+
+from . import _lib
+from ._lib import check, lib
+from .device import DeviceVector, get_context
+
+
+def _next_pow2(k):
+    p = 1
+    while p < k:
+        p *= 2
+    return p
+
+
+class CsrOperator:
+    def __init__(self, A, device=None):
+        if isinstance(A, CsrOperator):
+            raise TypeError("already a CsrOperator")
+        if scipy.sparse.issparse(A):
+            csr = A.tocsr() if A.format != "csr" else A
+        elif isinstance(A, np.ndarray):
+            if A.ndim != 2:
+                raise ValueError("A must be 2-D")
+            csr = scipy.sparse.csr_matrix(A)
+        else:
+            raise TypeError(
+                f"cannot place {type(A).__name__} on the device: pass a scipy.sparse matrix, a dense "
+                "ndarray, or a krylov_amd.CsrOperator (host-callback operators are not supported)"
+            )
+        if csr.shape[0] != csr.shape[1]:
+            raise ValueError("A must be square")
+        if np.iscomplexobj(csr.data):
+            raise TypeError("complex matrices are outside the MI355X path (float32/float64 only)")
+        dt = np.dtype(csr.dtype)
+        if dt not in (np.float32, np.float64):
+            dt = np.dtype(np.float64)
+        self.ctx = get_context(device)
+        self.shape = csr.shape
+        self.dtype = dt
+        self.n = csr.shape[0]
+        self.nnz = int(csr.nnz)
+        itype = np.int32 if (self.nnz < 2**31 and self.n < 2**31) else np.int64
+        indptr = np.ascontiguousarray(csr.indptr, dtype=itype)
+        indices = np.ascontiguousarray(csr.indices, dtype=itype)
+        data = np.ascontiguousarray(csr.data, dtype=dt)
+        self.index_dtype = np.dtype(itype)
+        h = ctypes.c_void_p()
+        check(
+            lib.kry_csr_create(
+                self.ctx.handle, self.n, self.nnz, _lib.ptr(indptr), _lib.ptr(indices),
+                _lib.ptr(data), _lib.dtype_code(dt), _lib.itype_code(itype), ctypes.byref(h),
+            )
+        )
+        self.handle = h
+        self._fin = weakref.finalize(self, lib.kry_csr_destroy, h)
+
+    @property
+    def device(self):
+        return self.ctx.device
+
+    def matvec_device(self, x, y):
+        """y = A x for DeviceVectors (no host traffic)."""
+        check(lib.kry_spmv(self.ctx.handle, self.handle, x.handle, y.handle))
+
+    def __matmul__(self, x):
+        x = np.asarray(x)
+        if x.shape[0] != self.n:
+            raise ValueError("dimension mismatch")
+        dt = np.result_type(self.dtype, x.dtype)
+        if dt not in (np.float32, np.float64):
+            raise TypeError(f"unsupported vector dtype {x.dtype}")
+        x2 = np.ascontiguousarray(x.reshape(self.n, -1), dtype=dt)
+        k = x2.shape[1]
+        kp = _next_pow2(k)
+        if kp != k:
+            x2 = np.concatenate([x2, np.zeros((self.n, kp - k), dtype=dt)], axis=1)
+        xv = DeviceVector(self.ctx, self.n, kp, dt)
+        xv.upload(x2)
+        yv = DeviceVector(self.ctx, self.n, kp, dt)
+        self.matvec_device(xv, yv)
+        y = yv.to_host()[:, :k]
+        return np.ascontiguousarray(y).reshape(x.shape)
+
+    matvec = __matmul__
+
+    def close(self):
+        self._fin()
+
+    def __repr__(self):
+        return f"CsrOperator(n={self.n}, nnz={self.nnz}, dtype={self.dtype}, device={self.device})"
+
+
+def as_device_operator(A, device=None):
+    """Return ``A`` as a CsrOperator (uploading scipy/dense inputs once)."""
+    if isinstance(A, CsrOperator):
+        return A
+    return CsrOperator(A, device=device)

@@ -1,0 +1,337 @@
+"""ORACLE — CPU restatement of the reference Krylov iterations (TEST INFRASTRUCTURE).
+
+This module is the checker, never the product: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it. The MI355X path (``krylov_amd``) never calls into ``oracle/``.
+
+It restates, for real dtypes and M = Ml = Mr = I, the iteration of
+``ju-liu/krylov`` 0.0.3 (``/root/reference/src/krylov``):
+
+* ``cg``      — ``cg.py:16-259`` (loop ``cg.py:155-234``)
+* ``gmres``   — ``gmres.py:41-251`` with ``ArnoldiMGS`` ``arnoldi.py:107-200``
+* ``minres``  — ``minres.py:28-253`` with ``ArnoldiLanczos`` ``arnoldi.py:203-281``
+* ``givens``  — ``givens.py:5-47`` (LAPACK ``?lartg`` per column)
+* ``Info``    — ``_helpers.py:93-98``
+
+Arithmetic is delegated exactly where the reference delegates it: SpMV to
+SciPy ``csr_matvec``/``csr_matvecs`` (``A @ x``), 1-D inner products to
+``np.dot`` (OpenBLAS), block inner products to ``np.einsum`` (sequential per
+column), rotations to LAPACK ``dlartg``. Parity pinned: every function here is
+checked against fixtures produced by the reference itself
+(``tests/golden/make_golden.py`` → ``tests/golden/solvers.npz``) in
+``tests/test_oracle.py``.
+"""
+from collections import namedtuple
+
+import numpy as np
+import scipy.linalg
+from scipy.linalg import lapack
+
+Info = namedtuple(
+    "IterInfo",
+    ["success", "xk", "numsteps", "resnorms", "num_operations", "arnoldi"],
+    defaults=(None, None),
+)
+
+
+class InvariantError(Exception):
+    """Stands for ``krylov.errors.ArgumentError`` (errors.py:1-9)."""
+
+
+def default_inner(shape):
+    """_helpers.py:101-110: np.dot for vectors, einsum over axis 0 otherwise."""
+    if len(shape) == 1:
+        return lambda x, y: np.dot(x.conj(), y)
+    return lambda x, y: np.einsum("i...,i...->...", x.conj(), y)
+
+
+def _safe(d):
+    """The reference's zero-division guard ``np.where(d != 0, d, 1.0)``."""
+    return np.where(d != 0, d, 1.0)
+
+
+def _real_norm2(v):
+    if np.any(v.imag != 0.0):
+        raise ValueError("inner product <x, M x> gave nonzero imaginary part")
+    return v.real
+
+
+def givens(X):
+    """givens.py:5-47 — one LAPACK lartg call per trailing column."""
+    assert X.shape[0] == 2
+    flat = X.reshape(2, -1)
+    lartg = lapack.get_lapack_funcs("lartg", (flat,))
+    cs, rs = [], []
+    for col in range(flat.shape[1]):
+        c, s, r = lartg(*flat[:, col])
+        cs.append(np.array([[c, s], [-np.conj(s), c]]))
+        rs.append(r)
+    G = np.moveaxis(np.array(cs), 0, -1).reshape(2, 2, *X.shape[1:])
+    return G, np.array(rs)
+
+
+def _rot(G, v):
+    """multi_matmul (gmres.py:19-21, minres.py:23-25)."""
+    return np.einsum("ij...,j...->i...", G, v)
+
+
+def cg(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates cg.py:16-259 with M = Ml = I (no Lanczos return)."""
+    b = np.asarray(b)
+    assert A.shape[0] == A.shape[1] == b.shape[0]
+    inner = default_inner(b.shape) if inner is None else inner
+    maxiter = A.shape[0] if maxiter is None else maxiter
+    x0 = np.zeros_like(b) if x0 is None else x0
+
+    def residual(z):  # cg.py:71-95
+        r = b - A @ z
+        return r, _real_norm2(inner(r, r))
+
+    r, rho = residual(x0)
+    if callback is not None:
+        callback(x0, r)
+    resnorms = [np.sqrt(rho)]
+    y = np.zeros(x0.shape, dtype=r.dtype)
+    rho_prev, rho_cur = None, rho
+    r = r.copy()
+    p = r.copy()
+    xk = None
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):  # cg.py:156-164
+            xk = x0 + y if xk is None else xk
+            resnorms[-1] = np.sqrt(residual(xk)[1])
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        if k > 0:  # cg.py:175-178
+            p = r + (rho_cur / _safe(rho_prev)) * p
+        Ap = A @ p
+        alpha = rho_cur / _safe(inner(p, Ap))  # cg.py:183-185
+        y += alpha * p
+        xk = None
+        r -= alpha * Ap
+        if callback is not None:
+            xk = x0 + y
+            callback(xk, r)
+        rr = _real_norm2(inner(r, r))
+        rho_prev, rho_cur = rho_cur, rr
+        resnorms.append(np.sqrt(rr))
+        k += 1
+    xk = x0 + y if xk is None else xk
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 2 + 2 * k}
+    return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)
+
+
+def _trisolve_columns(R, y):
+    """multi_solve_triangular (gmres.py:24-38): per-column solve, zero rhs -> 0."""
+    k = R.shape[0]
+    Rc = R.reshape(k, k, -1)
+    yc = y.reshape(k, -1)
+    cols = []
+    for c in range(Rc.shape[2]):
+        if np.all(yc[:, c] == 0.0):
+            cols.append(np.zeros(k))
+        else:
+            cols.append(scipy.linalg.solve_triangular(Rc[:, :, c], yc[:, c]))
+    return np.array(cols).T.reshape([k] + list(R.shape[2:]))
+
+
+def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200), M = I."""
+    b = np.asarray(b)
+    assert A.shape[0] == A.shape[1] == b.shape[0]
+    assert ortho.startswith("mgs")
+    sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    inner = default_inner(b.shape) if inner is None else inner
+    maxiter = A.shape[0] if maxiter is None else maxiter
+    x0 = np.zeros_like(b) if x0 is None else np.asarray(x0)
+
+    def resnorm_of(z):
+        r = b - A @ z
+        return np.sqrt(_real_norm2(inner(r, r)))
+
+    r0 = b - A @ x0
+    r0norm = np.sqrt(_real_norm2(inner(r0, r0)))
+    resnorms = [r0norm]
+    if callback is not None:
+        callback(x0, r0)
+
+    hdtype = np.result_type(A.dtype, r0.dtype)
+    V = [r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
+    invariant = False
+    steps = 0
+    R = np.zeros([maxiter + 1, maxiter] + list(b.shape[1:]), dtype=r0.dtype)
+    y = np.zeros([maxiter + 1] + list(b.shape[1:]), dtype=r0.dtype)
+    y[0] = r0norm
+    G = []
+
+    def solution(yv):
+        if yv is None:
+            return x0
+        if steps > 0:
+            coef = _trisolve_columns(R[:steps, :steps], yv)
+            acc = sum(c * v for c, v in zip(coef, V))
+            return x0 + acc
+        return x0
+
+    yk = None
+    xk = None
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            xk = solution(yk) if xk is None else xk
+            resnorms[-1] = resnorm_of(xk)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        # --- Arnoldi MGS step (arnoldi.py:167-200) ---
+        if invariant:
+            raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
+        w = A @ V[steps]
+        h = np.zeros([steps + 2] + list(b.shape[1:]), dtype=hdtype)
+        for _ in range(sweeps):
+            for j in range(steps + 1):
+                a = inner(V[j], w)
+                h[j] += a
+                w -= a * V[j]
+        h[steps + 1] = np.sqrt(inner(w, w))
+        if np.all(h[steps + 1] <= 1.0e-14):
+            invariant = True
+        else:
+            V.append(w / np.where(h[steps + 1] != 0.0, h[steps + 1], 1.0))
+        steps += 1
+        # --- Givens QR update (gmres.py:206-221) ---
+        R[: k + 2, k] = h[: k + 2]
+        for i in range(k):
+            R[i : i + 2, k] = _rot(G[i], R[i : i + 2, k])
+        g, rr = givens(R[k : k + 2, k])
+        G.append(g)
+        R[k, k] = rr
+        R[k + 1, k] = 0.0
+        y[k : k + 2] = _rot(G[k], y[k : k + 2])
+        yk = y[: k + 1]
+        xk = None
+        rn = np.array(np.abs(y[k + 1]))
+        if callback is not None:
+            xk = solution(yk)
+            callback(xk, rn)
+        resnorms.append(rn[()])
+        k += 1
+    if xk is None:
+        xk = solution(y[:steps])
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k,
+           "inner": 2 + k + k * (k + 1) / 2, "axpy": 4 + 2 * k + k * (k + 1) / 2}
+    return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)
+
+
+def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates minres.py:28-253 with Lanczos (arnoldi.py:203-281), M = I.
+
+    Precision follows the reference under NumPy-2 promotion: the Lanczos
+    scalars ``h`` are kept in the vector dtype, while ``R``, the rotations, ``y``
+    and therefore ``z``/``W`` are float64 (minres.py:195,219).
+    """
+    b = np.asarray(b)
+    assert A.shape[0] == A.shape[1] == b.shape[0]
+    inner = default_inner(b.shape) if inner is None else inner
+    maxiter = A.shape[0] if maxiter is None else maxiter
+    x0 = np.zeros_like(b) if x0 is None else x0
+
+    def resnorm_of(z):
+        r = b - A @ z
+        return np.sqrt(_real_norm2(inner(r, r)))
+
+    r = b - A @ x0
+    rnorm = np.sqrt(_real_norm2(inner(r, r)))
+    dtype = r.dtype
+    hdtype = np.result_type(A.dtype, r.dtype)
+    # Lanczos state (arnoldi.py:203-235)
+    lz_h = np.zeros([3] + list(b.shape[1:]), dtype=hdtype)
+    lz_scale = np.where(rnorm != 0.0, rnorm, 1.0)
+    lz_v = r / lz_scale
+    lz_p = r / lz_scale
+    lz_pold = None
+    lz_iter = 0
+    invariant = False
+
+    W = [np.zeros(b.shape, dtype=dtype), np.zeros(b.shape, dtype=dtype)]
+    y = np.array([rnorm, np.zeros_like(rnorm)])
+    G = [None, None]
+    yk = np.zeros(b.shape, dtype=dtype)
+    xk = None
+    rn = np.array(rnorm)
+    if callback is not None:
+        callback(x0, rn)
+    resnorms = [rn[()]]
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            xk = x0 + yk if xk is None else xk
+            resnorms[-1] = resnorm_of(xk)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        v = lz_v
+        # --- Lanczos step (arnoldi.py:237-281) ---
+        if invariant:
+            raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
+        w = A @ lz_v
+        if lz_iter > 0:
+            lz_h[0] = lz_h[2]
+            w -= lz_h[0] * lz_pold
+        a = inner(lz_v, w)
+        lz_h[1] = a
+        w -= a * lz_p
+        lz_h[2] = np.sqrt(inner(w, w))
+        if np.all(lz_h[2] <= 1.0e-14):
+            invariant = True
+            lz_v = lz_p = None
+        else:
+            s = np.where(lz_h[2] != 0.0, lz_h[2], 1.0)
+            lz_pold = lz_p
+            lz_p = w / s
+            lz_v = w / s
+        lz_iter += 1
+        h = lz_h.real
+        # --- QR update (minres.py:193-224) ---
+        Rv = np.zeros([4] + list(b.shape[1:]), dtype=float)
+        Rv[1] = h[0]
+        if G[1] is not None:
+            Rv[:2] = _rot(G[1], Rv[:2])
+        Rv[2] = h[1]
+        Rv[3] = h[2]
+        if G[0] is not None:
+            Rv[1:3] = _rot(G[0], Rv[1:3])
+        G[1] = G[0]
+        G[0], rr = givens(Rv[2:4])
+        Rv[2] = rr
+        Rv[3] = 0.0
+        y = _rot(G[0], y)
+        z = (v - Rv[0] * W[0] - Rv[1] * W[1]) / np.where(Rv[2] != 0.0, Rv[2], 1.0)
+        W[0], W[1] = W[1], z
+        yk += y[0] * z
+        xk = None
+        y = np.array([y[1], np.zeros_like(y[1])])
+        rn = np.array(np.abs(y[0]))
+        if callback is not None:
+            xk = x0 + yk
+            callback(xk, rn)
+        resnorms.append(rn[()])
+        k += 1
+    if xk is None:
+        xk = x0 + yk
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 4 + 8 * k}
+    return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)

@@ -1,0 +1,243 @@
+"""Solver parity on the MI355X against fixtures produced by the reference
+(tests/golden/solvers.npz) and the oracle, plus the reference's own solver
+tests restated for the device path (tests/test_cg.py, test_gmres.py,
+test_minres.py, test_solvers.py of ju-liu/krylov)."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from tests import gpu_helpers as H
+
+pytestmark = pytest.mark.gpu
+
+REAL_SPD_CASES = [
+    H.spd_dense((5,)),
+    H.spd_dense((5, 1)),
+    H.spd_dense((5, 3)),
+    H.spd_rhs_0((5,)),
+    H.spd_rhs_0sol0(),
+    H.symmetric_indefinite(),
+]
+
+
+@pytest.mark.parametrize("A_b", REAL_SPD_CASES)
+def test_cg_reference_cases(A_b):
+    import krylov_amd
+
+    A, b = A_b
+    calls = 0
+
+    def callback(x, r):
+        nonlocal calls
+        calls += 1
+
+    sol, info = krylov_amd.cg(A, b, tol=1.0e-7, callback=callback)
+    assert calls == info.numsteps + 1
+    assert info.success
+    H.assert_consistent(A, b, info, sol, 1.0e-7)
+
+
+@pytest.mark.parametrize("A_b", REAL_SPD_CASES)
+def test_minres_reference_cases(A_b):
+    import krylov_amd
+
+    A, b = A_b
+    calls = 0
+
+    def callback(x, r):
+        nonlocal calls
+        calls += 1
+
+    sol, info = krylov_amd.minres(A, b, tol=1.0e-7, callback=callback)
+    assert calls == info.numsteps + 1
+    assert info.success
+    H.assert_consistent(A, b, info, sol, 1.0e-7)
+
+
+@pytest.mark.parametrize("A_b", REAL_SPD_CASES + [H.real_unsymmetric()])
+@pytest.mark.parametrize("ortho", ["mgs", "mgs2"])
+def test_gmres_reference_cases(A_b, ortho):
+    import krylov_amd
+
+    A, b = A_b
+    calls = 0
+
+    def callback(x, r):
+        nonlocal calls
+        calls += 1
+
+    sol, info = krylov_amd.gmres(A, b, tol=1.0e-7, ortho=ortho, callback=callback)
+    assert calls == info.numsteps + 1
+    assert info.success
+    H.assert_consistent(A, b, info, sol, 1.0e-7)
+
+
+@pytest.mark.parametrize("name", ["cg", "gmres", "minres"])
+@pytest.mark.parametrize("shape", [(100,), (100, 1)])
+def test_readme_goldens(name, shape):
+    # tests/test_solvers.py:123-144 known answers
+    import krylov_amd
+
+    refs = {
+        "cg": [1004.1873775173957, 1000.0003174916551, 999.9999999997555],
+        "gmres": [1004.1873724888546, 1000.0003124630923, 999.999994971191],
+        "minres": [1004.187372488912, 1000.0003124632159, 999.9999949713145],
+    }[name]
+    A = np.diag([1.0e-3] + list(range(2, 101)))
+    b = np.ones(shape)
+    sol, _ = getattr(krylov_amd, name)(A, b)
+    assert sol.shape == b.shape
+    tol = 1.0e-11
+    assert abs(np.sum(np.abs(sol)) - refs[0]) < tol * refs[0]
+    assert abs(np.sqrt(np.dot(sol.T, sol)).item() - refs[1]) < tol * refs[1]
+    assert abs(np.max(np.abs(sol)) - refs[2]) < tol * refs[2]
+
+
+@pytest.mark.parametrize("name", ["cg", "gmres", "minres"])
+@pytest.mark.parametrize("shape", ["1d", "nx1"])
+def test_diag100_histories(golden, name, shape):
+    import krylov_amd
+
+    A = np.diag([1.0e-3] + list(range(2, 101)))
+    b = np.ones(100) if shape == "1d" else np.ones((100, 1))
+    sol, info = getattr(krylov_amd, name)(A, b)
+    H.assert_parity(info, golden["solvers"], f"diag100_{name}_{shape}", rtol=1e-9, xtol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["cg", "minres", "gmres"])
+def test_weighted_inner_goldens(name):
+    # tests/test_solvers.py:147-196 with inner = np.dot(x.T, w * y)
+    import krylov_amd
+
+    n = 100
+    A = np.diag([1.0e-3] + list(range(2, n + 1)))
+    w = 10 / np.arange(1, n + 1)
+    for b in (np.ones(n), np.ones((n, 1))):
+        sol, _ = getattr(krylov_amd, name)(A, b, inner=krylov_amd.WeightedInner(w))
+        sol = sol.reshape(-1)
+        assert abs(np.sum(np.abs(sol)) - 1004.1873775173957) < 1e-9 * 1004.1873775173957
+        assert abs(np.sqrt(np.dot(sol, sol)) - 1000.0003174916551) < 1e-9 * 1000.0003174916551
+        assert abs(np.max(np.abs(sol)) - 999.9999999997555) < 1e-9 * 999.9999999997555
+
+
+@pytest.mark.parametrize("name", ["cg", "minres", "gmres"])
+@pytest.mark.parametrize("b_shape", [(5,), (5, 1), (5, 3)])
+def test_explicit_residual(name, b_shape):
+    import krylov_amd
+
+    a = np.linspace(1.0, 2.0, b_shape[0])
+    a[-1] = 1e-2
+    _, info = getattr(krylov_amd, name)(np.diag(a), np.ones(b_shape), tol=1.0e-7)
+    assert np.all(info.resnorms[-1] < 1.0e-7)
+
+
+@pytest.mark.parametrize("name", ["cg", "minres", "gmres"])
+def test_exact_solution_as_initial_guess(name):
+    import krylov_amd
+
+    A = np.diag([1.0e-3] + list(range(2, 11)))
+    b = np.ones(10)
+    x0 = np.linalg.solve(A, b)
+    sol, info = getattr(krylov_amd, name)(A, b, x0=x0)
+    assert len(info.resnorms) == 1
+    if name == "gmres":
+        assert info.xk is x0
+
+
+@pytest.mark.parametrize("name", ["cg", "minres", "gmres"])
+def test_scipy_sparse_and_csr_operator(name):
+    import krylov_amd
+
+    n = 5
+    a = np.linspace(1.0, 2.0, n)
+    a[-1] = 1e-2
+    for A in (scipy.sparse.spdiags(a, [0], n, n), krylov_amd.CsrOperator(scipy.sparse.spdiags(a, [0], n, n))):
+        _, info = getattr(krylov_amd, name)(A, np.ones(n), tol=1.0e-12)
+        assert info.resnorms[-1] <= 1.0e-12
+
+
+def test_cg_poisson_histories(golden):
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    P = krylov_amd.CsrOperator(problems.poisson2d(64))
+    n = P.shape[0]
+    H.assert_parity(krylov_amd.cg(P, np.ones(n), tol=1e-8)[1], d, "cg_poisson64_1d")
+    H.assert_parity(krylov_amd.cg(P, d["poisson64_B"], tol=1e-8)[1], d, "cg_poisson64_blk8")
+    H.assert_parity(krylov_amd.cg(P, np.ones(n), x0=d["poisson64_x0"], tol=1e-6, maxiter=150)[1], d, "cg_poisson64_x0")
+    S = problems.stencil15_3d(24)
+    H.assert_parity(krylov_amd.cg(S, np.ones(S.shape[0]), tol=1e-8)[1], d, "cg_st15_24")
+
+
+def test_gmres_random_histories(golden):
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    R = krylov_amd.CsrOperator(problems.random_nonsym(5000))
+    for ortho in ("mgs", "mgs2"):
+        info = krylov_amd.gmres(R, np.ones(5000), ortho=ortho, maxiter=30, tol=0.0)[1]
+        H.assert_parity(info, d, f"gmres_rand5k_{ortho}", rtol=1e-10, xtol=1e-9)
+    info = krylov_amd.gmres(R, d["rand5k_B3"], maxiter=20, tol=0.0)[1]
+    H.assert_parity(info, d, "gmres_rand5k_blk3", rtol=1e-10, xtol=1e-9)
+
+
+def test_minres_histories(golden):
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    P = problems.poisson2d(64)
+    H.assert_parity(krylov_amd.minres(P, np.ones(P.shape[0]), tol=1e-8)[1], d, "minres_poisson64")
+
+
+def test_minres_fp32_weighted(golden):
+    """cfg5 pattern at 20^3: float32 operator, float64 weights (the reference
+    then runs its Lanczos vectors in float64), 50 fixed iterations; fp32
+    parity bar 1e-4 relative."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    W, w = problems.shifted_lap3d_weighted(20)
+    info = krylov_amd.minres(W, np.ones(W.shape[0], dtype=np.float32), inner=krylov_amd.WeightedInner(w),
+                             tol=0.0, maxiter=50)[1]
+    assert info.xk.dtype == np.float32
+    H.assert_parity(info, d, "minres_w20_f32", rtol=1e-4, xtol=1e-4, final_atol=1e-4 * d["minres_w20_f32_resnorms"][0])
+
+
+def test_cg_weighted_histories(golden):
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    W, w = problems.shifted_lap3d_weighted(20)
+    info = krylov_amd.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=krylov_amd.WeightedInner(w), tol=1e-8)[1]
+    H.assert_parity(info, d, "cg_w20_weighted", rtol=1e-8, xtol=1e-8)
+
+
+def test_restarted_gmres_reaches_tolerance():
+    import krylov_amd
+    from krylov_amd import problems
+
+    R = problems.random_nonsym(5000)
+    b = np.ones(5000)
+    x, infos = krylov_amd.gmres_restarted(R, b, restart=30, tol=1e-8, max_cycles=10)
+    assert np.linalg.norm(b - R @ x) <= 1.01e-8 * np.linalg.norm(b)
+    assert len(infos) >= 2
+
+
+def test_device_matches_oracle_on_metric_shape_small():
+    """Same generator as the metric (15-pt stencil) at 32^3: device vs oracle."""
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref as K
+
+    S = problems.stencil15_3d(32)
+    b = np.ones(S.shape[0])
+    _, ref = K.cg(S, b, tol=1e-10)
+    _, got = krylov_amd.cg(S, b, tol=1e-10)
+    assert got.numsteps == ref.numsteps
+    r, g = np.asarray(ref.resnorms), np.asarray(got.resnorms)
+    assert np.all(np.abs(g[:-1] - r[:-1]) <= 1e-10 * np.abs(r[:-1]))

@@ -1,0 +1,154 @@
+"""Pin the oracle (CPU restatement) against fixtures produced by the reference
+itself (tests/golden/make_golden.py) and by SciPy/LAPACK. CPU only."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from krylov_amd import problems
+from oracle import krylov_ref as K
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _check(prefix, sol, info, d):
+    assert info.numsteps == int(d[prefix + "_numsteps"])
+    assert info.success == bool(d[prefix + "_success"])
+    np.testing.assert_array_equal(np.asarray(info.resnorms, dtype=np.float64), d[prefix + "_resnorms"])
+    np.testing.assert_array_equal(info.xk, d[prefix + "_xk"])
+    ops = info.num_operations
+    np.testing.assert_array_equal([ops[k] for k in ("A", "M", "Ml", "Mr", "inner", "axpy")], d[prefix + "_ops"])
+    assert (sol is None) == bool(d[prefix + "_sol_is_none"])
+
+
+@pytest.mark.parametrize("name", ["cg", "gmres", "minres"])
+@pytest.mark.parametrize("shape", ["1d", "nx1"])
+def test_oracle_diag100(golden, name, shape):
+    A, b = problems.diag100()
+    bb = b if shape == "1d" else b[:, None]
+    sol, info = getattr(K, name)(A, bb)
+    _check(f"diag100_{name}_{shape}", sol, info, golden["solvers"])
+
+
+def test_oracle_readme_goldens():
+    # tests/test_solvers.py:126-128 (the reference's own known answers)
+    refs = {
+        "cg": [1004.1873775173957, 1000.0003174916551, 999.9999999997555],
+        "gmres": [1004.1873724888546, 1000.0003124630923, 999.999994971191],
+        "minres": [1004.187372488912, 1000.0003124632159, 999.9999949713145],
+    }
+    A, b = problems.diag100()
+    for name, ref in refs.items():
+        sol, _ = getattr(K, name)(A, b)
+        assert abs(np.sum(np.abs(sol)) - ref[0]) < 1e-11 * ref[0]
+        assert abs(np.sqrt(np.dot(sol, sol)) - ref[1]) < 1e-11 * ref[1]
+        assert abs(np.max(np.abs(sol)) - ref[2]) < 1e-11 * ref[2]
+
+
+def test_oracle_cg_histories(golden):
+    d = golden["solvers"]
+    P = problems.poisson2d(64)
+    n = P.shape[0]
+    _check("cg_poisson64_1d", *K.cg(P, np.ones(n), tol=1e-8), d)
+    _check("cg_poisson64_blk8", *K.cg(P, d["poisson64_B"], tol=1e-8), d)
+    _check("cg_poisson64_x0", *K.cg(P, np.ones(n), x0=d["poisson64_x0"], tol=1e-6, maxiter=150), d)
+    S = problems.stencil15_3d(24)
+    _check("cg_st15_24", *K.cg(S, np.ones(S.shape[0]), tol=1e-8), d)
+
+
+def test_oracle_gmres_histories(golden):
+    d = golden["solvers"]
+    R = problems.random_nonsym(5000)
+    for ortho in ("mgs", "mgs2"):
+        _check(f"gmres_rand5k_{ortho}", *K.gmres(R, np.ones(5000), ortho=ortho, maxiter=30, tol=0.0), d)
+    _check("gmres_rand5k_blk3", *K.gmres(R, d["rand5k_B3"], maxiter=20, tol=0.0), d)
+
+
+def test_oracle_minres_histories(golden):
+    d = golden["solvers"]
+    P = problems.poisson2d(64)
+    _check("minres_poisson64", *K.minres(P, np.ones(P.shape[0]), tol=1e-8), d)
+    W, w = problems.shifted_lap3d_weighted(20)
+    np.testing.assert_array_equal(w, d["minres_w20_w"])
+
+    def inner(x, y):
+        return np.dot(x.T, w * y)
+
+    _check("minres_w20_f32", *K.minres(W, np.ones(W.shape[0], dtype=np.float32), inner=inner, tol=0.0, maxiter=50), d)
+    _check("cg_w20_weighted", *K.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=inner, tol=1e-8), d)
+
+
+def test_oracle_givens(golden):
+    d = golden["lartg"]
+    G, r = K.givens(d["fg"].T.copy())
+    np.testing.assert_array_equal(G, d["givens_G"])
+    np.testing.assert_array_equal(r, d["givens_r"])
+
+
+def _c_matvec(lib, A, x):
+    vt = "f64" if A.dtype == np.float64 else "f32"
+    it = "i32" if A.indices.dtype == np.int32 else "i64"
+    multi = x.ndim == 2
+    fn = getattr(lib, f"oracle_csr_matvec_{vt}_{it}" + ("s" if multi else ""))
+    y = np.empty(x.shape, dtype=A.dtype)
+    args = [ctypes.c_int64(A.shape[0])]
+    if multi:
+        args.append(ctypes.c_int64(x.shape[1]))
+    for a in (A.indptr, A.indices, A.data, np.ascontiguousarray(x), y):
+        args.append(ctypes.c_void_p(a.ctypes.data))
+    fn(*args)
+    return y
+
+
+@pytest.mark.parametrize("key", ["f64_i32", "f64_i64", "f32_i32", "f32_i64"])
+def test_c_oracle_spmv_bitwise(golden, oracle_lib, key):
+    import scipy.sparse
+
+    d = golden["spmv"]
+    n = d[f"{key}_indptr"].shape[0] - 1
+    A = scipy.sparse.csr_matrix((d[f"{key}_data"], d[f"{key}_indices"], d[f"{key}_indptr"]), shape=(n, n))
+    A.indices = d[f"{key}_indices"]
+    A.indptr = d[f"{key}_indptr"]
+    y = _c_matvec(oracle_lib, A, d[f"{key}_x"])
+    np.testing.assert_array_equal(y.view(np.uint8), d[f"{key}_y"].view(np.uint8))
+    Y = _c_matvec(oracle_lib, A, d[f"{key}_X"])
+    np.testing.assert_array_equal(Y.view(np.uint8), d[f"{key}_Y"].view(np.uint8))
+
+
+def test_c_oracle_lartg_bitwise(golden, oracle_lib):
+    d = golden["lartg"]
+    P = ctypes.POINTER(ctypes.c_double)
+    oracle_lib.oracle_dlartg.argtypes = [ctypes.c_double, ctypes.c_double, P, P, P]
+    got = []
+    for f, g in d["fg"]:
+        c, s, r = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        oracle_lib.oracle_dlartg(f, g, c, s, r)
+        got.append((c.value, s.value, r.value))
+    np.testing.assert_array_equal(np.array(got).view(np.uint64), d["d"].view(np.uint64))
+    F = ctypes.POINTER(ctypes.c_float)
+    oracle_lib.oracle_slartg.argtypes = [ctypes.c_float, ctypes.c_float, F, F, F]
+    got = []
+    for f, g in d["fg32"]:
+        c, s, r = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        oracle_lib.oracle_slartg(f, g, c, s, r)
+        got.append((c.value, s.value, r.value))
+    np.testing.assert_array_equal(np.array(got, dtype=np.float32).view(np.uint32), d["s"].view(np.uint32))
+
+
+@pytest.mark.parametrize(
+    "name, fn",
+    [
+        ("stencil15_3d_24", lambda: problems.stencil15_3d(24)),
+        ("poisson2d_64", lambda: problems.poisson2d(64)),
+        ("random_nonsym_5000", lambda: problems.random_nonsym(5000)),
+        ("shifted_lap3d_weighted_20", lambda: problems.shifted_lap3d_weighted(20)[0]),
+    ],
+)
+def test_generators_match_pinned_hashes(name, fn):
+    with open(os.path.join(HERE, "golden", "problems.json")) as f:
+        pinned = json.load(f)
+    A = fn()
+    assert A.nnz == pinned[name]["nnz"]
+    assert problems.csr_sha256(A) == pinned[name]["sha256"]
