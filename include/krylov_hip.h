@@ -66,19 +66,21 @@ int kry_ctx_synchronize(kry_ctx *ctx);
 /* ---- CSR operator ------------------------------------------------------
  * Replaces the scipy.sparse matrix the reference multiplies with `A @ x`
  * (_helpers.py:44-48 Product.__matmul__, cg.py:86, gmres.py:106,
- * minres.py:111,121). Uploads once; the library owns the device copy.
- * Indices may be unsorted and contain duplicates; they are honoured in stored
- * order (SciPy csr_matvec semantics). */
+ * minres.py:111,121). Uploads once; the library owns the device copy, which
+ * it lays out as SELL-64 (slices of 64 rows = one wavefront, column-major
+ * within a slice; slices with very uneven rows stay CSR). Indices may be
+ * unsorted and contain duplicates; they are honoured in stored order (SciPy
+ * csr_matvec semantics). */
 int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr,
                    const void *indices, const void *data, int dtype, int itype,
                    kry_csr **out);
 int kry_csr_destroy(kry_csr *A);
-/* Host-only (no GPU needed): the row-tile partition the streaming SpMV kernel
- * uses. Tiles hold <= tile_nnz nonzeros and <= tile_rows rows, except a single
- * row longer than tile_nnz which gets a tile of its own. Returns the tile
- * count; if row_starts != NULL it receives ntiles + 1 row offsets. */
-int kry_csr_partition(int64_t n, const void *indptr, int itype, int64_t tile_nnz,
-                      int64_t tile_rows, int64_t *ntiles, int64_t *row_starts);
+/* Host-only (no GPU needed): the SELL-64 plan kry_csr_create will build —
+ * slice count, stored slots (nonzeros + padding of regular slices) and the
+ * number of irregular slices (64 * width > 2 * slice_nnz + 1024) that the
+ * kernel walks in CSR form instead. */
+int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
+                   int64_t *nslots, int64_t *nirregular);
 
 /* ---- vectors (n x k row-major blocks) ---------------------------------- */
 int kry_vec_create(kry_ctx *ctx, int64_t n, int32_t k, int dtype, kry_vec **out);

@@ -1,6 +1,7 @@
 // C-ABI: library, context, CSR operator, vectors, primitives, timers.
 #include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "device.hpp"
 
@@ -46,24 +47,59 @@ ProfScope::~ProfScope() {
   ctx->ev_used++;
 }
 
-// Tile partition for the streaming SpMV kernel (see krylov_hip.h).
+// ---------------------------------------------------------- SELL-64 layout
+// Host-side plan: slice s = rows [64 s, 64 s + 64); width = longest row;
+// a slice is irregular (CSR walk) when 64 * width > 2 * nnz_slice + 1024.
 template <typename I>
-static int64_t partition_rows(int64_t n, const I *ip, int64_t tile_nnz, int64_t tile_rows,
-                              std::vector<int64_t> *out) {
-  int64_t count = 0;
-  if (out) out->push_back(0);
-  int64_t r = 0;
-  while (r < n) {
-    const int64_t start = r, e_start = (int64_t)ip[r];
-    if ((int64_t)ip[r + 1] - e_start > tile_nnz) {
-      r += 1;
-    } else {
-      while (r < n && r - start < tile_rows && (int64_t)ip[r + 1] - e_start <= tile_nnz) ++r;
-    }
-    ++count;
-    if (out) out->push_back(r);
+static void sell_plan(int64_t n, const I *ip, std::vector<int64_t> *sptr, std::vector<int32_t> *width,
+                      int64_t *nslices, int64_t *nslots, int64_t *nirr) {
+  const int64_t ns = (n + kSlice - 1) / kSlice;
+  if (sptr) sptr->assign(ns + 1, 0);
+  if (width) width->assign(ns, 0);
+  int64_t slots = 0, irr = 0;
+  for (int64_t s = 0; s < ns; ++s) {
+    const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+    int64_t w = 0;
+    for (int64_t r = r0; r < r1; ++r) w = std::max<int64_t>(w, (int64_t)ip[r + 1] - (int64_t)ip[r]);
+    const int64_t snnz = (int64_t)ip[r1] - (int64_t)ip[r0];
+    const bool irregular = kSlice * w > 2 * snnz + 1024 || w > (int64_t(1) << 30);
+    if (irregular) ++irr;
+    if (width) (*width)[s] = irregular ? -1 : (int32_t)w;
+    if (!irregular) slots += kSlice * w;
+    if (sptr) (*sptr)[s + 1] = slots;
   }
-  return count;
+  *nslices = ns;
+  *nslots = slots;
+  *nirr = irr;
+}
+
+template <typename I, typename MV>
+static void sell_fill(int64_t n, const I *ip, const I *ix, const MV *dv, const std::vector<int64_t> &sptr,
+                      const std::vector<int32_t> &width, std::vector<I> &sidx, std::vector<MV> &sval) {
+  const int64_t ns = (int64_t)width.size();
+  const int64_t slots = sptr[ns];
+  sidx.assign(slots + 256, I(-1));
+  sval.assign(slots + 256, MV(0));
+  auto work = [&](int64_t sa, int64_t sb) {
+    for (int64_t s = sa; s < sb; ++s) {
+      if (width[s] < 0) continue;
+      const int64_t base = sptr[s];
+      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+      for (int64_t r = r0; r < r1; ++r) {
+        const int64_t lane = r - r0;
+        int64_t j = 0;
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e, ++j) {
+          sidx[base + j * kSlice + lane] = ix[e];
+          sval[base + j * kSlice + lane] = dv[e];
+        }
+      }
+    }
+  };
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 4096) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
+  for (auto &x : th) x.join();
 }
 
 template <typename V>
@@ -183,23 +219,63 @@ int kry_ctx_synchronize(kry_ctx *ctx) {
   KRY_API_END
 }
 
-int kry_csr_partition(int64_t n, const void *indptr, int itype, int64_t tile_nnz, int64_t tile_rows,
-                      int64_t *ntiles, int64_t *row_starts) {
+int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, int64_t *nslots,
+                   int64_t *nirregular) {
   KRY_API_BEGIN
-  KRY_REQUIRE(indptr && ntiles && n >= 0 && tile_nnz > 0 && tile_rows > 0, KRY_EINVAL,
-              "bad partition arguments");
-  std::vector<int64_t> rs;
-  int64_t cnt;
+  KRY_REQUIRE(indptr && nslices && nslots && nirregular && n >= 0, KRY_EINVAL, "bad layout arguments");
   if (itype == KRY_I32)
-    cnt = partition_rows(n, static_cast<const int32_t *>(indptr), tile_nnz, tile_rows, row_starts ? &rs : nullptr);
+    sell_plan(n, static_cast<const int32_t *>(indptr), nullptr, nullptr, nslices, nslots, nirregular);
   else if (itype == KRY_I64)
-    cnt = partition_rows(n, static_cast<const int64_t *>(indptr), tile_nnz, tile_rows, row_starts ? &rs : nullptr);
+    sell_plan(n, static_cast<const int64_t *>(indptr), nullptr, nullptr, nslices, nslots, nirregular);
   else
     throw Error{KRY_EINVAL, "bad itype"};
-  *ntiles = cnt;
-  if (row_starts) std::copy(rs.begin(), rs.end(), row_starts);
   KRY_API_END
 }
+
+}  // extern "C"
+
+namespace {
+template <typename I, typename MV>
+void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
+  hipStream_t st = A->ctx->stream;
+  const int64_t n = A->n, nnz = A->nnz;
+  KRY_REQUIRE(ip[0] == 0 && (int64_t)ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
+  for (int64_t r = 0; r < n; ++r)
+    KRY_REQUIRE(ip[r + 1] >= ip[r], KRY_EINVAL, "indptr must be non-decreasing");
+  std::vector<int64_t> sptr;
+  std::vector<int32_t> width;
+  sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
+  std::vector<I> sidx;
+  std::vector<MV> sval;
+  sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
+  A->sptr = dev_alloc(sptr.size() * 8);
+  A->swidth = dev_alloc(width.size() * 4 + 4);
+  A->sidx = dev_alloc(sidx.size() * sizeof(I));
+  A->sval = dev_alloc(sval.size() * sizeof(MV));
+  KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
+  if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
+  KRY_HIP(hipMemcpyAsync(A->sidx, sidx.data(), sidx.size() * sizeof(I), hipMemcpyHostToDevice, st));
+  KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+  if (A->nirregular > 0) {
+    A->indptr = dev_alloc((n + 1) * sizeof(I));
+    A->indices = dev_alloc((nnz + 1) * sizeof(I));
+    A->data = dev_alloc((nnz + 1) * sizeof(MV));
+    KRY_HIP(hipMemcpyAsync(A->indptr, ip, (n + 1) * sizeof(I), hipMemcpyHostToDevice, st));
+    if (nnz) {
+      KRY_HIP(hipMemcpyAsync(A->indices, ix, nnz * sizeof(I), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->data, dv, nnz * sizeof(MV), hipMemcpyHostToDevice, st));
+    }
+  }
+  KRY_HIP(hipStreamSynchronize(st));  // host staging vectors die at return
+}
+}  // namespace
+
+static void csr_free(kry_csr *A) {
+  void *bufs[] = {A->sptr, A->swidth, A->sidx, A->sval, A->indptr, A->indices, A->data};
+  for (void *b : bufs) dev_free(b);
+}
+
+extern "C" {
 
 int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
                    const void *data, int dtype, int itype, kry_csr **out) {
@@ -212,46 +288,27 @@ int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, con
                                     "int32 indices cannot address this matrix");
   KRY_HIP(hipSetDevice(ctx->device));
   auto *A = new kry_csr();
+  A->ctx = ctx;
+  A->n = n;
+  A->nnz = nnz;
+  A->dtype = dtype;
+  A->itype = itype;
+  static const int32_t zi32 = 0;
+  static const int64_t zi64 = 0;
+  static const double zd = 0;
   try {
-    A->ctx = ctx;
-    A->n = n;
-    A->nnz = nnz;
-    A->dtype = dtype;
-    A->itype = itype;
-    const size_t is = isize(itype), vs = dsize(dtype);
-    const int64_t nnz_pad = (nnz + 7) / 4 * 4;  // 16-byte loads may run 3 past the end
-    A->indptr = dev_alloc((n + 1) * is);
-    A->indices = dev_alloc(nnz_pad * is);
-    A->data = dev_alloc(nnz_pad * vs);
-    KRY_HIP(hipMemcpyAsync(A->indptr, indptr, (n + 1) * is, hipMemcpyHostToDevice, ctx->stream));
-    KRY_HIP(hipMemsetAsync(A->indices, 0, nnz_pad * is, ctx->stream));
-    KRY_HIP(hipMemsetAsync(A->data, 0, nnz_pad * vs, ctx->stream));
-    if (nnz) {
-      KRY_HIP(hipMemcpyAsync(A->indices, indices, nnz * is, hipMemcpyHostToDevice, ctx->stream));
-      KRY_HIP(hipMemcpyAsync(A->data, data, nnz * vs, hipMemcpyHostToDevice, ctx->stream));
-    }
-    std::vector<int64_t> rs;
-    if (itype == KRY_I32) {
-      const int32_t *ip = static_cast<const int32_t *>(indptr);
-      KRY_REQUIRE(ip[0] == 0 && ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
-      A->ntiles = partition_rows(n, ip, kTileNnz, kTileRows, &rs);
-      std::vector<int32_t> t(rs.begin(), rs.end());
-      A->tiles = dev_alloc(t.size() * 4);
-      KRY_HIP(hipMemcpyAsync(A->tiles, t.data(), t.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-      KRY_HIP(hipStreamSynchronize(ctx->stream));
-    } else {
-      const int64_t *ip = static_cast<const int64_t *>(indptr);
-      KRY_REQUIRE(ip[0] == 0 && ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
-      A->ntiles = partition_rows(n, ip, kTileNnz, kTileRows, &rs);
-      A->tiles = dev_alloc(rs.size() * 8);
-      KRY_HIP(hipMemcpyAsync(A->tiles, rs.data(), rs.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-      KRY_HIP(hipStreamSynchronize(ctx->stream));
-    }
+    const void *ix = nnz ? indices : (itype == KRY_I32 ? (const void *)&zi32 : (const void *)&zi64);
+    const void *dv = nnz ? data : (const void *)&zd;
+    if (itype == KRY_I32 && dtype == KRY_F64)
+      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const double *>(dv));
+    else if (itype == KRY_I32)
+      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const float *>(dv));
+    else if (dtype == KRY_F64)
+      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const double *>(dv));
+    else
+      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const float *>(dv));
   } catch (...) {
-    dev_free(A->indptr);
-    dev_free(A->indices);
-    dev_free(A->data);
-    dev_free(A->tiles);
+    csr_free(A);
     delete A;
     throw;
   }
@@ -264,10 +321,7 @@ int kry_csr_destroy(kry_csr *A) {
   if (!A) return KRY_OK;
   (void)hipSetDevice(A->ctx->device);
   (void)hipStreamSynchronize(A->ctx->stream);
-  dev_free(A->indptr);
-  dev_free(A->indices);
-  dev_free(A->data);
-  dev_free(A->tiles);
+  csr_free(A);
   delete A;
   KRY_API_END
 }

@@ -51,10 +51,10 @@ struct OpCgUpdate {
   __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
     constexpr int W = Vec16<V>::W;
     V yv[W], rv[W], pv[W], av[W];
-    VIO<V>::load(y, e, N, yv);
+    VIO<V>::load_nt(y, e, N, yv);   // y and Ap: streamed once per iteration
     VIO<V>::load(r, e, N, rv);
     VIO<V>::load(p, e, N, pv);
-    VIO<V>::load(Ap, e, N, av);
+    VIO<V>::load_nt(Ap, e, N, av);
 #pragma unroll
     for (int v = 0; v < W; ++v) {
       const V a = (V)alpha[(e + v) & (k - 1)];
@@ -67,8 +67,8 @@ struct OpCgUpdate {
         acc[v] += w ? dterm_w(rd, w[(e + v) / k], rd) : dterm(rd, rd);
       }
     }
-    VIO<V>::store(y, e, N, yv);
-    VIO<V>::store(r, e, N, rv);
+    VIO<V>::store_nt(y, e, N, yv);
+    VIO<V>::store(r, e, N, rv);  // r and p are the next SpMV's gather sources
   }
 };
 

@@ -13,10 +13,9 @@ namespace kry {
 
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kWave = 64;            // CDNA wavefront
-constexpr int kMaxGrid = 2048;       // persistent grid cap: 256 CUs x 8 blocks
+constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
-constexpr int kTileNnz = 2048;       // LDS product slots per SpMV tile
-constexpr int kTileRows = kBlock;    // rows per SpMV tile (one per thread)
+constexpr int kSlice = 64;           // SELL slice height = one wavefront
 constexpr int kNumXcd = 8;
 
 // ---------------------------------------------------------------- errors

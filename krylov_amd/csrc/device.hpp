@@ -25,11 +25,24 @@ __device__ __forceinline__ double dterm_w(double x, double w, double y) { return
 // The SpMV input x[j, c] may be materialised on the fly from other vectors
 // (the p-update of CG, the normalisation of GMRES), so the gather never
 // needs a separate pass over HBM. The owner row writes the same value out.
+// operator()(j, c) reads global column c; bind<KT>(c0) returns a copy for the
+// SpMV inner loop that serves local columns c0 + [0, KT) with any per-column
+// scalars held in registers.
 template <typename V>
 struct SrcPlain {
   const V *x;
   int k;
   __device__ __forceinline__ V operator()(int64_t j, int c) const { return x[j * k + c]; }
+  template <int KT>
+  struct Bound {
+    const V *x;
+    int k, c0;
+    __device__ __forceinline__ V operator()(int64_t j, int c) const { return x[j * k + c0 + c]; }
+  };
+  template <int KT>
+  __device__ __forceinline__ Bound<KT> bind(int c0) const {
+    return Bound<KT>{x, k, c0};
+  }
 };
 
 // p = r + omega * p_old (cg.py:178); first iteration p = r (cg.py:138).
@@ -47,6 +60,30 @@ struct SrcCgP {
     const V t = om * pold[j * k + c];
     return rj + t;
   }
+  template <int KT>
+  struct Bound {
+    const V *r, *pold;
+    V om[KT];
+    int k, c0, first;
+    __device__ __forceinline__ V operator()(int64_t j, int c) const {
+      const V rj = r[j * k + c0 + c];
+      if (first) return rj;
+      const V t = om[c] * pold[j * k + c0 + c];
+      return rj + t;
+    }
+  };
+  template <int KT>
+  __device__ __forceinline__ Bound<KT> bind(int c0) const {
+    Bound<KT> b;
+    b.r = r;
+    b.pold = pold;
+    b.k = k;
+    b.c0 = c0;
+    b.first = first;
+#pragma unroll
+    for (int c = 0; c < KT; ++c) b.om[c] = first ? V(0) : (V)omega[c0 + c];
+    return b;
+  }
 };
 
 // -------------------------------------------------------------- epilogues
@@ -56,7 +93,7 @@ template <typename V>
 struct EpiStore {
   V *y;
   int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s) const {
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     y[i * k + c] = s;
     return 0.0;
   }
@@ -69,7 +106,7 @@ struct EpiStoreDot {
   const V *q;
   const double *w;
   int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s) const {
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     y[i * k + c] = s;
     const double qv = (double)q[i * k + c];
     return w ? dterm_w(qv, w[i], (double)s) : dterm(qv, (double)s);
@@ -83,7 +120,7 @@ struct EpiResidual {
   V *r;
   const double *w;
   int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s) const {
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     const V ri = b[i * k + c] - s;
     r[i * k + c] = ri;
     const double rv = (double)ri;
@@ -99,10 +136,10 @@ struct EpiCgAp {
   SrcCgP<V> src;
   const double *w;
   int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s) const {
-    const V pi = src(i, c);
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
+    const V pi = xi;  // p_i, materialised by the bound source at row i
     pnew[i * k + c] = pi;
-    Ap[i * k + c] = s;
+    __builtin_nontemporal_store(s, Ap + i * k + c);  // read once, by the update pass
     const double pv = (double)pi;
     return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
   }
@@ -117,7 +154,7 @@ struct EpiLanczos {
   const double *h0;   // stored in the Lanczos dtype
   const double *w;
   int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s) const {
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     V o = s;
     if (pold) {
       const V t = (V)h0[c] * pold[i * k + c];
@@ -134,132 +171,111 @@ __device__ __forceinline__ bool halted(const Ctrl *ctrl, int step) {
   return ctrl != nullptr && step >= ctrl->stop_at;
 }
 
-// ------------------------------------------------- streaming SpMV (k = 1)
-// One persistent workgroup walks a contiguous run of row tiles (<= kTileNnz
-// nonzeros, <= 256 rows). Phase 1: all 256 lanes stream the tile's
-// (indices, data) with 16-byte loads and store data[e] * x[indices[e]] into
-// LDS. Phase 2: lane r sums row r's products sequentially from LDS. HBM sees
-// every matrix byte exactly once, coalesced; x gathers hit L2 (XCD-contiguous
-// tiles). A row longer than a tile is streamed through LDS in chunks and
-// summed by lane 0 (exact order kept).
-template <typename V, typename MV, typename I, class Src, class Epi>
-__global__ __launch_bounds__(kBlock) void spmv_stream_kernel(
-    const I *__restrict__ indptr, const I *__restrict__ indices, const MV *__restrict__ data,
-    const I *__restrict__ tiles, int64_t ntiles, Src src, Epi epi, double *__restrict__ part,
+// ------------------------------------------------------ SELL-64 SpMV
+// The operator is stored once, at upload, as SELL-64: rows in slices of 64
+// (one wavefront), each slice column-major with width = its longest row and
+// padding marked by column index -1. Lane r of a wave owns row r of the slice
+// and sums it sequentially over the slice columns, so:
+//  * every value / index load is one contiguous 64-lane access (HBM streamed
+//    once, no LDS staging, no barriers);
+//  * for stencil-like matrices lane r's gather x[col] sits next to lane r+1's
+//    (a few cache lines per wave-instruction, served from the XCD's L2);
+//  * the per-row summation order is the stored CSR order: bitwise
+//    csr_matvec / csr_matvecs.
+// Slices whose padding would exceed ~2x their nonzeros (very uneven rows) are
+// flagged irregular (width -1) and walked in CSR form by the same lanes.
+// k > 1 right-hand sides: each lane keeps KT column accumulators; for k > 8
+// the waves split into k/8 column groups.
+template <typename V, typename MV, typename I, int KT, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
+    const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
+    const MV *__restrict__ sval, int64_t nslices, int64_t n, int k, const I *__restrict__ indptr,
+    const I *__restrict__ indices, const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part,
     const Ctrl *ctrl, int step) {
-  if (halted(ctrl, step)) return;
-  __shared__ V prod[kTileNnz];
-  __shared__ double red[kBlock];
-  const int tid = threadIdx.x;
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t t_begin = ntiles * g / gridDim.x;
-  const int64_t t_end = ntiles * (g + 1) / gridDim.x;
-  double acc = 0.0;
-  for (int64_t t = t_begin; t < t_end; ++t) {
-    const int64_t r0 = tiles[t], r1 = tiles[t + 1];
-    const int64_t e0 = indptr[r0], e1 = indptr[r1];
-    if (e1 - e0 <= kTileNnz) {
-      const int64_t eb = e0 & ~int64_t(3);
-      for (int64_t e = eb + 4 * tid; e < e1; e += 4 * kBlock) {
-        I col[4];
-        V val[4];
-        if constexpr (sizeof(I) == 4) {
-          const int4 c4 = *reinterpret_cast<const int4 *>(indices + e);
-          col[0] = c4.x; col[1] = c4.y; col[2] = c4.z; col[3] = c4.w;
-        } else {
-          const longlong2 a = *reinterpret_cast<const longlong2 *>(indices + e);
-          const longlong2 b = *reinterpret_cast<const longlong2 *>(indices + e + 2);
-          col[0] = a.x; col[1] = a.y; col[2] = b.x; col[3] = b.y;
-        }
-        if constexpr (sizeof(MV) == 8) {
-          const double2 a = *reinterpret_cast<const double2 *>(data + e);
-          const double2 b = *reinterpret_cast<const double2 *>(data + e + 2);
-          val[0] = a.x; val[1] = a.y; val[2] = b.x; val[3] = b.y;
-        } else {
-          const float4 a = *reinterpret_cast<const float4 *>(data + e);
-          val[0] = (V)a.x; val[1] = (V)a.y; val[2] = (V)a.z; val[3] = (V)a.w;
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int64_t ee = e + v;
-          if (ee >= e0 && ee < e1) prod[ee - e0] = val[v] * src(col[v], 0);
-        }
-      }
-      __syncthreads();
-      const int nr = (int)(r1 - r0);
-      if (tid < nr) {
-        const int64_t row = r0 + tid;
-        const int a = (int)(indptr[row] - e0), b = (int)(indptr[row + 1] - e0);
-        V s = 0;
-        for (int e = a; e < b; ++e) s = s + prod[e];
-        acc += epi(row, 0, s);
-      }
-      __syncthreads();
-    } else {
-      // a single long row: chunked through LDS, sequential sum by lane 0
-      V s = 0;
-      for (int64_t cb = e0; cb < e1; cb += kTileNnz) {
-        const int64_t ce = cb + kTileNnz < e1 ? cb + kTileNnz : e1;
-        for (int64_t e = cb + tid; e < ce; e += kBlock) prod[e - cb] = (V)data[e] * src(indices[e], 0);
-        __syncthreads();
-        if (tid == 0)
-          for (int e = 0; e < (int)(ce - cb); ++e) s = s + prod[e];
-        __syncthreads();
-      }
-      if (tid == 0) acc += epi(r0, 0, s);
-    }
-  }
-  if (part != nullptr) {
-    red[tid] = acc;
-    block_tree_reduce(red, kBlock, 1);
-    if (tid == 0) part[g] = red[0];
-  }
-}
-
-// ------------------------------------------- row-major block SpMV (k >= 2)
-// Thread per (row, chunk of KT columns): y[i, c0:c0+KT] accumulated in
-// registers in stored nonzero order (csr_matvecs semantics), the row's
-// nonzeros loaded once per chunk, x rows (k contiguous values) gathered.
-template <typename V, typename MV, typename I, int KT, class Src, class Epi>
-__global__ __launch_bounds__(kBlock) void spmv_rows_kernel(
-    const I *__restrict__ indptr, const I *__restrict__ indices, const MV *__restrict__ data,
-    int64_t n, int k, Src src, Epi epi, double *__restrict__ part, const Ctrl *ctrl, int step) {
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock * KT];
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int nch = k / KT;
-  const int64_t total = n * nch;
-  const int64_t per = ((total + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
-  const int64_t q0 = per * g;
-  const int64_t q1 = q0 + per < total ? q0 + per : total;
-  double acc[KT];
+  const int nch = k / KT;                        // column groups (1 unless k > 8)
+  const int64_t W = (int64_t)gridDim.x * 4 / nch;  // waves per column group
+  const int64_t wg = (int64_t)g * 4 + wid;
+  const int ch = (int)(wg % nch);
+  const int64_t m = wg / nch;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const int c0 = ch * KT;
+  const auto bs = src.template bind<KT>(c0);
+  double dacc[KT];
 #pragma unroll
-  for (int c = 0; c < KT; ++c) acc[c] = 0.0;
-  for (int64_t q = q0 + tid; q < q1; q += kBlock) {
-    const int64_t row = q / nch;
-    const int c0 = (int)(q % nch) * KT;
-    V s[KT];
+  for (int c = 0; c < KT; ++c) dacc[c] = 0.0;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t row = s * 64 + lane;
+    V acc[KT];
 #pragma unroll
-    for (int c = 0; c < KT; ++c) s[c] = 0;
-    const int64_t eb = indptr[row], ee = indptr[row + 1];
-    for (int64_t e = eb; e < ee; ++e) {
-      const int64_t j = indices[e];
-      const V a = (V)data[e];
+    for (int c = 0; c < KT; ++c) acc[c] = V(0);
+    if (w >= 0) {
+      const I *ci = sidx + sptr[s] + lane;
+      const MV *cv = sval + sptr[s] + lane;
+      for (int j0 = 0; j0 < w; j0 += UNR) {
+        I col[UNR];
+        V a[UNR];
 #pragma unroll
-      for (int c = 0; c < KT; ++c) {
-        const V t = a * src(j, c0 + c);
-        s[c] = s[c] + t;
+        for (int u = 0; u < UNR; ++u) {
+          const bool in = j0 + u < w;
+          col[u] = in ? __builtin_nontemporal_load(ci + (int64_t)(j0 + u) * 64) : I(-1);
+          a[u] = in ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
+        }
+        V xv[UNR][KT];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+          for (int c = 0; c < KT; ++c) xv[u][c] = col[u] >= 0 ? bs(col[u], c) : V(0);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (col[u] >= 0) {
+#pragma unroll
+            for (int c = 0; c < KT; ++c) {
+              const V p = a[u] * xv[u][c];
+              acc[c] = acc[c] + p;
+            }
+          }
+      }
+    } else if (row < n) {
+      for (I e = indptr[row]; e < indptr[row + 1]; ++e) {
+        const I j = indices[e];
+        const V a = (V)data[e];
+#pragma unroll
+        for (int c = 0; c < KT; ++c) {
+          const V p = a * bs(j, c);
+          acc[c] = acc[c] + p;
+        }
       }
     }
+    if (row < n) {
 #pragma unroll
-    for (int c = 0; c < KT; ++c) acc[c] += epi(row, c0 + c, s[c]);
+      for (int c = 0; c < KT; ++c) dacc[c] += epi(row, c0 + c, acc[c], bs(row, c));
+    }
   }
   if (part != nullptr) {
 #pragma unroll
-    for (int c = 0; c < KT; ++c) red[tid * KT + c] = acc[c];
-    block_tree_reduce(red, kBlock * KT, k);
-    if (tid < k) part[(int64_t)g * k + tid] = red[tid];
+    for (int c = 0; c < KT; ++c) red[tid * KT + c] = dacc[c];
+    if (nch == 1) {
+      block_tree_reduce(red, kBlock * KT, k);
+      if (tid < k) part[(int64_t)g * k + tid] = red[tid];
+    } else {
+      // column group of wave w in this block: (g*4 + w) % nch; fixed order
+      __syncthreads();
+      double sum = 0.0;
+      if (tid < k) {
+        const int cg = tid / KT, cc = tid % KT;
+        for (int t = 0; t < kBlock; ++t)
+          if ((int)(((int64_t)g * 4 + (t >> 6)) % nch) == cg) sum += red[t * KT + cc];
+      }
+      __syncthreads();
+      if (tid < k) part[(int64_t)g * k + tid] = sum;
+    }
   }
 }
 
@@ -311,6 +327,32 @@ struct VIO {
       for (int v = 0; v < W; ++v) o[v] = e + v < N ? p[e + v] : V(0);
     }
   }
+  // non-temporal forms for streams nobody re-reads soon (keeps the vectors the
+  // next SpMV gathers resident in L2 / MALL)
+  __device__ __forceinline__ static void load_nt(const V *p, int64_t e, int64_t N, V (&o)[W]) {
+    if (e + W <= N) {
+      typedef V vec_t __attribute__((ext_vector_type(W)));
+      const vec_t t = __builtin_nontemporal_load(reinterpret_cast<const vec_t *>(p + e));
+#pragma unroll
+      for (int v = 0; v < W; ++v) o[v] = t[v];
+    } else {
+#pragma unroll
+      for (int v = 0; v < W; ++v) o[v] = e + v < N ? p[e + v] : V(0);
+    }
+  }
+  __device__ __forceinline__ static void store_nt(V *p, int64_t e, int64_t N, const V (&o)[W]) {
+    if (e + W <= N) {
+      typedef V vec_t __attribute__((ext_vector_type(W)));
+      vec_t t;
+#pragma unroll
+      for (int v = 0; v < W; ++v) t[v] = o[v];
+      __builtin_nontemporal_store(t, reinterpret_cast<vec_t *>(p + e));
+    } else {
+#pragma unroll
+      for (int v = 0; v < W; ++v)
+        if (e + v < N) p[e + v] = o[v];
+    }
+  }
   __device__ __forceinline__ static void store(V *p, int64_t e, int64_t N, const V (&o)[W]) {
     if (e + W <= N) {
       if constexpr (W == 2) {
@@ -334,7 +376,18 @@ __device__ __forceinline__ void reduce_partials(const double *part, int P, int k
   const int c = tid & (k - 1);
   const int step = kBlock / k;
   double s = 0.0;
-  for (int p = tid / k; p < P; p += step) s += part[(int64_t)p * k + c];
+  // loads issued 8 at a time (independent), added in the fixed sequential
+  // order: latency of one L2 round trip per 8 partials, same bits as a plain
+  // loop
+  int p = tid / k;
+  for (; p + 7 * step < P; p += 8 * step) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(p + u * step) * k + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; p < P; p += step) s += part[(int64_t)p * k + c];
   red[tid] = s;
   block_tree_reduce(red, kBlock, k);
 }
@@ -392,36 +445,36 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
 }
 
 // -------------------------------------------------------- host launchers
+template <typename V, typename MV, typename I, int KT, int UNR, class Src, class Epi>
+int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
+                hipStream_t st) {
+  const int nch = k / KT;
+  int64_t waves = A->nslices * nch;
+  int grid = (int)((waves + 3) / 4);
+  if (grid > kMaxGrid) grid = kMaxGrid;
+  if (grid < 1) grid = 1;
+  if (nch > 1) grid = (grid + 7) / 8 * 8;  // 4 * grid must be a multiple of nch (<= 32)
+  if (grid > kMaxGrid) grid = kMaxGrid;
+  hipLaunchKernelGGL((spmv_sell_kernel<V, MV, I, KT, UNR, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
+                     static_cast<const int64_t *>(A->sptr), static_cast<const int *>(A->swidth),
+                     static_cast<const I *>(A->sidx), static_cast<const MV *>(A->sval), A->nslices, A->n, k,
+                     static_cast<const I *>(A->indptr), static_cast<const I *>(A->indices),
+                     static_cast<const MV *>(A->data), src, epi, part, ctrl, step);
+  return grid;
+}
+
+// y-side epilogue Epi / x-side source Src composition of one SpMV launch;
+// returns the number of block partials written to `part` (if non-null).
 template <typename V, typename MV, typename I, class Src, class Epi>
-void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *grid_out,
-                 const Ctrl *ctrl, int step, hipStream_t st) {
-  const I *ip = static_cast<const I *>(A->indptr);
-  const I *ix = static_cast<const I *>(A->indices);
-  const MV *dv = static_cast<const MV *>(A->data);
+void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *grid_out, const Ctrl *ctrl,
+                 int step, hipStream_t st) {
+  KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
-  if (k == 1) {
-    grid = (int)(A->ntiles < kMaxGrid ? A->ntiles : kMaxGrid);
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((spmv_stream_kernel<V, MV, I, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, ip, ix,
-                       dv, static_cast<const I *>(A->tiles), A->ntiles, src, epi, part, ctrl, step);
-  } else {
-    const int KT = k >= 8 ? 8 : k;
-    const int64_t total = A->n * (k / KT);
-    grid = grid_for(total, kBlock * 2);
-    switch (KT) {
-      case 2:
-        hipLaunchKernelGGL((spmv_rows_kernel<V, MV, I, 2, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, ip,
-                           ix, dv, A->n, k, src, epi, part, ctrl, step);
-        break;
-      case 4:
-        hipLaunchKernelGGL((spmv_rows_kernel<V, MV, I, 4, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, ip,
-                           ix, dv, A->n, k, src, epi, part, ctrl, step);
-        break;
-      default:
-        hipLaunchKernelGGL((spmv_rows_kernel<V, MV, I, 8, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, ip,
-                           ix, dv, A->n, k, src, epi, part, ctrl, step);
-        break;
-    }
+  switch (k) {
+    case 1: grid = launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st); break;
+    case 2: grid = launch_sell<V, MV, I, 2, 8>(A, k, src, epi, part, ctrl, step, st); break;
+    case 4: grid = launch_sell<V, MV, I, 4, 4>(A, k, src, epi, part, ctrl, step, st); break;
+    default: grid = launch_sell<V, MV, I, 8, 4>(A, k, src, epi, part, ctrl, step, st); break;
   }
   KRY_HIP(hipGetLastError());
   if (grid_out) *grid_out = grid;

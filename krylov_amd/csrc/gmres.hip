@@ -27,7 +27,7 @@ struct kry_gmres {
   size_t vstride = 0;  // elements per basis vector (padded)
   void *b = nullptr, *x0 = nullptr, *V = nullptr, *wv = nullptr, *xk = nullptr, *rt = nullptr;
   double *w = nullptr;
-  double *part = nullptr;
+  double *part = nullptr, *part1 = nullptr, *part2 = nullptr;  // partial rows (MGS ping-pong)
   double *scal = nullptr;  // alpha[k], hsafe[k], crit[k], tmp[k]
   double *h = nullptr;     // (maxiter + 2) x k, current Arnoldi column
   double *R = nullptr;     // (maxiter + 1) x maxiter x k
@@ -79,6 +79,66 @@ struct OpMgs {
     VIO<V>::store(w, e, N, wv);
   }
 };
+
+// One MGS pass j (arnoldi.py:159-162) in a single launch: every block first
+// reduces the previous pass's partials into alpha_j = <V_j, w> (fixed order,
+// identical in every block), block 0 records h[j] += alpha_j, then the block
+// applies w -= alpha_j V_j to its span and emits partials of the next inner
+// product (<V_{j+1}, w>, <V_0, w> for the next sweep, or <w, w>).
+template <typename V>
+__global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__restrict__ w,
+                                                        const V *__restrict__ Vj, const V *__restrict__ q,
+                                                        const double *__restrict__ part_in, int P_in,
+                                                        double *__restrict__ part_out, double *__restrict__ h, int j,
+                                                        int first_sweep, const double *__restrict__ wt,
+                                                        const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  __shared__ double red[kBlock * W];
+  __shared__ double alpha[kMaxCols];
+  const int tid = threadIdx.x;
+  reduce_partials(part_in, P_in, k, red);
+  if (tid < k) {
+    const V a = (V)red[tid];
+    alpha[tid] = (double)a;
+    if (blockIdx.x == 0) {
+      const V prev = first_sweep ? V(0) : (V)h[(int64_t)j * k + tid];
+      h[(int64_t)j * k + tid] = (double)(prev + a);
+    }
+  }
+  __syncthreads();
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t ngrp = (N + W - 1) / W;
+  const int64_t per = ((ngrp + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+  const int64_t v0 = per * g;
+  const int64_t v1 = v0 + per < ngrp ? v0 + per : ngrp;
+  double acc[W];
+#pragma unroll
+  for (int v = 0; v < W; ++v) acc[v] = 0.0;
+  for (int64_t gi = v0 + tid; gi < v1; gi += kBlock) {
+    const int64_t e = gi * W;
+    V wv[W], vj[W], qv[W];
+    VIO<V>::load(w, e, N, wv);
+    VIO<V>::load(Vj, e, N, vj);
+    if (q) VIO<V>::load(q, e, N, qv);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V t = (V)alpha[(e + v) & (k - 1)] * vj[v];
+      wv[v] = wv[v] - t;  // Av -= alpha * P[j]
+      if (e + v < N) {
+        const double a = q ? (double)qv[v] : (double)wv[v];
+        const double b = (double)wv[v];
+        acc[v] += wt ? dterm_w(a, wt[(e + v) / k], b) : dterm(a, b);
+      }
+    }
+    VIO<V>::store(w, e, N, wv);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < W; ++v) red[tid * W + v] = acc[v];
+  block_tree_reduce(red, kBlock * W, k);
+  if (tid < k) part_out[(int64_t)g * k + tid] = red[tid];
+}
 
 // out = src / hsafe  (arnoldi.py:193-195, the guarded normalisation)
 template <typename V>
@@ -342,18 +402,30 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
       ProfScope ps(s->ctx, PROF_SPMV);
       launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{Vk, k}, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step, st);
     }
+    // the SpMV's partials of <V_0, w> -> one value per column, so every MGS
+    // block reduces a single partial row for its first coefficient
+    hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->part1);
+    const double *pin = s->part1;
+    int Pin = 1;
+    double *pbuf[2] = {s->part, s->part2};
+    int flip = 0;
+    const int64_t ngrp = (N + Vec16<V>::W - 1) / Vec16<V>::W;
+    const int Gm = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ngrp + 1023) / 1024));
     for (int sw = 0; sw < s->sweeps; ++sw) {
       for (int j = 0; j <= col; ++j) {
-        hipLaunchKernelGGL(gm_coef_kernel<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->h, j,
-                           sw == 0 ? 1 : 0, s->ctrl, step);
         const V *Vj = basis<V>(s->V, s->vstride, j);
         const V *q = j < col ? basis<V>(s->V, s->vstride, j + 1) : (sw + 1 < s->sweeps ? V0 : nullptr);
+        double *pout = pbuf[flip];
         ProfScope ps(s->ctx, PROF_MGS);
-        P = launch_elementwise<V>(N, k, OpMgs<V>{w, Vj, q, s->scal + G_ALPHA * k, s->w, k}, s->part, s->ctrl, step,
-                                  st);
+        hipLaunchKernelGGL(gm_mgs_kernel<V>, dim3(Gm), dim3(kBlock), 0, st, N, k, w, Vj, q, pin, Pin, pout, s->h, j,
+                           sw == 0 ? 1 : 0, s->w, s->ctrl, step);
+        pin = pout;
+        Pin = Gm;
+        flip ^= 1;
       }
     }
-    hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->h, s->R, s->y,
+    P = Pin;
+    hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, pin, P, k, s->scal, s->h, s->R, s->y,
                        s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
     KRY_HIP(hipGetLastError());
     // V_{col+1} = w / guard(h[col+1]) unless invariant; the kernel runs for
@@ -400,7 +472,7 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 }
 
 void gm_free(kry_gmres *s) {
-  void *bufs[] = {s->b, s->x0, s->V, s->wv, s->xk, s->rt, s->w, s->part, s->scal, s->h, s->R, s->y,
+  void *bufs[] = {s->b, s->x0, s->V, s->wv, s->xk, s->rt, s->w, s->part, s->part1, s->part2, s->scal, s->h, s->R, s->y,
                   s->Gc, s->Gs, s->yy, s->hist, s->ctrl};
   for (void *b : bufs) dev_free(b);
 }
@@ -450,6 +522,8 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     KRY_HIP(hipMemsetAsync(s->xk, 0, vb, ctx->stream));
     KRY_HIP(hipMemsetAsync(s->wv, 0, vb, ctx->stream));
     s->part = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
+    s->part1 = static_cast<double *>(dev_alloc((size_t)k * 8));
+    s->part2 = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
     s->scal = static_cast<double *>(dev_alloc(G_COUNT * (size_t)k * 8));
     s->h = static_cast<double *>(dev_alloc(((size_t)maxiter + 2) * k * 8));
     s->R = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8));

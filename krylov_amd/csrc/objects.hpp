@@ -25,11 +25,16 @@ struct kry_csr {
   kry_ctx *ctx = nullptr;
   int64_t n = 0, nnz = 0;
   int dtype = 0, itype = 0;
-  void *indptr = nullptr;   // itype, n + 1
-  void *indices = nullptr;  // itype, nnz padded to a multiple of 4 (zeros)
-  void *data = nullptr;     // dtype, nnz padded to a multiple of 4 (zeros)
-  void *tiles = nullptr;    // itype, ntiles + 1 row starts (streaming kernel)
-  int64_t ntiles = 0;
+  // SELL-64 image (device): slice s covers rows [64 s, 64 s + 64)
+  int64_t nslices = 0, nslots = 0, nirregular = 0;
+  void *sptr = nullptr;     // int64, nslices + 1 slot offsets
+  void *swidth = nullptr;   // int32, slice width, -1 = irregular (CSR walk)
+  void *sidx = nullptr;     // itype, nslots (+ pad), -1 = padding
+  void *sval = nullptr;     // dtype, nslots (+ pad)
+  // CSR arrays, kept on the device only when irregular slices exist
+  void *indptr = nullptr;
+  void *indices = nullptr;
+  void *data = nullptr;
 };
 
 struct kry_vec {

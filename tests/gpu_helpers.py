@@ -59,17 +59,25 @@ def assert_consistent(A, b, info, sol, tol):
     assert np.asarray(info.resnorms).shape == (info.numsteps + 1, *b.shape[1:])
 
 
-def assert_parity(info, d, prefix, rtol=1e-10, xtol=1e-9, final_atol=None):
+def assert_parity(info, d, prefix, rtol=1e-10, xtol=1e-9, final_atol=None, prefix_steps=None, tail_rtol=None):
     """Device run vs the reference fixture: identical step count and success,
     updated-residual history within rtol, final explicit residual within an
-    absolute round-off bound, solution within xtol."""
+    absolute round-off bound, solution within xtol.
+
+    prefix_steps / tail_rtol: for problems whose history is chaotic in the
+    summation order of the inner products (documented per test), check the
+    first prefix_steps entries at rtol and the rest at tail_rtol."""
     assert info.numsteps == int(d[prefix + "_numsteps"])
     assert info.success == bool(d[prefix + "_success"])
     got = np.asarray(info.resnorms, dtype=np.float64)
     ref = d[prefix + "_resnorms"]
     assert got.shape == ref.shape
     rel = np.abs(got[:-1] - ref[:-1]) / np.maximum(np.abs(ref[:-1]), 1e-300)
-    assert np.all(rel <= rtol), (np.max(rel), int(np.argmax(rel)))
+    if prefix_steps is None:
+        assert np.all(rel <= rtol), (np.max(rel), int(np.argmax(rel)))
+    else:
+        assert np.all(rel[:prefix_steps] <= rtol), (np.max(rel[:prefix_steps]), int(np.argmax(rel[:prefix_steps])))
+        assert np.all(rel[prefix_steps:] <= tail_rtol), (np.max(rel[prefix_steps:]),)
     if final_atol is None:
         final_atol = 1e-12 * np.max(np.abs(ref[0])) + 1e-300
     assert np.all(np.abs(got[-1] - ref[-1]) <= final_atol)

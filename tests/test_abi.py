@@ -1,5 +1,5 @@
 """The C-ABI library loads, exports every symbol include/krylov_hip.h declares,
-and its host-only logic (tile partition, error mapping) is right. CPU only:
+and its host-only logic (SELL-64 layout plan, error mapping) is right. CPU only:
 no kernel is launched here."""
 import ctypes
 import os
@@ -57,52 +57,56 @@ def test_no_device_fails_loudly():
         Context(0)
 
 
-def _partition(indptr, tile_nnz, tile_rows):
+def _layout(indptr):
     from krylov_amd import _lib
 
-    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indptr = np.ascontiguousarray(indptr)
+    it = _lib.KRY_I32 if indptr.dtype == np.int32 else _lib.KRY_I64
+    ns, slots, irr = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib.kry_csr_layout(indptr.shape[0] - 1, _lib.ptr(indptr), it, ctypes.byref(ns),
+                                        ctypes.byref(slots), ctypes.byref(irr)))
+    return ns.value, slots.value, irr.value
+
+
+def _layout_py(indptr):
+    """Restatement of the SELL-64 plan: slices of 64 rows, width = longest
+    row, irregular when 64 * width > 2 * nnz_slice + 1024."""
     n = indptr.shape[0] - 1
-    cnt = ctypes.c_int64()
-    _lib.check(_lib.lib.kry_csr_partition(n, _lib.ptr(indptr), _lib.KRY_I64, tile_nnz, tile_rows,
-                                           ctypes.byref(cnt), None))
-    rs = np.zeros(cnt.value + 1, dtype=np.int64)
-    _lib.check(_lib.lib.kry_csr_partition(n, _lib.ptr(indptr), _lib.KRY_I64, tile_nnz, tile_rows,
-                                           ctypes.byref(cnt), rs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
-    return rs
+    ns = (n + 63) // 64
+    slots = irr = 0
+    for s in range(ns):
+        r0, r1 = 64 * s, min(n, 64 * s + 64)
+        lens = np.diff(indptr[r0:r1 + 1])
+        w = int(lens.max()) if len(lens) else 0
+        if 64 * w > 2 * int(indptr[r1] - indptr[r0]) + 1024:
+            irr += 1
+        else:
+            slots += 64 * w
+    return ns, slots, irr
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_partition_invariants(seed):
+def test_sell_layout_matches_restatement(seed):
     rng = np.random.default_rng(seed)
     n = 5000
     lens = rng.integers(0, 40, n)
     lens[rng.choice(n, 5, replace=False)] = rng.integers(2049, 9000, 5)  # long rows
-    indptr = np.concatenate([[0], np.cumsum(lens)])
-    rs = _partition(indptr, 2048, 256)
-    assert rs[0] == 0 and rs[-1] == n
-    assert np.all(np.diff(rs) >= 1)
-    for a, b in zip(rs[:-1], rs[1:]):
-        nnz = indptr[b] - indptr[a]
-        if b - a == 1 and nnz > 2048:
-            continue  # a long row alone in its tile
-        assert nnz <= 2048 and b - a <= 256
-    # maximality: a tile could not have taken its next row
-    for a, b in zip(rs[:-2], rs[1:-1]):
-        if b - a == 1 and indptr[b] - indptr[a] > 2048:
-            continue
-        assert b - a == 256 or indptr[b + 1] - indptr[a] > 2048
+    indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    got = _layout(indptr)
+    assert got == _layout_py(indptr)
+    assert got[2] >= 1  # the long rows make their slices irregular
+    assert _layout(indptr.astype(np.int32)) == got
 
 
-def test_partition_int32_matches_int64():
-    from krylov_amd import _lib, problems
+def test_sell_layout_of_stencils_is_regular():
+    from krylov_amd import problems
 
-    A = problems.poisson2d(40)
-    cnt32 = ctypes.c_int64()
-    ip32 = np.ascontiguousarray(A.indptr, dtype=np.int32)
-    _lib.check(_lib.lib.kry_csr_partition(A.shape[0], _lib.ptr(ip32), _lib.KRY_I32, 2048, 256,
-                                           ctypes.byref(cnt32), None))
-    rs = _partition(A.indptr, 2048, 256)
-    assert cnt32.value == len(rs) - 1
+    for A in (problems.poisson2d(40), problems.stencil15_3d(12)):
+        ns, slots, irr = _layout(A.indptr)
+        assert irr == 0
+        assert ns == (A.shape[0] + 63) // 64
+        assert A.nnz <= slots <= 1.2 * A.nnz
+        assert (ns, slots, irr) == _layout_py(A.indptr)
 
 
 def test_error_mapping():
@@ -110,7 +114,7 @@ def test_error_mapping():
     from krylov_amd.errors import ArgumentError
 
     with pytest.raises(ValueError):
-        _lib.check(_lib.lib.kry_csr_partition(-1, None, _lib.KRY_I32, 1, 1, None, None))
+        _lib.check(_lib.lib.kry_csr_layout(-1, None, _lib.KRY_I32, None, None, None))
     with pytest.raises(ArgumentError):
         _lib.check(_lib.KRY_EINVARIANT)
     with pytest.raises(np.linalg.LinAlgError):
