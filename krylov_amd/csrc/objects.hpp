@@ -31,6 +31,14 @@ struct kry_csr {
   void *swidth = nullptr;   // int32, slice width, -1 = irregular (CSR walk)
   void *sidx = nullptr;     // itype, nslots (+ pad), -1 = padding
   void *sval = nullptr;     // dtype, nslots (+ pad)
+  // x-window image (single-RHS SpMV): groups of kGroupSlices slices whose x
+  // footprint fits LDS; sloc holds group-local column indices
+  int64_t ngroups = 0, nwindowed = 0;
+  void *gwin = nullptr;     // int32, ngroups + 1 offsets into the window list
+  void *wstart = nullptr;   // int64 first column of each window
+  void *wlen = nullptr;     // int32 window length
+  void *wlofs = nullptr;    // int32 window offset in the group's LDS image
+  void *sloc = nullptr;     // int32, nslots (+ pad): LDS index per slot
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;

@@ -172,6 +172,7 @@ int main(int argc, char **argv) {
   printf("upload + SELL-64 build %.2fs: %ld slices, %ld slots (%.2f%% padding), %ld irregular\n",
          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), A->nslices, A->nslots,
          100.0 * (A->nslots - nnz) / nnz, A->nirregular);
+  printf("x-window groups: %ld of %ld windowed\n", A->nwindowed, A->ngroups);
 
   double *d_x, *d_y, *d_p, *d_ap, *d_om, *d_out, *part;
   CK(hipMalloc(&d_x, n * 8));
