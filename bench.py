@@ -2,20 +2,23 @@
 
 Workload (BASELINE.json metric): CG on the 3-D 15-point stencil
 216^3 (n = 10,077,696, nnz = 149,770,936, fp64, int32 indices), b = ones,
-tol = 0 (fixed iteration count). One step = one CG iteration (one fused
-p-update + SpMV + <p,Ap>, one fused x/r update + <r,r>, two scalar kernels).
+tol = 0 (fixed iteration count). One step = one CG iteration: one fused
+p-update + SpMV + <p,Ap> launch, one fused x/r update + <r,r> launch and two
+one-block scalar kernels, no host sync inside a 32-iteration chunk.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--quick]
 
 N > 1 (launched by torch.distributed.run): each rank solves its own RHS
-column of the same matrix on its own GPU (RHS sharding) and
-every iteration performs one RCCL allreduce of the residual-norm vector for
-the global stop test; value = total RHS-iterations per second (weak scaling).
+column of the same matrix on its own GPU (RHS sharding) with
+one RCCL allreduce of the residual-norm vector per iteration for the global
+stop rule; value = total RHS-iterations per second (weak scaling).
 
-Extra fields: the live SpMV roofline (HIP events around every SpMV launch of
-the timed region), GMRES(30) iterations/s on the cfg3 matrix (N = 1), and
-the CPU baseline (the oracle: the reference's iteration on NumPy/SciPy) on a
-bounded sample of the same workload (rank 0, N = 1 only).
+Also reported (N = 1): the live SpMV roofline (HIP events around every SpMV
+launch of the timed region), GMRES(30) on the cfg3 matrix, the secondary
+BASELINE configs (cfg2 CG Poisson 1000^2, cfg4 block CG 8 RHS on Poisson
+3163^2, cfg5 weighted fp32 MINRES 200^3), and the CPU baseline: the oracle
+(the reference iteration on NumPy/SciPy) on a bounded sample of the metric
+workload, rank 0 only.
 """
 import argparse
 import json
@@ -31,24 +34,26 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def spmv_fused_bytes(n, nnz, vb=8, ib=4):
-    """Algorithmic bytes of one fused CG SpMV launch: the matrix once
-    (nnz*(vb+ib) + (n+1)*ib), plus r and p_old read (the gather builds
-    p = r + omega p_old) and p, Ap written: S + 2 n vb with SURVEY's
-    S = nnz(vb+ib) + (n+1) ib + 2 n vb."""
-    return nnz * (vb + ib) + (n + 1) * ib + 4 * n * vb
+def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
+    """S = nnz (vb + ib) + (n + 1) ib + 2 n k vb."""
+    mvb = vb if mvb is None else mvb
+    return nnz * (mvb + ib) + (n + 1) * ib + 2 * n * k * vb
 
 
-def cg_iteration_bytes(n, nnz, vb=8, ib=4):
-    """Algorithmic bytes of one CG iteration as implemented: fused SpMV
-    (above) + update pass (read y, r, p, Ap; write y, r = 6 n vb)."""
-    return spmv_fused_bytes(n, nnz, vb, ib) + 6 * n * vb
+def spmv_fused_bytes(n, nnz, k=1, vb=8, ib=4):
+    """One fused CG SpMV launch: S with x replaced by (r, p_old) read and
+    (p, Ap) written: S + 2 n k vb."""
+    return spmv_S(n, nnz, k, vb, ib) + 2 * n * k * vb
+
+
+def cg_iteration_bytes(n, nnz, k=1, vb=8, ib=4):
+    """Fused SpMV launch + update pass (read y, r, p, Ap; write y, r)."""
+    return spmv_fused_bytes(n, nnz, k, vb, ib) + 6 * n * k * vb
 
 
 def gmres_cycle_bytes(n, nnz, m=30, vb=8, ib=4):
-    """Per 30-step cycle: 31 S + (1950 + 37) n vb."""
-    S = nnz * (vb + ib) + (n + 1) * ib + 2 * n * vb
-    return (m + 1) * S + (1950 + 37) * n * vb
+    """Per m-step cycle: (m + 1) S + (1950 + 37) n vb."""
+    return (m + 1) * spmv_S(n, nnz) + (1950 + 37) * n * vb
 
 
 def dist_setup():
@@ -60,7 +65,7 @@ def dist_setup():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
         pg = dist
     return world, rank, local, pg
 
@@ -80,64 +85,48 @@ def allmax(pg, x):
     return float(t.item())
 
 
-def make_comm(pg, ctx, world, rank):
-    import ctypes
-
-    from krylov_amd import _lib
-
-    idbuf = np.zeros(128, dtype=np.uint8)
-    if rank == 0:
-        _lib.check(_lib.lib.kry_comm_unique_id(_lib.ptr(idbuf)))
-    import torch
-
-    t = torch.from_numpy(idbuf.astype(np.int64))
-    pg.broadcast(t, src=0)
-    idbuf = t.numpy().astype(np.uint8)
-    h = ctypes.c_void_p()
-    _lib.check(_lib.lib.kry_comm_create(ctx.handle, world, rank, _lib.ptr(idbuf), ctypes.byref(h)))
-    return h
-
-
-def run_cg(A_host, steps, warmup, world, rank, local, pg):
-    import ctypes
-
-    import krylov_amd
+def _cg_state(A, B, comm=None, rank=0, world=1):
+    """Device CG state on the product path (krylov_amd.cg's engine), with the
+    RCCL communicator attached when sharded."""
     from krylov_amd import _helpers, _lib
     from krylov_amd.cg import _CGState
+
+    prob = _helpers.Problem(A, B, None, None)
+    st = _CGState(prob)
+    ncols = prob.kpad
+    if comm is not None:
+        _lib.check(_lib.lib.kry_cg_attach_comm(st.h, comm.handle, rank * prob.kpad, world * prob.kpad))
+        ncols = world * prob.kpad
+    st.start()
+    st.set_criterion(np.zeros(ncols))  # tol = atol = 0: never converges -> fixed steps
+    return st, ncols
+
+
+def _iterate(st, k, ncols, chunk=32):
+    done = 0
+    while done < k:
+        s = min(chunk, k - done)
+        hist = st.run(s, ncols)
+        assert len(hist) == s, "solver stopped early"
+        done += s
+
+
+def run_metric(A_host, steps, warmup, world, rank, local, pg):
+    import krylov_amd
+    from krylov_amd import _lib, distributed
     from krylov_amd.device import get_context
 
     ctx = get_context(local)
     A = krylov_amd.CsrOperator(A_host, device=local)
-    n = A.n
-    b = np.ones(n)
-    prob = _helpers.Problem(A, b, None, None)
-    st = _CGState(prob)
-    comm = None
-    if world > 1:
-        comm = make_comm(pg, ctx, world, rank)
-        _lib.check(_lib.lib.kry_cg_attach_comm(st.h, comm, rank, world))
-    st.start()
-    # tol = 0, atol = 0: never converges -> exactly the requested iterations
-    st.set_criterion(np.zeros(world if comm else 1))
-    ncols = world if comm else 1
-    chunk = _helpers.CHUNK
-
-    def iterate(k):
-        done = 0
-        while done < k:
-            s = min(chunk, k - done)
-            hist = st.run(s, ncols)
-            assert len(hist) == s, "solver stopped early"
-            done += s
-        return hist
-
-    iterate(warmup)
+    comm = distributed.ShardComm.from_torch(device=local) if world > 1 else None
+    st, ncols = _cg_state(A, np.ones(A.n), comm, rank, world)
+    _iterate(st, warmup, ncols)
     ctx.synchronize()
     ctx.profile(True)
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
-    hist = iterate(steps)
+    _iterate(st, steps, ncols)
     ctx.synchronize()
     t1 = time.perf_counter()
     barrier(pg)
@@ -145,21 +134,33 @@ def run_cg(A_host, steps, warmup, world, rank, local, pg):
     cnt, spmv_ms = ctx.profile_read(_lib.PROF_SPMV)
     ucnt, upd_ms = ctx.profile_read(_lib.PROF_UPDATE)
     ctx.profile(False)
+    del st
     if comm is not None:
-        _lib.check(_lib.lib.kry_comm_destroy(comm))
-    return {
-        "elapsed": elapsed,
-        "spmv_count": cnt,
-        "spmv_ms": spmv_ms,
-        "update_count": ucnt,
-        "update_ms": upd_ms,
-        "last_resnorm": float(np.max(hist[-1])),
-        "n": n,
-        "nnz": A.nnz,
-    }
+        comm.close()
+    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_ms": spmv_ms, "update_count": ucnt, "update_ms": upd_ms,
+            "n": A.n, "nnz": A.nnz}
 
 
-def run_gmres(steps_warm=1):
+def run_cg_config(A_host, B, steps, warmup=5):
+    """CG iterations/s on one GPU for a secondary config (k = B.shape[1])."""
+    import krylov_amd
+    from krylov_amd.device import get_context
+
+    ctx = get_context()
+    A = krylov_amd.CsrOperator(A_host)
+    st, ncols = _cg_state(A, B)
+    _iterate(st, warmup, ncols)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    _iterate(st, steps, ncols)
+    ctx.synchronize()
+    t = time.perf_counter() - t0
+    k = 1 if B.ndim == 1 else B.shape[1]
+    return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "rhs": k, "n": A.n, "nnz": A.nnz,
+            "gbs": cg_iteration_bytes(A.n, A.nnz, k) * steps / t / 1e9}
+
+
+def run_gmres():
     import krylov_amd
     from krylov_amd import _helpers, problems
     from krylov_amd.device import get_context
@@ -167,12 +168,11 @@ def run_gmres(steps_warm=1):
 
     R = problems.random_nonsym(2_000_000)
     A = krylov_amd.CsrOperator(R)
-    b = np.ones(R.shape[0])
-    prob = _helpers.Problem(A, b, None, None)
+    prob = _helpers.Problem(A, np.ones(R.shape[0]), None, None)
     ctx = get_context()
     st = _GmresState(prob, 30, 1)
     times = []
-    for rep in range(steps_warm + 3):
+    for rep in range(4):
         st.start()
         st.set_criterion(np.zeros(1))
         ctx.synchronize()
@@ -182,20 +182,64 @@ def run_gmres(steps_warm=1):
         ctx.synchronize()
         t1 = time.perf_counter()
         assert len(hist) == 30
-        if rep >= steps_warm:
+        if rep >= 1:
             times.append(t1 - t0)
     t = float(np.median(times))
-    return {"gmres30_it_per_s": 30.0 / t, "gmres30_cycle_ms": 1e3 * t,
-            "gmres30_gbs": gmres_cycle_bytes(R.shape[0], R.nnz) / t / 1e9, "n": R.shape[0], "nnz": int(R.nnz)}
+    return {"it_per_s": 30.0 / t, "cycle_ms": 1e3 * t, "gbs": gmres_cycle_bytes(R.shape[0], R.nnz) / t / 1e9,
+            "n": R.shape[0], "nnz": int(R.nnz), "config": "cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"}
+
+
+def run_minres_cfg5(steps=100):
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.device import get_context
+    from krylov_amd.minres import _MinresState
+
+    W, w = problems.shifted_lap3d_weighted(200)
+    A = krylov_amd.CsrOperator(W)
+    prob = _helpers.Problem(A, np.ones(W.shape[0], dtype=np.float32), None, krylov_amd.WeightedInner(w))
+    ctx = get_context()
+    st = _MinresState(prob)
+    st.start()
+    st.set_criterion(np.zeros(1))
+    st.run(5)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    while done < steps:
+        hist, inv = st.run(min(32, steps - done))
+        assert len(hist) == min(32, steps - done) and not inv, "MINRES stopped early"
+        done += len(hist)
+    ctx.synchronize()
+    t = time.perf_counter() - t0
+    return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "n": W.shape[0], "nnz": int(W.nnz),
+            "config": "cfg5 shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights (vectors f64 as in the reference)"}
+
+
+def pmc_traffic(n, nnz):
+    """HBM bytes per launch of the fused CG SpMV from the committed PMC
+    summary (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes, read side
+    calibrated on a same-width stream of known size), if it was taken on this
+    workload. PMC needs its own rocprofv3 runs, so it cannot be live here."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except OSError:
+        return {}
+    if d.get("n") != n or d.get("nnz") != nnz:
+        return {}
+    return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
+            "source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f "
+                      "calibrated)" % d["read_scale_from_calibration"]}
 
 
 def cpu_baseline(A_host, target_s=12.0):
     """The oracle (reference iteration on NumPy/SciPy, oracle/krylov_ref.py)
-    timed on this host: CG with tol=0 on the same matrix, bounded sample."""
+    timed on this host: CG with tol=0 on the metric matrix, bounded sample."""
     from oracle import krylov_ref
 
     b = np.ones(A_host.shape[0])
-    # calibrate: 2 iterations, then size the sample to ~target_s
     t0 = time.perf_counter()
     krylov_ref.cg(A_host, b, tol=0.0, atol=0.0, maxiter=2)
     t_cal = time.perf_counter() - t0
@@ -221,28 +265,29 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=216, help="stencil edge (216 = BASELINE metric)")
+    ap.add_argument("--quick", action="store_true", help="metric only (no GMRES leg, no CPU baseline)")
+    ap.add_argument("--configs", action="store_true", help="also time the secondary BASELINE configs (cfg2, cfg4, cfg5)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-gmres", action="store_true")
     args = ap.parse_args()
 
     world, rank, local, pg = dist_setup()
-    if world != args.gpus and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     os.environ["KRYLOV_DEVICE"] = str(local)
+    if world > 1 and args.gpus != world:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
 
     from krylov_amd import problems
 
     A_host = problems.stencil15_3d(args.m)
     n, nnz = A_host.shape[0], int(A_host.nnz)
-    res = run_cg(A_host, args.steps, args.warmup, world, rank, local, pg)
+    res = run_metric(A_host, args.steps, args.warmup, world, rank, local, pg)
     T = res["elapsed"]
-    value = world * args.steps / T
     spmv_avg_s = res["spmv_ms"] / max(res["spmv_count"], 1) / 1e3
     spmv_bytes = spmv_fused_bytes(n, nnz)
     achieved = spmv_bytes / spmv_avg_s / 1e9
+    traffic = pmc_traffic(n, nnz)
     out = {
         "metric": "CG iters/sec + SpMV GB/s (fp64, n=10M, nnz=150M); GMRES(30) iters/sec",
-        "value": value,
+        "value": world * args.steps / T,
         "unit": "CG iters/s (RHS-iterations/s over all GPUs)",
         "n_gpus": world,
         "steps": args.steps,
@@ -259,7 +304,7 @@ def main():
             "nnz": nnz,
             "index": "int32",
             "rhs_per_gpu": 1,
-            "parallelism": f"rhs-shard x{world}" + (" (RCCL resnorm allreduce/iter)" if world > 1 else ""),
+            "parallelism": f"rhs-shard x{world}" + (" (one RCCL resnorm allreduce per iteration)" if world > 1 else ""),
         },
         "spmv_gbs": achieved,
         "spmv_ms": 1e3 * spmv_avg_s,
@@ -270,16 +315,28 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel": "spmv_stream_kernel<double,double,int,SrcCgP,EpiCgAp> (fused p-update + SpMV + <p,Ap>)",
+            "traffic": traffic.get("traffic_bytes_per_launch"),
+            "traffic_source": traffic.get("source"),
+            "kernel": "spmv_sell_kernel<double,double,int,1,16,SrcCgP,EpiCgAp> (fused p-update + SELL-64 SpMV + <p,Ap>)",
             "bytes_per_launch": spmv_bytes,
+            "bytes_formula": "nnz*(8+4) + (n+1)*4 + 4*n*8  (SURVEY S + 2n*8 for the fused p-update)",
             "launches_timed": res["spmv_count"],
         },
     }
-    if world == 1 and not args.no_gmres:
-        out["gmres"] = run_gmres()
-        out["gmres30_it_per_s"] = out["gmres"]["gmres30_it_per_s"]
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if world == 1 and not args.quick:
+        g = run_gmres()
+        out["gmres30_it_per_s"] = g["it_per_s"]
+        out["gmres"] = g
+    if world == 1 and args.configs:
+        extra = {}
+        extra["cfg2_cg_poisson1000"] = run_cg_config(problems.poisson2d(1000), np.ones(1_000_000), 200, 10)
+        P3 = problems.poisson2d(3163)
+        B = np.random.default_rng(0).standard_normal((P3.shape[0], 8))
+        extra["cfg4_blockcg_8rhs_per_gpu"] = run_cg_config(P3, B, 20, 3)
+        del P3, B
+        extra["cfg5_minres_fp32_weighted"] = run_minres_cfg5()
+        out["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu and not args.quick:
         out["cpu_baseline"] = cpu_baseline(A_host)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -158,3 +158,12 @@ def device_count():
     c = _int(0)
     check(lib.kry_device_count(ctypes.byref(c)))
     return c.value
+
+
+def csr_layout(indptr):
+    """SELL-64 plan of a CSR row pointer: (nslices, nslots, nirregular)."""
+    indptr = np.ascontiguousarray(indptr)
+    ns, slots, irr = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    check(lib.kry_csr_layout(indptr.shape[0] - 1, ptr(indptr), itype_code(indptr.dtype), ctypes.byref(ns),
+                             ctypes.byref(slots), ctypes.byref(irr)))
+    return ns.value, slots.value, irr.value

@@ -1,0 +1,127 @@
+"""Right-hand-side sharding across GPUs.
+
+The reference is "fully blocked": a block ``b`` of shape (n, K) runs K
+independent CG recurrences whose only coupling is the stop rule
+``np.all(resnorms[-1] <= criterion)`` over all columns (cg.py:156,162). Here
+the K columns are split into equal contiguous blocks, one per process/GPU;
+each GPU runs the whole fused CG loop on its block against a replicated copy
+of A, and every iteration performs exactly one ``ncclAllReduce`` (RCCL over
+xGMI) of the zero-padded residual-norm vector so that every rank applies the
+global stop rule and records the global history. The result equals the
+unsharded block solve (same per-column recurrences, same stop step).
+
+One process per GPU (launched by ``torch.distributed.run``); the RCCL
+unique id is exchanged over whatever process group the caller has (gloo is
+enough: it is control-plane only).
+"""
+import ctypes
+import weakref
+
+import numpy as np
+
+from . import _helpers, _lib
+from ._helpers import Info, Problem
+from ._lib import check, lib
+from .cg import _CGState
+from .device import get_context
+
+
+class ShardComm:
+    """An RCCL communicator over ``world`` ranks, one GPU each."""
+
+    def __init__(self, rank, world, unique_id, device=None):
+        self.ctx = get_context(device)
+        self.rank = int(rank)
+        self.world = int(world)
+        idb = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
+        assert idb.size == 128
+        h = ctypes.c_void_p()
+        check(lib.kry_comm_create(self.ctx.handle, self.world, self.rank, _lib.ptr(idb), ctypes.byref(h)))
+        self.handle = h
+        self._fin = weakref.finalize(self, lib.kry_comm_destroy, h)
+
+    @staticmethod
+    def unique_id():
+        buf = np.zeros(128, dtype=np.uint8)
+        check(lib.kry_comm_unique_id(_lib.ptr(buf)))
+        return buf.tobytes()
+
+    @classmethod
+    def from_torch(cls, group=None, device=None):
+        """Create the communicator, exchanging the unique id through an
+        initialised ``torch.distributed`` process group (any backend)."""
+        import torch
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        idt = torch.zeros(128, dtype=torch.int64)
+        if rank == 0:
+            idt = torch.from_numpy(np.frombuffer(cls.unique_id(), dtype=np.uint8).astype(np.int64))
+        dist.broadcast(idt, src=0, group=group)
+        uid = idt.numpy().astype(np.uint8).tobytes()
+        return cls(rank, world, uid, device=device)
+
+    def allreduce(self, values):
+        """Sum a small float64 vector over ranks (setup-time exchanges)."""
+        v = np.ascontiguousarray(values, dtype=np.float64).copy()
+        check(lib.kry_comm_allreduce(self.handle, _lib.dptr(v), v.size))
+        return v
+
+    def close(self):
+        self._fin()
+
+
+def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None):
+    """Block CG on this rank's RHS columns ``B`` (n, k_local), k_local equal
+    on every rank, with the reference's global stop rule.
+
+    Returns ``(xk_local or None, Info)``; ``Info.resnorms`` holds the GLOBAL
+    history (each entry an array over all world * k_local columns, in rank
+    order), identical on every rank.
+    """
+    if callback is not None:
+        raise NotImplementedError("callbacks are not supported on the sharded path")
+    B = np.asarray(B)
+    if B.ndim == 1:
+        B = B[:, None]
+    prob = Problem(A, B, x0, None, device=comm.ctx.device)
+    kc, kp, world = prob.kc, prob.kpad, comm.world
+    total = kp * world
+    off = kp * comm.rank
+    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+
+    def glob(local_vals):
+        """local kpad values -> global zero-padded vector, summed over ranks"""
+        v = np.zeros(total)
+        v[off:off + kp] = local_vals
+        return comm.allreduce(v)
+
+    real = np.concatenate([np.arange(r * kp, r * kp + kc) for r in range(world)])
+
+    st = _CGState(prob)
+    check(lib.kry_cg_attach_comm(st.h, comm.handle, off, total))
+    rho0 = st.start()
+    rn0 = glob(np.sqrt(rho0.astype(prob.inner_dtype)).astype(np.float64))
+    resnorms = [rn0[real]]
+    criterion = np.maximum(tol * resnorms[0], atol)
+    crit_full = np.full(total, np.inf)
+    crit_full[real] = criterion
+    st.set_criterion(crit_full)
+    k = 0
+    success = False
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            sq = glob(st.residual_norm2())
+            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        hist = st.run(min(_helpers.CHUNK, maxiter - k), ncols=total)
+        for row in hist:
+            resnorms.append(np.asarray(row)[real])
+            k += 1
+    xk = prob.unpad_vec(st.get(0), prob.r0_dtype)
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 2 + 2 * k}
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)

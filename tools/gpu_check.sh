@@ -4,7 +4,7 @@
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT/prof
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -m pytest tests -q -m gpu ${PYTEST_ARGS} > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 600 python -m pytest tests -q -m gpu ${PYTEST_ARGS} > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 echo "pytest exit $?" >> $OUT/pytest_gpu.log
 tail -3 $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; cat $OUT/smoke.log | tail -20; exit 1; }
@@ -13,6 +13,9 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.log 2>&1 || { echo 
 tail -c 3000 $OUT/bench.log
 if [ -n "$PROFILE" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 10 --no-cpu > $OUT/prof/bench_stdout.log 2>&1
-  echo "rocprof exit $?"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py ${BENCH_ARGS} --no-cpu > $OUT/prof/bench_stdout.log 2>&1
+  rc=$?; echo "rocprof exit $rc"; [ $rc -ne 0 ] && exit $rc
+fi
+if [ -n "$PMC" ]; then
+  $GRAFT_REPO_ROOT/tools/pmc_traffic.sh || exit 1
 fi

@@ -81,6 +81,24 @@ __global__ __launch_bounds__(256) void read_ceiling(const int4 *__restrict__ a, 
 }
 
 
+// PMC calibration: the SELL matrix stream alone, with the library kernel's
+// access widths (4-B index + 8-B value per lane, nontemporal, coalesced per
+// wave). Algorithmic bytes = 12 * nslots; FETCH_SIZE / that = the counter's
+// scale for this access pattern (MI355X_MICROARCH.md "HBM": uncalibrated
+// widths must be calibrated on a known byte count).
+__global__ __launch_bounds__(256) void sell_stream_calib(const int *__restrict__ idx, const double *__restrict__ val,
+                                                         int64_t ns, double *out) {
+  double s = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    const int c = __builtin_nontemporal_load(idx + i);
+    const double v = __builtin_nontemporal_load(val + i);
+    s += c >= 0 ? v : 0.0;
+  }
+  if (s == 12345.678) out[0] = s;
+}
+
+
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v2i __attribute__((ext_vector_type(2)));
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -237,6 +255,10 @@ int main(int argc, char **argv) {
   report("read ceiling (SELL idx+val, 16 B/lane)", nnz * 12.0, [&] {
     hipLaunchKernelGGL(read_ceiling, dim3(2048), dim3(256), 0, 0, (const int4 *)A->sidx, nnz / 4,
                        (const double2 *)A->sval, nnz / 2, d_out);
+  });
+  report("SELL stream calibration (4+8 B/lane nt)", A->nslots * 12.0, [&] {
+    hipLaunchKernelGGL(sell_stream_calib, dim3(8192), dim3(256), 0, 0, (const int *)A->sidx,
+                       (const double *)A->sval, A->nslots, d_out);
   });
   report("library SELL SpMV y = A x", S, [&] {
     launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr, nullptr,
