@@ -61,7 +61,7 @@ def dist_setup():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -118,7 +118,7 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
 
     ctx = get_context(local)
     A = krylov_amd.CsrOperator(A_host, device=local)
-    comm = distributed.ShardComm.from_torch(device=local) if world > 1 else None
+    comm = distributed.ShardComm.from_torch(device=local) if pg is not None else None
     st, ncols = _cg_state(A, np.ones(A.n), comm, rank, world)
     _iterate(st, warmup, ncols)
     ctx.synchronize()

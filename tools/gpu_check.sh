@@ -19,3 +19,8 @@ fi
 if [ -n "$PMC" ]; then
   $GRAFT_REPO_ROOT/tools/pmc_traffic.sh || exit 1
 fi
+if [ -n "$TORCHRUN" ]; then
+  cd $GRAFT_REPO_ROOT
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --quick --steps 64 --warmup 8 > $OUT/bench_torchrun.log 2>&1 || { echo "torchrun bench failed"; tail -20 $OUT/bench_torchrun.log; exit 1; }
+  tail -1 $OUT/bench_torchrun.log
+fi
