@@ -2,8 +2,8 @@
 
 Workload (BASELINE.json metric): CG on the 3-D 15-point stencil
 216^3 (n = 10,077,696, nnz = 149,770,936, fp64, int32 indices), b = ones,
-tol = 0 (fixed iteration count). One step = one CG iteration: one fused
-p-update + SpMV + <p,Ap> launch, one fused x/r update + <r,r> launch and two
+tol = 0 (fixed iteration count). One step = one CG iteration: the SpMV
+(+ <p,Ap>) launch, the fused x/r update (+ <r,r>) launch, the p pass and two
 one-block scalar kernels, no host sync inside a 32-iteration chunk.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--quick]
@@ -40,15 +40,9 @@ def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
     return nnz * (mvb + ib) + (n + 1) * ib + 2 * n * k * vb
 
 
-def spmv_fused_bytes(n, nnz, k=1, vb=8, ib=4):
-    """One fused CG SpMV launch: S with x replaced by (r, p_old) read and
-    (p, Ap) written: S + 2 n k vb."""
-    return spmv_S(n, nnz, k, vb, ib) + 2 * n * k * vb
-
-
 def cg_iteration_bytes(n, nnz, k=1, vb=8, ib=4):
-    """Fused SpMV launch + update pass (read y, r, p, Ap; write y, r)."""
-    return spmv_fused_bytes(n, nnz, k, vb, ib) + 6 * n * k * vb
+    """SpMV + fused x/r/rho pass (6 vectors) + p pass (3)."""
+    return spmv_S(n, nnz, k, vb, ib) + 9 * n * k * vb
 
 
 def gmres_cycle_bytes(n, nnz, m=30, vb=8, ib=4):
@@ -282,7 +276,7 @@ def main():
     res = run_metric(A_host, args.steps, args.warmup, world, rank, local, pg)
     T = res["elapsed"]
     spmv_avg_s = res["spmv_ms"] / max(res["spmv_count"], 1) / 1e3
-    spmv_bytes = spmv_fused_bytes(n, nnz)
+    spmv_bytes = spmv_S(n, nnz)
     achieved = spmv_bytes / spmv_avg_s / 1e9
     traffic = pmc_traffic(n, nnz)
     out = {
@@ -317,9 +311,11 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("traffic_bytes_per_launch"),
             "traffic_source": traffic.get("source"),
-            "kernel": "spmv_sell_kernel<double,double,int,1,16,SrcCgP,EpiCgAp> (fused p-update + SELL-64 SpMV + <p,Ap>)",
+            "kernel": "spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact "
+                      "index image, Ap stored + <p,Ap> partials)",
             "bytes_per_launch": spmv_bytes,
-            "bytes_formula": "nnz*(8+4) + (n+1)*4 + 4*n*8  (SURVEY S + 2n*8 for the fused p-update)",
+            "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; the "
+                             "compact image moves nnz*(8+2) for the matrix)",
             "launches_timed": res["spmv_count"],
         },
     }

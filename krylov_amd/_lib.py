@@ -54,6 +54,7 @@ _SIGNATURES = {
     "kry_csr_create": [_vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
     "kry_csr_destroy": [_vp],
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
+    "kry_csr_info": [_vp, _ip64],
     "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
     "kry_vec_destroy": [_vp],
     "kry_vec_upload": [_vp, _vp],

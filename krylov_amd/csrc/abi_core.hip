@@ -1,5 +1,7 @@
 // C-ABI: library, context, CSR operator, vectors, primitives, timers.
 #include <algorithm>
+#include <atomic>
+#include <climits>
 #include <cstring>
 #include <thread>
 
@@ -102,105 +104,6 @@ static void sell_fill(int64_t n, const I *ip, const I *ix, const MV *dv, const s
   for (auto &x : th) x.join();
 }
 
-// ------------------------------------------------------- x-window plan
-// Group = kGroupSlices consecutive slices (512 rows). A group is "windowed"
-// when its distinct column indices form at most kMaxWindows runs (gaps of
-// <= kWindowGap merged) covering <= kWindowMax elements and none of its
-// slices is irregular: the SpMV then stages those x runs into LDS with
-// coalesced loads and its lanes gather from LDS through group-local indices
-// (sloc). For a 3-D stencil that is three windows (the planes k-1, k, k+1).
-template <typename I>
-static void window_plan(int64_t n, const I *ip, const I *ix, const std::vector<int32_t> &width,
-                        const std::vector<int64_t> &sptr, std::vector<int32_t> &gwin, std::vector<int64_t> &wstart,
-                        std::vector<int32_t> &wlen, std::vector<int32_t> &wlofs, std::vector<int32_t> &sloc,
-                        int64_t *nwindowed) {
-  const int64_t ns = (int64_t)width.size();
-  const int64_t ng = (ns + kGroupSlices - 1) / kGroupSlices;
-  std::vector<std::vector<std::pair<int64_t, int32_t>>> wins(ng);  // per group: (start, len)
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ng < 64) nt = 1;
-  auto plan = [&](int64_t ga, int64_t gb) {
-    std::vector<int64_t> cols;
-    for (int64_t g = ga; g < gb; ++g) {
-      const int64_t s0 = g * kGroupSlices, s1 = std::min<int64_t>(ns, s0 + kGroupSlices);
-      bool ok = true;
-      for (int64_t s = s0; s < s1; ++s) ok = ok && width[s] >= 0;
-      if (!ok) continue;
-      const int64_t r0 = s0 * kSlice, r1 = std::min<int64_t>(n, s1 * kSlice);
-      cols.clear();
-      for (int64_t e = (int64_t)ip[r0]; e < (int64_t)ip[r1]; ++e) cols.push_back((int64_t)ix[e]);
-      if (cols.empty()) continue;
-      std::sort(cols.begin(), cols.end());
-      std::vector<std::pair<int64_t, int32_t>> w;
-      int64_t st = cols[0], last = cols[0], total = 0;
-      for (size_t i = 1; i <= cols.size() && ok; ++i) {
-        if (i == cols.size() || cols[i] - last > kWindowGap) {
-          const int64_t len = last - st + 1;
-          total += len;
-          w.emplace_back(st, (int32_t)len);
-          if (total > kWindowMax || (int64_t)w.size() > kMaxWindows) ok = false;
-          if (i < cols.size()) st = cols[i];
-        }
-        if (i < cols.size()) last = cols[i];
-      }
-      if (ok) wins[g] = std::move(w);
-    }
-  };
-  {
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(plan, ng * t / nt, ng * (t + 1) / nt);
-    for (auto &x : th) x.join();
-  }
-  gwin.assign(ng + 1, 0);
-  int64_t cnt = 0;
-  for (int64_t g = 0; g < ng; ++g) {
-    gwin[g + 1] = gwin[g] + (int32_t)wins[g].size();
-    cnt += !wins[g].empty();
-  }
-  *nwindowed = cnt;
-  wstart.resize(gwin[ng]);
-  wlen.resize(gwin[ng]);
-  wlofs.resize(gwin[ng]);
-  for (int64_t g = 0; g < ng; ++g) {
-    int32_t lofs = 0;
-    for (size_t i = 0; i < wins[g].size(); ++i) {
-      wstart[gwin[g] + i] = wins[g][i].first;
-      wlen[gwin[g] + i] = wins[g][i].second;
-      wlofs[gwin[g] + i] = lofs;
-      lofs += wins[g][i].second;
-    }
-  }
-  sloc.assign(sptr[ns] + 256, -1);
-  auto remap = [&](int64_t ga, int64_t gb) {
-    for (int64_t g = ga; g < gb; ++g) {
-      const auto &w = wins[g];
-      if (w.empty()) continue;
-      std::vector<int32_t> pre(w.size(), 0);
-      for (size_t q = 1; q < w.size(); ++q) pre[q] = pre[q - 1] + w[q - 1].second;
-      const int64_t s0 = g * kGroupSlices, s1 = std::min<int64_t>(ns, s0 + kGroupSlices);
-      for (int64_t s = s0; s < s1; ++s) {
-        const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
-        for (int64_t r = r0; r < r1; ++r) {
-          int64_t j = 0;
-          for (int64_t e = ip[r]; e < ip[r + 1]; ++e, ++j) {
-            const int64_t c = (int64_t)ix[e];
-            size_t lo = 0, hi = w.size();  // last window with start <= c
-            while (hi - lo > 1) {
-              const size_t mid = (lo + hi) / 2;
-              if (w[mid].first <= c) lo = mid; else hi = mid;
-            }
-            sloc[sptr[s] + j * kSlice + (r - r0)] = pre[lo] + (int32_t)(c - w[lo].first);
-          }
-        }
-      }
-    }
-  };
-  {
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(remap, ng * t / nt, ng * (t + 1) / nt);
-    for (auto &x : th) x.join();
-  }
-}
 
 template <typename V>
 struct OpDot {
@@ -319,6 +222,16 @@ int kry_ctx_synchronize(kry_ctx *ctx) {
   KRY_API_END
 }
 
+int kry_csr_info(const kry_csr *A, int64_t *info) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(A && info, KRY_EINVAL, "null argument");
+  info[0] = A->nslices;
+  info[1] = A->nslots;
+  info[2] = A->nirregular;
+  info[3] = A->compact ? 1 : 0;
+  KRY_API_END
+}
+
 int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, int64_t *nslots,
                    int64_t *nirregular) {
   KRY_API_BEGIN
@@ -334,6 +247,50 @@ int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, i
 
 }  // extern "C"
 
+// Compact column image: for every slot column (slice s, column j) the base is
+// the smallest column index among its lanes and every lane stores col - base
+// as uint16 (0xFFFF = padding). Possible when each slot column spans at most
+// 65534 columns (banded and stencil matrices); the gathers then read 2 B of
+// index per nonzero instead of 4. Returns false (nothing built) otherwise.
+template <typename I>
+static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int32_t> &width,
+                         const std::vector<I> &sidx, std::vector<uint16_t> &sdelta, std::vector<int32_t> &scbase) {
+  const int64_t ns = (int64_t)width.size();
+  const int64_t slots = sptr[ns];
+  sdelta.assign(slots + 256, 0xFFFF);
+  scbase.assign(slots / kSlice + 16, 0);
+  std::atomic<bool> ok{true};
+  auto work = [&](int64_t sa, int64_t sb) {
+    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
+      const int64_t base = sptr[s];
+      for (int64_t j = 0; j < width[s]; ++j) {
+        const I *c = sidx.data() + base + j * kSlice;
+        int64_t mn = INT64_MAX, mx = -1;
+        for (int l = 0; l < kSlice; ++l)
+          if (c[l] >= 0) {
+            mn = std::min<int64_t>(mn, c[l]);
+            mx = std::max<int64_t>(mx, c[l]);
+          }
+        if (mx < 0) mn = 0;
+        if (mx - mn > 65534 || mn > INT32_MAX) {
+          ok = false;
+          return;
+        }
+        scbase[base / kSlice + j] = (int32_t)mn;
+        uint16_t *d = sdelta.data() + base + j * kSlice;
+        for (int l = 0; l < kSlice; ++l)
+          if (c[l] >= 0) d[l] = (uint16_t)(c[l] - mn);
+      }
+    }
+  };
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 4096) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
+  for (auto &x : th) x.join();
+  return ok.load();
+}
+
 namespace {
 template <typename I, typename MV>
 void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
@@ -348,37 +305,26 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   std::vector<I> sidx;
   std::vector<MV> sval;
   sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
-  // x-window image: opt-in (KRY_SPMV_WINDOWS=1). Measured on the metric
-  // matrix it is bitwise exact but slower than plain SELL (0.50 vs 0.39 ms:
-  // the stage -> barrier -> compute sequence is latency-bound), so the default
-  // upload skips the plan entirely.
-  const char *wenv = getenv("KRY_SPMV_WINDOWS");
-  if (wenv && atoi(wenv) != 0) {
-    std::vector<int32_t> gwin, wlen, wlofs, sloc;
-    std::vector<int64_t> wstart;
-    window_plan(n, ip, ix, width, sptr, gwin, wstart, wlen, wlofs, sloc, &A->nwindowed);
-    A->ngroups = (int64_t)gwin.size() - 1;
-    if (A->nwindowed > 0) {
-      A->gwin = dev_alloc(gwin.size() * 4);
-      A->wstart = dev_alloc(wstart.size() * 8 + 8);
-      A->wlen = dev_alloc(wlen.size() * 4 + 4);
-      A->wlofs = dev_alloc(wlofs.size() * 4 + 4);
-      A->sloc = dev_alloc(sloc.size() * 4);
-      KRY_HIP(hipMemcpyAsync(A->gwin, gwin.data(), gwin.size() * 4, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->wstart, wstart.data(), wstart.size() * 8, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->wlen, wlen.data(), wlen.size() * 4, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->wlofs, wlofs.data(), wlofs.size() * 4, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->sloc, sloc.data(), sloc.size() * 4, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipStreamSynchronize(st));
-    }
-  }
   A->sptr = dev_alloc(sptr.size() * 8);
   A->swidth = dev_alloc(width.size() * 4 + 4);
-  A->sidx = dev_alloc(sidx.size() * sizeof(I));
+  // compact image unless disabled (KRY_SELL_COMPACT=0) or impossible
+  const char *cenv = getenv("KRY_SELL_COMPACT");
+  std::vector<uint16_t> sdelta;
+  std::vector<int32_t> scbase;
+  A->compact = sizeof(I) == 4 && !(cenv && atoi(cenv) == 0) && A->nslots > 0 &&
+               compact_fill(sptr, width, sidx, sdelta, scbase);
+  if (A->compact) {
+    A->sdelta = dev_alloc(sdelta.size() * 2);
+    A->scbase = dev_alloc(scbase.size() * 4);
+    KRY_HIP(hipMemcpyAsync(A->sdelta, sdelta.data(), sdelta.size() * 2, hipMemcpyHostToDevice, st));
+    KRY_HIP(hipMemcpyAsync(A->scbase, scbase.data(), scbase.size() * 4, hipMemcpyHostToDevice, st));
+  } else {
+    A->sidx = dev_alloc(sidx.size() * sizeof(I));
+    KRY_HIP(hipMemcpyAsync(A->sidx, sidx.data(), sidx.size() * sizeof(I), hipMemcpyHostToDevice, st));
+  }
   A->sval = dev_alloc(sval.size() * sizeof(MV));
   KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
   if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
-  KRY_HIP(hipMemcpyAsync(A->sidx, sidx.data(), sidx.size() * sizeof(I), hipMemcpyHostToDevice, st));
   KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
   if (A->nirregular > 0) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
@@ -395,8 +341,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 }  // namespace
 
 static void csr_free(kry_csr *A) {
-  void *bufs[] = {A->sptr, A->swidth, A->sidx, A->sval, A->indptr, A->indices, A->data,
-                  A->gwin, A->wstart, A->wlen, A->wlofs, A->sloc};
+  void *bufs[] = {A->sptr, A->swidth, A->sidx, A->sval, A->indptr, A->indices, A->data, A->sdelta, A->scbase};
   for (void *b : bufs) dev_free(b);
 }
 

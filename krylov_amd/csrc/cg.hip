@@ -1,14 +1,16 @@
 // CG device loop (reference cg.py:16-259 with M = Ml = I).
 //
-// One iteration = four launches on the context stream, no host sync:
-//   1. SpMV   p = r + omega p_old (materialised in the gather), Ap = A p,
-//             partial <p, Ap>                          cg.py:175-183
-//   2. tiny   alpha = rho / guard(<p, Ap>)             cg.py:185
+// One iteration = five launches on the context stream, no host sync:
+//   1. SpMV   Ap = A p, partial <p, Ap>                 cg.py:180-183
+//   2. tiny   alpha = rho / guard(<p, Ap>)              cg.py:185
 //   3. update y += alpha p, r -= alpha Ap, partial <r, r>   cg.py:196-209
 //   4. tiny   rho shift, omega, resnorm = sqrt(rho) -> history, stop test
 //             np.all(resnorm <= criterion) -> ctrl.stop_at  cg.py:156,214-217
+//   5. p pass p = r + omega p for the next iteration    cg.py:175-178
 // (+ with an attached communicator: one ncclAllReduce of the zero-padded
 //  residual-norm vector and a tiny global stop test.)
+// The p update is its own streaming pass (not folded into the SpMV's gather):
+// the SpMV then gathers one vector instead of two, which is what bounds it.
 #include "solver_common.hpp"
 
 using namespace kry;
@@ -20,7 +22,7 @@ struct kry_cg {
   int k = 1;
   int dtype = 0;
   bool scalar_f32 = false;
-  void *b = nullptr, *x0 = nullptr, *y = nullptr, *r = nullptr, *p[2] = {nullptr, nullptr};
+  void *b = nullptr, *x0 = nullptr, *y = nullptr, *r = nullptr, *p = nullptr;
   void *Ap = nullptr, *xk = nullptr, *rt = nullptr;
   double *w = nullptr;
   double *part = nullptr;  // 2 * kMaxGrid * k
@@ -69,6 +71,28 @@ struct OpCgUpdate {
     }
     VIO<V>::store_nt(y, e, N, yv);
     VIO<V>::store(r, e, N, rv);  // r and p are the next SpMV's gather sources
+  }
+};
+
+// p = r + omega * p, in place (cg.py:178 with M = I: p = MPr + omega p).
+template <typename V>
+struct OpCgP {
+  V *p;
+  const V *r;
+  const double *omega;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V pv[W], rv[W];
+    VIO<V>::load(p, e, N, pv);
+    VIO<V>::load(r, e, N, rv);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V om = (V)omega[(e + v) & (k - 1)];
+      const V t = om * pv[v];
+      pv[v] = rv[v] + t;
+    }
+    VIO<V>::store(p, e, N, pv);
   }
 };
 
@@ -171,15 +195,12 @@ void cg_run_impl(kry_cg *s, int max_steps) {
   const int64_t N = s->n * (int64_t)k;
   double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
   for (int step = 0; step < max_steps; ++step) {
-    const int64_t i = s->it + step;
-    V *pcur = static_cast<V *>(s->p[i & 1]);
-    const V *pold = static_cast<const V *>(s->p[(i + 1) & 1]);
-    SrcCgP<V> src{static_cast<const V *>(s->r), pold, s->scal + S_OMEGA * k, k, i == 0 ? 1 : 0};
+    V *p = static_cast<V *>(s->p);
     int PA, PB;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
-      launch_spmv<V, MV, I>(s->A, k, src, EpiCgAp<V>{static_cast<V *>(s->Ap), pcur, src, s->w, k}, partA, &PA,
-                        s->ctrl, step, st);
+      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{p, k}, EpiApDot<V>{static_cast<V *>(s->Ap), s->w, k}, partA, &PA,
+                            s->ctrl, step, st);
     }
     if (s->scalar_f32)
       hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
@@ -188,7 +209,7 @@ void cg_run_impl(kry_cg *s, int max_steps) {
     {
       ProfScope ps(s->ctx, PROF_UPDATE);
       PB = launch_elementwise<V>(N, k,
-                                 OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), pcur,
+                                 OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), p,
                                                static_cast<const V *>(s->Ap), s->scal + S_ALPHA * k, s->w, k},
                                  partB, s->ctrl, step, st);
     }
@@ -200,6 +221,11 @@ void cg_run_impl(kry_cg *s, int max_steps) {
       hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
                          s->ctrl, step, gb, s->col_offset, s->total_k);
     KRY_HIP(hipGetLastError());
+    {
+      ProfScope ps(s->ctx, PROF_OTHER);
+      launch_elementwise<V>(N, k, OpCgP<V>{p, static_cast<const V *>(s->r), s->scal + S_OMEGA * k, k}, nullptr,
+                            s->ctrl, step, st);
+    }
     if (s->comm) {
       // exactly one collective per iteration: the residual-norm vector
       ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k, ncclDouble, ncclSum, s->comm->comm, st);
@@ -245,7 +271,7 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
   }
 
 static void cg_free(kry_cg *s) {
-  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p[0], s->p[1], s->Ap, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
+  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p, s->Ap, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
                   s->ctrl, s->gbuf, s->gcrit};
   for (void *b : bufs) dev_free(b);
 }
@@ -267,7 +293,7 @@ int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out) 
     s->k = k;
     s->dtype = dtype;
     const size_t vb = ((size_t)A->n * k + 15) / 16 * 16 * dsize(dtype);
-    void **vecs[] = {&s->b, &s->y, &s->r, &s->p[0], &s->p[1], &s->Ap, &s->xk, &s->rt};
+    void **vecs[] = {&s->b, &s->y, &s->r, &s->p, &s->Ap, &s->xk, &s->rt};
     for (void **v : vecs) {
       *v = dev_alloc(vb);
       KRY_HIP(hipMemsetAsync(*v, 0, vb, ctx->stream));
@@ -328,7 +354,7 @@ int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
   KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
   s->it = 0;
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
-  // p0 = r0 is materialised by the first iteration's gather (first = 1)
+  KRY_HIP(hipMemcpyAsync(s->p, s->r, vb, hipMemcpyDeviceToDevice, st));  // p0 = r0 (cg.py:138)
   KRY_HIP(hipMemcpyAsync(rho0, s->scal + S_TMP * s->k, s->k * 8, hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
   s->started = true;

@@ -18,10 +18,6 @@ constexpr int kWave = 64;            // CDNA wavefront
 constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
 constexpr int kSlice = 64;           // SELL slice height = one wavefront
-constexpr int kGroupSlices = 8;      // slices per x-window group (512 rows)
-constexpr int kWindowMax = 3072;     // LDS x-window capacity (elements)
-constexpr int kMaxWindows = 64;      // runs per group
-constexpr int kWindowGap = 32;       // column gaps up to this are loaded through
 constexpr int kNumXcd = 8;
 
 // ---------------------------------------------------------------- errors

@@ -145,6 +145,20 @@ struct EpiCgAp {
   }
 };
 
+// CG: Ap = A p (nontemporal: read once, by the update pass) and <p, Ap>
+// (cg.py:178-183); xi is p_i, read by the bound source at row i.
+template <typename V>
+struct EpiApDot {
+  V *Ap;
+  const double *w;
+  int k;
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
+    __builtin_nontemporal_store(s, Ap + i * k + c);
+    const double pv = (double)xi;
+    return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
+  }
+};
+
 // MINRES Lanczos: w = A v - h0 * p_old (arnoldi.py:244-249) and <v, w>.
 template <typename V>
 struct EpiLanczos {
@@ -186,9 +200,10 @@ __device__ __forceinline__ bool halted(const Ctrl *ctrl, int step) {
 // flagged irregular (width -1) and walked in CSR form by the same lanes.
 // k > 1 right-hand sides: each lane keeps KT column accumulators; for k > 8
 // the waves split into k/8 column groups.
-template <typename V, typename MV, typename I, int KT, int UNR, class Src, class Epi>
+template <typename V, typename MV, typename I, int KT, int UNR, bool D16, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
+    const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
     const MV *__restrict__ sval, int64_t nslices, int64_t n, int k, const I *__restrict__ indptr,
     const I *__restrict__ indices, const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part,
     const Ctrl *ctrl, int step) {
@@ -216,15 +231,24 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
 #pragma unroll
     for (int c = 0; c < KT; ++c) acc[c] = V(0);
     if (w >= 0) {
-      const I *ci = sidx + sptr[s] + lane;
-      const MV *cv = sval + sptr[s] + lane;
+      const int64_t base = sptr[s];
+      const I *ci = sidx + base + lane;
+      const uint16_t *cd = sdelta + base + lane;
+      const int *cb = scbase + (base >> 6);  // slot-column bases: wave-uniform (scalar loads)
+      const MV *cv = sval + base + lane;
       for (int j0 = 0; j0 < w; j0 += UNR) {
         I col[UNR];
         V a[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const bool in = j0 + u < w;
-          col[u] = in ? __builtin_nontemporal_load(ci + (int64_t)(j0 + u) * 64) : I(-1);
+          if constexpr (D16) {
+            const unsigned d = in ? (unsigned)__builtin_nontemporal_load(cd + (int64_t)(j0 + u) * 64) : 0xFFFFu;
+            const int b = in ? cb[j0 + u] : 0;
+            col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
+          } else {
+            col[u] = in ? __builtin_nontemporal_load(ci + (int64_t)(j0 + u) * 64) : I(-1);
+          }
           a[u] = in ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
         }
         V xv[UNR][KT];
@@ -279,97 +303,6 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
   }
 }
 
-// ------------------------------------------ x-windowed SELL-64 SpMV (k = 1)
-// One workgroup per group of kGroupSlices slices (512 rows). If the group is
-// windowed, the block first stages its x runs into LDS with coalesced loads
-// (for CG the staging evaluates p = r + omega p_old once per element), then
-// every wave walks its slices exactly like spmv_sell_kernel but reads x from
-// LDS through the group-local indices: the per-nonzero gather no longer goes
-// through the texture/address units, only the matrix stream does. Groups
-// that are not windowed (scattered columns, irregular slices) gather from
-// global memory as before. Same summation order => bitwise csr_matvec.
-template <typename V, typename MV, typename I, int UNR, class Src, class Epi>
-__global__ __launch_bounds__(kBlock) void spmv_win_kernel(
-    const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
-    const int *__restrict__ sloc, const MV *__restrict__ sval, int64_t nslices, int64_t ngroups, int64_t n,
-    const int *__restrict__ gwin, const int64_t *__restrict__ wstart, const int *__restrict__ wlen,
-    const int *__restrict__ wlofs, const I *__restrict__ indptr, const I *__restrict__ indices,
-    const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part, const Ctrl *ctrl, int step) {
-  if (halted(ctrl, step)) return;
-  __shared__ V xw[kWindowMax];
-  __shared__ double red[kBlock];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t g0 = ngroups * g / gridDim.x, g1 = ngroups * (g + 1) / gridDim.x;
-  const auto bs = src.template bind<1>(0);
-  constexpr int SPW = kGroupSlices / 4;  // slices per wave per group
-  double dacc = 0.0;
-  for (int64_t grp = g0; grp < g1; ++grp) {
-    const int w0 = gwin[grp], w1 = gwin[grp + 1];
-    const bool windowed = w1 > w0;
-    if (windowed) {
-      for (int wi = w0; wi < w1; ++wi) {
-        const int64_t st = wstart[wi];
-        const int len = wlen[wi], lo = wlofs[wi];
-        for (int i = tid; i < len; i += kBlock) xw[lo + i] = bs(st + i, 0);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int sl = 0; sl < SPW; ++sl) {
-      const int64_t s = grp * kGroupSlices + wid * SPW + sl;
-      if (s < nslices) {
-        const int w = swidth[s];
-        const int64_t row = s * 64 + lane;
-        V acc = V(0);
-        if (w >= 0) {
-          const int64_t base = sptr[s] + lane;
-          for (int j0 = 0; j0 < w; j0 += UNR) {
-            int64_t col[UNR];
-            V a[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-              const bool in = j0 + u < w;
-              const int64_t off = base + (int64_t)(j0 + u) * 64;
-              if (windowed)
-                col[u] = in ? (int64_t)__builtin_nontemporal_load(sloc + off) : -1;
-              else
-                col[u] = in ? (int64_t)__builtin_nontemporal_load(sidx + off) : -1;
-              a[u] = in ? (V)__builtin_nontemporal_load(sval + off) : V(0);
-            }
-            V xv[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-              if (col[u] < 0) xv[u] = V(0);
-              else if (windowed) xv[u] = xw[col[u]];
-              else xv[u] = bs(col[u], 0);
-            }
-#pragma unroll
-            for (int u = 0; u < UNR; ++u)
-              if (col[u] >= 0) {
-                const V p = a[u] * xv[u];
-                acc = acc + p;
-              }
-          }
-        } else if (row < n) {
-          for (I e = indptr[row]; e < indptr[row + 1]; ++e) {
-            const V p = (V)data[e] * bs(indices[e], 0);
-            acc = acc + p;
-          }
-        }
-        if (row < n) dacc += epi(row, 0, acc, bs(row, 0));
-      }
-    }
-    __syncthreads();
-  }
-  if (part != nullptr) {
-    red[tid] = dacc;
-    block_tree_reduce(red, kBlock, 1);
-    if (tid == 0) part[g] = red[0];
-  }
-}
 
 // ---------------------------------------------------- elementwise passes
 // Op(e, N, acc) handles the W = 16/sizeof(V) consecutive elements at flat
@@ -537,9 +470,9 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
 }
 
 // -------------------------------------------------------- host launchers
-template <typename V, typename MV, typename I, int KT, int UNR, class Src, class Epi>
-int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
-                hipStream_t st) {
+template <typename V, typename MV, typename I, int KT, int UNR, bool D16, class Src, class Epi>
+int launch_sell_img(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
+                    hipStream_t st) {
   const int nch = k / KT;
   int64_t waves = A->nslices * nch;
   int grid = (int)((waves + 3) / 4);
@@ -547,12 +480,22 @@ int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const C
   if (grid < 1) grid = 1;
   if (nch > 1) grid = (grid + 7) / 8 * 8;  // 4 * grid must be a multiple of nch (<= 32)
   if (grid > kMaxGrid) grid = kMaxGrid;
-  hipLaunchKernelGGL((spmv_sell_kernel<V, MV, I, KT, UNR, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL((spmv_sell_kernel<V, MV, I, KT, UNR, D16, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
                      static_cast<const int64_t *>(A->sptr), static_cast<const int *>(A->swidth),
-                     static_cast<const I *>(A->sidx), static_cast<const MV *>(A->sval), A->nslices, A->n, k,
+                     static_cast<const I *>(A->sidx), static_cast<const uint16_t *>(A->sdelta),
+                     static_cast<const int *>(A->scbase), static_cast<const MV *>(A->sval), A->nslices, A->n, k,
                      static_cast<const I *>(A->indptr), static_cast<const I *>(A->indices),
                      static_cast<const MV *>(A->data), src, epi, part, ctrl, step);
   return grid;
+}
+
+template <typename V, typename MV, typename I, int KT, int UNR, class Src, class Epi>
+int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
+                hipStream_t st) {
+  if constexpr (sizeof(I) == 4) {
+    if (A->compact) return launch_sell_img<V, MV, I, KT, UNR, true>(A, k, src, epi, part, ctrl, step, st);
+  }
+  return launch_sell_img<V, MV, I, KT, UNR, false>(A, k, src, epi, part, ctrl, step, st);
 }
 
 // y-side epilogue Epi / x-side source Src composition of one SpMV launch;
@@ -562,25 +505,6 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                  int step, hipStream_t st) {
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
-  if (k == 1 && A->nwindowed > 0) {
-    static const int win_grid = [] {
-      const char *e = getenv("KRY_WIN_GRID");
-      return e ? atoi(e) : 1536;
-    }();
-    grid = (int)std::min<int64_t>(A->ngroups, win_grid);
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((spmv_win_kernel<V, MV, I, 16, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
-                       static_cast<const int64_t *>(A->sptr), static_cast<const int *>(A->swidth),
-                       static_cast<const I *>(A->sidx), static_cast<const int *>(A->sloc),
-                       static_cast<const MV *>(A->sval), A->nslices, A->ngroups, A->n,
-                       static_cast<const int *>(A->gwin), static_cast<const int64_t *>(A->wstart),
-                       static_cast<const int *>(A->wlen), static_cast<const int *>(A->wlofs),
-                       static_cast<const I *>(A->indptr), static_cast<const I *>(A->indices),
-                       static_cast<const MV *>(A->data), src, epi, part, ctrl, step);
-    KRY_HIP(hipGetLastError());
-    if (grid_out) *grid_out = grid;
-    return;
-  }
   switch (k) {
     case 1: grid = launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st); break;
     case 2: grid = launch_sell<V, MV, I, 2, 8>(A, k, src, epi, part, ctrl, step, st); break;

@@ -31,14 +31,12 @@ struct kry_csr {
   void *swidth = nullptr;   // int32, slice width, -1 = irregular (CSR walk)
   void *sidx = nullptr;     // itype, nslots (+ pad), -1 = padding
   void *sval = nullptr;     // dtype, nslots (+ pad)
-  // x-window image (single-RHS SpMV): groups of kGroupSlices slices whose x
-  // footprint fits LDS; sloc holds group-local column indices
-  int64_t ngroups = 0, nwindowed = 0;
-  void *gwin = nullptr;     // int32, ngroups + 1 offsets into the window list
-  void *wstart = nullptr;   // int64 first column of each window
-  void *wlen = nullptr;     // int32 window length
-  void *wlofs = nullptr;    // int32 window offset in the group's LDS image
-  void *sloc = nullptr;     // int32, nslots (+ pad): LDS index per slot
+  // compact column image (SELL-64/d16): when every slot column of every
+  // regular slice spans <= 65534 columns, sidx is replaced by a per-lane
+  // uint16 delta (0xFFFF = padding) over a per-slot-column int32 base
+  bool compact = false;
+  void *sdelta = nullptr;   // uint16, nslots (+ pad)
+  void *scbase = nullptr;   // int32, nslots / 64 (+ pad): base of slot column j of slice s at sptr[s] / 64 + j
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;

@@ -70,6 +70,12 @@ class CsrOperator:
     def device(self):
         return self.ctx.device
 
+    def layout(self):
+        """The device image: {"slices", "slots", "irregular", "compact"}."""
+        info = np.zeros(4, dtype=np.int64)
+        check(lib.kry_csr_info(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3])}
+
     def matvec_device(self, x, y):
         """y = A x for DeviceVectors (no host traffic)."""
         check(lib.kry_spmv(self.ctx.handle, self.handle, x.handle, y.handle))

@@ -15,14 +15,18 @@ def _golden_csr(d, key):
     return A
 
 
+@pytest.mark.parametrize("compact", ["1", "0"])
 @pytest.mark.parametrize("key", ["f64_i32", "f64_i64", "f32_i32", "f32_i64"])
-def test_spmv_bitwise_adversarial(golden, key):
+def test_spmv_bitwise_adversarial(golden, key, compact, monkeypatch):
     """Unsorted indices, duplicates, explicit zeros, empty rows, a 3000-nnz row
-    (longer than one LDS tile), magnitudes 1e+-20: bitwise SciPy."""
+    (an irregular slice), magnitudes 1e+-20: bitwise SciPy, with the column
+    indices stored as int32 and as compact uint16 deltas."""
     import krylov_amd
 
+    monkeypatch.setenv("KRY_SELL_COMPACT", compact)
     d = golden["spmv"]
     A = krylov_amd.CsrOperator(_golden_csr(d, key))
+    assert A.layout()["compact"] == (compact == "1")  # indices fit int32: CsrOperator passes int32
     y = A @ d[f"{key}_x"]
     np.testing.assert_array_equal(y.view(np.uint8), d[f"{key}_y"].view(np.uint8))
     Y = A @ d[f"{key}_X"]  # row-major block, csr_matvecs semantics
@@ -38,6 +42,66 @@ def test_spmv_block_widths(k):
     X = np.random.default_rng(k).standard_normal((3000, k))
     got = krylov_amd.CsrOperator(A) @ X
     np.testing.assert_array_equal(got, A @ X)
+
+
+@pytest.mark.parametrize("key", ["f64_i64", "f32_i64"])
+def test_spmv_int64_image_through_abi(golden, key):
+    """int64 indices handed straight to kry_csr_create keep an int64 image
+    (never compact) and stay bitwise."""
+    import ctypes
+
+    from krylov_amd import _lib
+    from krylov_amd.device import DeviceVector, get_context
+
+    d = golden["spmv"]
+    ctx = get_context()
+    ip, ix = d[f"{key}_indptr"].astype(np.int64), d[f"{key}_indices"].astype(np.int64)
+    dv = np.ascontiguousarray(d[f"{key}_data"])
+    n = ip.shape[0] - 1
+    h = ctypes.c_void_p()
+    _lib.check(_lib.lib.kry_csr_create(ctx.handle, n, ix.shape[0], _lib.ptr(ip), _lib.ptr(ix), _lib.ptr(dv),
+                                       _lib.dtype_code(dv.dtype), _lib.KRY_I64, ctypes.byref(h)))
+    try:
+        info = np.zeros(4, dtype=np.int64)
+        _lib.check(_lib.lib.kry_csr_info(h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        assert info[3] == 0
+        x = DeviceVector.from_host(ctx, d[f"{key}_x"])
+        y = DeviceVector(ctx, n, 1, dv.dtype)
+        _lib.check(_lib.lib.kry_spmv(ctx.handle, h, x.handle, y.handle))
+        got = y.to_host().reshape(-1)
+        np.testing.assert_array_equal(got.view(np.uint8), d[f"{key}_y"].view(np.uint8))
+    finally:
+        _lib.lib.kry_csr_destroy(h)
+
+
+def test_compact_image_selection():
+    """Stencils and bands get the compact image; a random sparsity pattern
+    (slot columns spanning more than 65534 columns) keeps int32 indices; the
+    two images give the same bits."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    S = problems.stencil15_3d(40)
+    assert krylov_amd.CsrOperator(S).layout()["compact"]
+    R = problems.random_nonsym(200_000, seed=1)
+    assert not krylov_amd.CsrOperator(R).layout()["compact"]
+    x = np.random.default_rng(0).standard_normal(S.shape[0])
+    np.testing.assert_array_equal(krylov_amd.CsrOperator(S) @ x, S @ x)
+
+
+def test_compact_boundary_spread(monkeypatch):
+    """Slot columns spanning exactly 65534 columns are compact, 65535 are not."""
+    import krylov_amd
+
+    n = 70_000
+    for span, expect in ((65534, True), (65535, False)):
+        rows = np.arange(64)
+        cols = np.where(rows == 0, span, 0).astype(np.int32)  # slot column 0 spans [0, span]
+        A = scipy.sparse.csr_matrix((np.arange(1.0, 65.0), (rows, cols)), shape=(n, n))
+        op = krylov_amd.CsrOperator(A)
+        assert op.layout()["compact"] == expect
+        x = np.random.default_rng(span).standard_normal(n)
+        np.testing.assert_array_equal(op @ x, A @ x)
 
 
 def test_spmv_mixed_f32_matrix_f64_vector():

@@ -2,8 +2,8 @@
 
 Reads <dir>/{micro,bench}_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv,
 averages the counters per kernel name (KiB per dispatch -> bytes), derives
-the read-side scale from the calibration kernel (known bytes = 12 * nslots of
-the 216^3 SELL-64 matrix) and reports the CG-fused SpMV kernel's corrected
+the read-side scale from the calibration kernel (known bytes = 10 * nslots of
+the 216^3 compact SELL-64 image) and reports the CG SpMV kernel's corrected
 traffic per launch next to its algorithmic bytes.
 """
 import csv
@@ -41,17 +41,18 @@ def main(out):
     nslices, nslots, nirr = _lib.csr_layout(A.indptr)
     f = lambda w, c: per_kernel(os.path.join(out, f"{w}_{c}", "run_counter_collection.csv"), c)
     mf, mw, bf, bw = f("micro", "FETCH_SIZE"), f("micro", "WRITE_SIZE"), f("bench", "FETCH_SIZE"), f("bench", "WRITE_SIZE")
-    cal_fetch, _ = find(mf, "sell_stream_calib")
-    scale = 12.0 * nslots / cal_fetch
-    fetch, name = find(bf, "spmv_sell_kernel", "SrcCgP", "EpiCgAp")
-    write, _ = find(bw, "spmv_sell_kernel", "SrcCgP", "EpiCgAp")
-    alg = bench.spmv_fused_bytes(n, nnz)
+    cal_fetch, _ = find(mf, "sell_stream_calib<unsigned short>")
+    scale = 10.0 * nslots / cal_fetch
+    fetch, name = find(bf, "spmv_sell_kernel", "true", "EpiApDot")
+    write, _ = find(bw, "spmv_sell_kernel", "true", "EpiApDot")
+    alg = bench.spmv_S(n, nnz)
     res = {
         "kernel": name,
         "fetch_raw_bytes": fetch,
         "write_bytes": write,
         "read_scale_from_calibration": scale,
-        "calibration": "sell_stream_calib: 12 B x nslots known bytes, FETCH_SIZE x 1024 measured",
+        "calibration": "sell_stream_calib<uint16>: the compact image's 2 + 8 B/lane nontemporal matrix stream, "
+                       "10 B x nslots known bytes, FETCH_SIZE x 1024 measured",
         "traffic_bytes_per_launch": fetch * scale + write,
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (fetch * scale + write) / alg,

@@ -86,91 +86,38 @@ __global__ __launch_bounds__(256) void read_ceiling(const int4 *__restrict__ a, 
 // wave). Algorithmic bytes = 12 * nslots; FETCH_SIZE / that = the counter's
 // scale for this access pattern (MI355X_MICROARCH.md "HBM": uncalibrated
 // widths must be calibrated on a known byte count).
-__global__ __launch_bounds__(256) void sell_stream_calib(const int *__restrict__ idx, const double *__restrict__ val,
+template <typename IX>
+__global__ __launch_bounds__(256) void sell_stream_calib(const IX *__restrict__ idx, const double *__restrict__ val,
                                                          int64_t ns, double *out) {
   double s = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-    const int c = __builtin_nontemporal_load(idx + i);
+    const IX c = __builtin_nontemporal_load(idx + i);
     const double v = __builtin_nontemporal_load(val + i);
-    s += c >= 0 ? v : 0.0;
+    s += c != IX(-1) ? v : 0.0;
   }
   if (s == 12345.678) out[0] = s;
 }
 
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v2i __attribute__((ext_vector_type(2)));
-typedef double v2d __attribute__((ext_vector_type(2)));
-// ---- prototype: SELL-64 with G consecutive columns per lane (slot-major) ----
-// slot(s, j, lane) = base_s + (j / G) * 64 G + lane * G + j % G; width padded to
-// a multiple of G with index -1. Index loads are G*4 B per lane, value loads
-// G*8 B per lane (two 16-B loads for G = 4).
-template <int G, int UNRG, bool CGP, bool NT = true, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void spmv_sellg(const int64_t *__restrict__ sptr, const int *__restrict__ swid,
-                                                 const int *__restrict__ sidx, const double *__restrict__ sval,
-                                                 int64_t nslices, int64_t n, const double *__restrict__ x,
-                                                 const double *__restrict__ pold, const double *__restrict__ omp,
-                                                 double *__restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t W = (int64_t)gridDim.x * 4, wg = (int64_t)g * 4 + wid;
-  const int64_t s0 = nslices * wg / W, s1 = nslices * (wg + 1) / W;
-  const double om = CGP ? omp[0] : 0.0;
-  for (int64_t s = s0; s < s1; ++s) {
-    const int ngrp = swid[s] / G;
-    const int *ci = sidx + sptr[s] + lane * G;
-    const double *cv = sval + sptr[s] + lane * G;
-    double acc = 0.0;
-    for (int q0 = 0; q0 < ngrp; q0 += UNRG) {
-      int col[UNRG][G];
-      double a[UNRG][G];
-#pragma unroll
-      for (int uq = 0; uq < UNRG; ++uq) {
-        const bool in = q0 + uq < ngrp;
-        const int64_t off = (int64_t)(q0 + uq) * 64 * G;
-        if constexpr (G == 4) {
-          v4i c4 = in ? __builtin_nontemporal_load(reinterpret_cast<const v4i *>(ci + off)) : v4i{-1, -1, -1, -1};
-          col[uq][0] = c4.x; col[uq][1] = c4.y; col[uq][2] = c4.z; col[uq][3] = c4.w;
-          v2d v0 = in ? __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cv + off)) : v2d{0, 0};
-          v2d v1 = in ? __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cv + off + 2)) : v2d{0, 0};
-          a[uq][0] = v0.x; a[uq][1] = v0.y; a[uq][2] = v1.x; a[uq][3] = v1.y;
-        } else if constexpr (G == 2) {
-          v2i c2 = in ? __builtin_nontemporal_load(reinterpret_cast<const v2i *>(ci + off)) : v2i{-1, -1};
-          col[uq][0] = c2.x; col[uq][1] = c2.y;
-          v2d v0 = in ? __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cv + off)) : v2d{0, 0};
-          a[uq][0] = v0.x; a[uq][1] = v0.y;
-        } else {
-          if (NT) {
-            col[uq][0] = in ? __builtin_nontemporal_load(ci + off) : -1;
-            a[uq][0] = in ? __builtin_nontemporal_load(cv + off) : 0.0;
-          } else {
-            col[uq][0] = in ? ci[off] : -1;
-            a[uq][0] = in ? cv[off] : 0.0;
-          }
-        }
-      }
-      double xv[UNRG][G];
-#pragma unroll
-      for (int uq = 0; uq < UNRG; ++uq)
-#pragma unroll
-        for (int e = 0; e < G; ++e) {
-          const int j = col[uq][e];
-          double v = j >= 0 ? x[j] : 0.0;
-          if (CGP) { const double t = om * (j >= 0 ? pold[j] : 0.0); v = v + t; }
-          xv[uq][e] = v;
-        }
-#pragma unroll
-      for (int uq = 0; uq < UNRG; ++uq)
-#pragma unroll
-        for (int e = 0; e < G; ++e)
-          if (col[uq][e] >= 0) { const double p = a[uq][e] * xv[uq][e]; acc = acc + p; }
+__global__ __launch_bounds__(256) void pupdate_kernel(const double *__restrict__ r, const double *__restrict__ pold,
+                                                      const double *__restrict__ om, double *__restrict__ p,
+                                                      int64_t n) {
+  const double o = om[0];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * i < n; i += stride) {
+    if (2 * i + 1 < n) {
+      const double2 rr = reinterpret_cast<const double2 *>(r)[i];
+      const double2 pp = reinterpret_cast<const double2 *>(pold)[i];
+      const double t0 = o * pp.x, t1 = o * pp.y;
+      reinterpret_cast<double2 *>(p)[i] = make_double2(rr.x + t0, rr.y + t1);
+    } else {
+      const double t0 = o * pold[2 * i];
+      p[2 * i] = r[2 * i] + t0;
     }
-    const int64_t row = s * 64 + lane;
-    if (row < n) y[row] = acc;
   }
 }
+
 
 int main(int argc, char **argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 216;
@@ -184,13 +131,21 @@ int main(int argc, char **argv) {
 
   kry_ctx *ctx;
   KC(kry_ctx_create(0, &ctx));
-  kry_csr *A;
+  // A: the library's default image (compact uint16 deltas for this stencil);
+  // A32: the same matrix with int32 indices (KRY_SELL_COMPACT=0)
+  kry_csr *A, *A32;
   auto t0 = std::chrono::steady_clock::now();
   KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
-  printf("upload + SELL-64 build %.2fs: %ld slices, %ld slots (%.2f%% padding), %ld irregular\n",
+  printf("upload + SELL-64 build %.2fs: %ld slices, %ld slots (%.2f%% padding), %ld irregular, compact %d\n",
          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), A->nslices, A->nslots,
-         100.0 * (A->nslots - nnz) / nnz, A->nirregular);
-  printf("x-window groups: %ld of %ld windowed\n", A->nwindowed, A->ngroups);
+         100.0 * (A->nslots - nnz) / nnz, A->nirregular, (int)A->compact);
+  setenv("KRY_SELL_COMPACT", "0", 1);
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A32));
+  unsetenv("KRY_SELL_COMPACT");
+  if (!A->compact || A32->compact || !A32->sidx) {
+    fprintf(stderr, "unexpected images (compact %d / %d)\n", (int)A->compact, (int)A32->compact);
+    return 1;
+  }
 
   double *d_x, *d_y, *d_p, *d_ap, *d_om, *d_out, *part;
   CK(hipMalloc(&d_x, n * 8));
@@ -223,6 +178,7 @@ int main(int argc, char **argv) {
     y2ref[i] = s2;
   }
 
+  CK(hipMemcpy(d_p, pref.data(), n * 8, hipMemcpyHostToDevice));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -253,89 +209,45 @@ int main(int argc, char **argv) {
   };
 
   report("read ceiling (SELL idx+val, 16 B/lane)", nnz * 12.0, [&] {
-    hipLaunchKernelGGL(read_ceiling, dim3(2048), dim3(256), 0, 0, (const int4 *)A->sidx, nnz / 4,
-                       (const double2 *)A->sval, nnz / 2, d_out);
+    hipLaunchKernelGGL(read_ceiling, dim3(2048), dim3(256), 0, 0, (const int4 *)A32->sidx, nnz / 4,
+                       (const double2 *)A32->sval, nnz / 2, d_out);
   });
-  report("SELL stream calibration (4+8 B/lane nt)", A->nslots * 12.0, [&] {
-    hipLaunchKernelGGL(sell_stream_calib, dim3(8192), dim3(256), 0, 0, (const int *)A->sidx,
+  report("SELL stream calibration (4+8 B/lane nt)", A32->nslots * 12.0, [&] {
+    hipLaunchKernelGGL(sell_stream_calib<int>, dim3(8192), dim3(256), 0, 0, (const int *)A32->sidx,
+                       (const double *)A32->sval, A32->nslots, d_out);
+  });
+  report("d16 stream calibration (2+8 B/lane nt)", A->nslots * 10.0, [&] {
+    hipLaunchKernelGGL(sell_stream_calib<uint16_t>, dim3(8192), dim3(256), 0, 0, (const uint16_t *)A->sdelta,
                        (const double *)A->sval, A->nslots, d_out);
   });
-  report("library SELL SpMV y = A x", S, [&] {
-    launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr, nullptr,
-                                     nullptr, 0, 0);
-  });
-  check("y = A x", d_y, yref);
-  report("library SELL SpMV + <x, y> partials", S, [&] {
-    launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_x, 1}, EpiStoreDot<double>{d_y, d_x, nullptr, 1},
-                                     part, nullptr, nullptr, 0, 0);
-  });
-  check("y = A x (dot epilogue)", d_y, yref);
-  SrcCgP<double> src{d_x, d_x, d_om, 1, 0};
-  report("library CG-fused p-update+SpMV+<p,Ap>", S + 16.0 * n, [&] {
-    launch_spmv<double, double, int>(A, 1, src, EpiCgAp<double>{d_ap, d_p, src, nullptr, 1}, part, nullptr,
-                                     nullptr, 0, 0);
-  });
-  check("Ap (CG-fused)", d_ap, y2ref);
-  check("p  (CG-fused)", d_p, pref);
-
-  {
-    const int G = 1;
-    const int64_t ns = (n + 63) / 64;
-    std::vector<int64_t> sp(ns + 1, 0);
-    std::vector<int> sw(ns);
-    for (int64_t s2 = 0; s2 < ns; ++s2) {
-      int w = 0;
-      for (int64_t r = s2 * 64; r < std::min<int64_t>(n, s2 * 64 + 64); ++r) w = std::max(w, ip[r + 1] - ip[r]);
-      sw[s2] = w;
-      sp[s2 + 1] = sp[s2] + 64 * w;
-    }
-    const int64_t slots = sp[ns];
-    std::vector<int> si(slots + 1024, -1);
-    std::vector<double> sv(slots + 1024, 0.0);
-    for (int64_t s2 = 0; s2 < ns; ++s2)
-      for (int l = 0; l < 64; ++l) {
-        const int64_t r = s2 * 64 + l;
-        if (r >= n) continue;
-        for (int e = ip[r]; e < ip[r + 1]; ++e) {
-          const int j = e - ip[r];
-          const int64_t slot = sp[s2] + (int64_t)(j / G) * 64 * G + l * G + j % G;
-          si[slot] = ix[e];
-          sv[slot] = dv[e];
-        }
-      }
-    int64_t *d_sp;
-    int *d_sw, *d_si;
-    double *d_sv;
-    CK(hipMalloc(&d_sp, sp.size() * 8));
-    CK(hipMalloc(&d_sw, sw.size() * 4));
-    CK(hipMalloc(&d_si, si.size() * 4));
-    CK(hipMalloc(&d_sv, sv.size() * 8));
-    CK(hipMemcpy(d_sp, sp.data(), sp.size() * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(d_sw, sw.data(), sw.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(d_si, si.data(), si.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(d_sv, sv.data(), sv.size() * 8, hipMemcpyHostToDevice));
-#define PV(UNR, NTF, MINW, GRID)                                                                                 \
-    {                                                                                                            \
-      char nm[96];                                                                                               \
-      snprintf(nm, 96, "proto U%d nt=%d minw=%d grid=%d", UNR, (int)NTF, MINW, GRID);                            \
-      report(nm, S, [&] {                                                                                        \
-        hipLaunchKernelGGL((spmv_sellg<1, UNR, false, NTF, MINW>), dim3(GRID), dim3(256), 0, 0, d_sp, d_sw, d_si, \
-                           d_sv, ns, n, d_x, d_x, d_om, d_y);                                                    \
-      });                                                                                                        \
-    }
-    PV(16, true, 1, 2048)
-    PV(16, false, 1, 2048)
-    PV(8, true, 1, 2048)
-    PV(4, true, 1, 2048)
-    PV(24, true, 1, 2048)
-    PV(16, true, 1, 1024)
-    PV(16, true, 1, 4096)
-    PV(16, true, 1, 8192)
-    PV(8, true, 2, 2048)
-    PV(8, true, 4, 4096)
-    PV(16, true, 2, 4096)
-    check("last proto", d_y, yref);
+  for (kry_csr *M : {A32, A}) {
+    const char *tag = M->compact ? "d16" : "i32";
+    char nm[96];
+    snprintf(nm, 96, "SELL %s y = A x", tag);
+    report(nm, S, [&] {
+      launch_spmv<double, double, int>(M, 1, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr, nullptr,
+                                       nullptr, 0, 0);
+    });
+    check(nm, d_y, yref);
+    snprintf(nm, 96, "SELL %s CG: Ap = A p, <p, Ap>", tag);
+    report(nm, S, [&] {
+      launch_spmv<double, double, int>(M, 1, SrcPlain<double>{d_p, 1}, EpiApDot<double>{d_ap, nullptr, 1}, part,
+                                       nullptr, nullptr, 0, 0);
+    });
+    check(nm, d_ap, y2ref);
+    snprintf(nm, 96, "SELL %s fused p-update + SpMV (old CG)", tag);
+    SrcCgP<double> src{d_x, d_x, d_om, 1, 0};
+    report(nm, S + 16.0 * n, [&] {
+      launch_spmv<double, double, int>(M, 1, src, EpiCgAp<double>{d_ap, d_y, src, nullptr, 1}, part, nullptr,
+                                       nullptr, 0, 0);
+    });
+    check(nm, d_ap, y2ref);
   }
+  report("CG p pass p = r + om p_old (3 vectors)", 24.0 * n, [&] {
+    hipLaunchKernelGGL(pupdate_kernel, dim3(4096), dim3(256), 0, 0, d_x, d_x, d_om, d_y, n);
+  });
+  check("p pass", d_y, pref);
+  KC(kry_csr_destroy(A32));
   KC(kry_csr_destroy(A));
   KC(kry_ctx_destroy(ctx));
   return 0;
