@@ -81,10 +81,12 @@ int kry_csr_destroy(kry_csr *A);
  * kernel walks in CSR form instead. */
 int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
                    int64_t *nslots, int64_t *nirregular);
-/* The device image kry_csr_create built: info[0..3] = slices, slots,
+/* The device image kry_csr_create built: info[0..4] = slices, slots,
  * irregular slices, compact (1 when the column indices are stored as uint16
  * deltas over per-slot-column int32 bases: every slot column spans <= 65534
- * columns, int32 indices and KRY_SELL_COMPACT != 0 in the environment). */
+ * columns, int32 indices and KRY_SELL_COMPACT != 0 in the environment), and
+ * the number of column blocks of the column-blocked image used by
+ * single-RHS SpMVs on scattered sparsity (0 = none; KRY_SPMV_CB=0 disables). */
 int kry_csr_info(const kry_csr *A, int64_t *info);
 
 /* ---- vectors (n x k row-major blocks) ---------------------------------- */

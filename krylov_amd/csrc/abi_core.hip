@@ -229,6 +229,7 @@ int kry_csr_info(const kry_csr *A, int64_t *info) {
   info[1] = A->nslots;
   info[2] = A->nirregular;
   info[3] = A->compact ? 1 : 0;
+  info[4] = A->cb_nb;
   KRY_API_END
 }
 
@@ -291,6 +292,104 @@ static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int
   return ok.load();
 }
 
+// Column-blocked image (see kry_csr::cb_*). Returns false when not useful or
+// not possible: rows not sorted, x small enough to stay cache-resident, the
+// columns not scattered (most entries within half a block of the diagonal),
+// or a segment too long for uint16 offsets.
+template <typename MV>
+struct CbHost {
+  int64_t nb = 0, cols = 0, ng = 0;
+  std::vector<int64_t> gptr;
+  std::vector<uint16_t> roff;
+  std::vector<int32_t> col;
+  std::vector<MV> val;
+};
+
+template <typename I, typename MV>
+static bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<MV> &cb) {
+  if (sizeof(I) != 4 || n * 8 < (int64_t(8) << 20)) return false;
+  const int64_t nnz = (int64_t)ip[n];
+  const char *cenv = getenv("KRY_CB_COLS");  // tuning override: columns per block
+  int64_t cols = cenv ? std::max<int64_t>(1024, atoll(cenv)) : std::max<int64_t>(int64_t(1) << 18, (n + 15) / 16);
+  const int64_t nb = (n + cols - 1) / cols;
+  if (nb < 2) return false;
+  // sorted rows and scattered columns
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<int64_t> far(nt, 0);
+  std::atomic<bool> sorted{true};
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+        int64_t f = 0;
+        for (int64_t r = r0; r < r1; ++r)
+          for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
+            if (e > ip[r] && ix[e] < ix[e - 1]) sorted = false;
+            const int64_t d = (int64_t)ix[e] - r;
+            f += (d > cols / 2 || d < -cols / 2);
+          }
+        far[t] = f;
+      });
+    for (auto &x : th) x.join();
+  }
+  int64_t nfar = 0;
+  for (int64_t f : far) nfar += f;
+  if (!sorted || nnz == 0 || nfar * 4 < nnz) return false;
+  const int64_t ng = (n + kCbRows - 1) / kCbRows;
+  // per (block, row) counts -> per (block, group) segment lengths
+  std::vector<uint16_t> roff(nb * n + 256, 0);
+  std::vector<int64_t> seg(nb * ng, 0);
+  std::atomic<bool> fits{true};
+  auto pass1 = [&](int64_t g0, int64_t g1) {
+    std::vector<int64_t> cnt(nb);
+    for (int64_t g = g0; g < g1; ++g) {
+      std::fill(cnt.begin(), cnt.end(), 0);
+      const int64_t r0 = g * kCbRows, r1 = std::min<int64_t>(n, r0 + kCbRows);
+      for (int64_t r = r0; r < r1; ++r) {
+        for (int64_t b = 0; b < nb; ++b) {
+          if (cnt[b] > 65535) fits = false;
+          roff[b * n + r] = (uint16_t)cnt[b];
+        }
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) cnt[ix[e] / cols]++;
+      }
+      for (int64_t b = 0; b < nb; ++b) {
+        if (cnt[b] > 65535) fits = false;
+        seg[b * ng + g] = cnt[b];
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass1, ng * t / nt, ng * (t + 1) / nt);
+  for (auto &x : th) x.join();
+  th.clear();
+  if (!fits) return false;
+  cb.gptr.assign(nb * ng + 1, 0);
+  for (int64_t i = 0; i < nb * ng; ++i) cb.gptr[i + 1] = cb.gptr[i] + seg[i];
+  cb.col.assign(nnz + 256, 0);
+  cb.val.assign(nnz + 256, MV(0));
+  auto pass2 = [&](int64_t g0, int64_t g1) {
+    std::vector<int64_t> pos(nb);
+    for (int64_t g = g0; g < g1; ++g) {
+      for (int64_t b = 0; b < nb; ++b) pos[b] = cb.gptr[b * ng + g];
+      const int64_t r0 = g * kCbRows, r1 = std::min<int64_t>(n, r0 + kCbRows);
+      for (int64_t r = r0; r < r1; ++r)
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
+          const int64_t p = pos[ix[e] / cols]++;
+          cb.col[p] = (int32_t)ix[e];
+          cb.val[p] = dv[e];
+        }
+    }
+  };
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass2, ng * t / nt, ng * (t + 1) / nt);
+  for (auto &x : th) x.join();
+  cb.nb = nb;
+  cb.cols = cols;
+  cb.ng = ng;
+  cb.roff = std::move(roff);
+  return true;
+}
+
 namespace {
 template <typename I, typename MV>
 void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
@@ -326,6 +425,26 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
   if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
   KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+  // column-blocked image for scattered single-RHS SpMVs (KRY_SPMV_CB=0 disables)
+  const char *cbenv = getenv("KRY_SPMV_CB");
+  if (!(cbenv && atoi(cbenv) == 0)) {
+    CbHost<MV> cb;
+    if (cb_build(n, ip, ix, dv, cb)) {
+      A->cb_nb = cb.nb;
+      A->cb_cols = cb.cols;
+      A->cb_ng = cb.ng;
+      A->cb_gptr = dev_alloc(cb.gptr.size() * 8);
+      A->cb_roff = dev_alloc(cb.roff.size() * 2);
+      A->cb_col = dev_alloc(cb.col.size() * 4);
+      A->cb_val = dev_alloc(cb.val.size() * sizeof(MV));
+      A->cb_y = dev_alloc((size_t)n * 8 + 64);
+      KRY_HIP(hipMemcpyAsync(A->cb_gptr, cb.gptr.data(), cb.gptr.size() * 8, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->cb_roff, cb.roff.data(), cb.roff.size() * 2, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->cb_col, cb.col.data(), cb.col.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->cb_val, cb.val.data(), cb.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipStreamSynchronize(st));
+    }
+  }
   if (A->nirregular > 0) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
     A->indices = dev_alloc((nnz + 1) * sizeof(I));
@@ -341,7 +460,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 }  // namespace
 
 static void csr_free(kry_csr *A) {
-  void *bufs[] = {A->sptr, A->swidth, A->sidx, A->sval, A->indptr, A->indices, A->data, A->sdelta, A->scbase};
+  void *bufs[] = {A->sptr,   A->swidth, A->sidx,   A->sval,   A->indptr, A->indices, A->data,
+                  A->sdelta, A->scbase, A->cb_gptr, A->cb_roff, A->cb_col, A->cb_val,  A->cb_y};
   for (void *b : bufs) dev_free(b);
 }
 

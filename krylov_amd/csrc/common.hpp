@@ -18,6 +18,8 @@ constexpr int kWave = 64;            // CDNA wavefront
 constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
 constexpr int kSlice = 64;           // SELL slice height = one wavefront
+constexpr int kCbRows = 256;         // rows per column-blocked segment (one per thread)
+constexpr int kCbCap = 1024;         // products staged in LDS per chunk
 constexpr int kNumXcd = 8;
 
 // ---------------------------------------------------------------- errors

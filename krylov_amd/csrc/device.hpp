@@ -469,6 +469,75 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
   }
 }
 
+// ------------------------------------------- column-blocked SpMV (k = 1)
+// Pass b of cb_nb: each block takes 256-row groups; the group's entries with
+// columns in block b (stored in row order) are multiplied against the
+// L2-resident x block with coalesced loads and staged in LDS, then thread r
+// adds its row's products to the running sum in stored order (the same
+// sequence of roundings as csr_matvec: sum from 0, product rounded, then
+// added). The running sums live in cb_y between passes; the last pass applies
+// the epilogue.
+template <typename V, typename MV, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t n, int64_t ng,
+                                                         const int64_t *__restrict__ gptr,
+                                                         const uint16_t *__restrict__ roff,
+                                                         const int *__restrict__ col, const MV *__restrict__ val,
+                                                         double *__restrict__ ysum, Src src, Epi epi,
+                                                         double *__restrict__ part, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ V prod[kCbCap];
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const auto bs = src.template bind<1>(0);
+  const bool last = b + 1 == nb;
+  double dacc = 0.0;
+  for (int64_t g = blockIdx.x; g < ng; g += gridDim.x) {
+    const int64_t s0 = gptr[(int64_t)b * ng + g];
+    const int len = (int)(gptr[(int64_t)b * ng + g + 1] - s0);
+    const int64_t row = g * kCbRows + tid;
+    const bool has = row < n;
+    int r0 = 0, r1 = 0;
+    if (has) {
+      r0 = roff[(int64_t)b * n + row];
+      r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
+    }
+    V acc = (b == 0 || !has) ? V(0) : (V)ysum[row];
+    for (int c0 = 0; c0 < len; c0 += kCbCap) {
+      const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
+      __syncthreads();  // the previous chunk has been consumed
+      // kCbCap / kBlock entries per thread, all loads issued before the gathers
+      constexpr int U = kCbCap / kBlock;
+      int j[U];
+      V a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = c0 + tid + u * kBlock;
+        j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
+        a[u] = e < c1 ? (V)__builtin_nontemporal_load(val + s0 + e) : V(0);
+      }
+      V xj[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xj[u] = j[u] >= 0 ? bs(j[u], 0) : V(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j[u] >= 0) prod[tid + u * kBlock] = a[u] * xj[u];
+      __syncthreads();
+      const int lo = r0 > c0 ? r0 : c0, hi = r1 < c1 ? r1 : c1;
+      for (int e = lo; e < hi; ++e) acc = acc + prod[e - c0];
+    }
+    if (has) {
+      if (!last) ysum[row] = (double)acc;
+      else dacc += epi(row, 0, acc, bs(row, 0));
+    }
+  }
+  if (last && part != nullptr) {
+    __syncthreads();
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[blockIdx.x] = red[0];
+  }
+}
+
 // -------------------------------------------------------- host launchers
 template <typename V, typename MV, typename I, int KT, int UNR, bool D16, class Src, class Epi>
 int launch_sell_img(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
@@ -505,6 +574,24 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                  int step, hipStream_t st) {
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
+  if constexpr (sizeof(I) == 4) {
+    if (k == 1 && A->cb_nb > 0) {
+      static const int cb_grid = [] {
+        const char *e = getenv("KRY_CB_GRID");  // tuning override
+        return e ? std::max(1, std::min(atoi(e), kMaxGrid)) : kMaxGrid;
+      }();
+      grid = (int)std::min<int64_t>(A->cb_ng, cb_grid);
+      for (int b = 0; b < (int)A->cb_nb; ++b)
+        hipLaunchKernelGGL((spmv_cb_kernel<V, MV, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, b, (int)A->cb_nb,
+                           A->n, A->cb_ng, static_cast<const int64_t *>(A->cb_gptr),
+                           static_cast<const uint16_t *>(A->cb_roff), static_cast<const int *>(A->cb_col),
+                           static_cast<const MV *>(A->cb_val), static_cast<double *>(A->cb_y), src, epi, part,
+                           ctrl, step);
+      KRY_HIP(hipGetLastError());
+      if (grid_out) *grid_out = grid;
+      return;
+    }
+  }
   switch (k) {
     case 1: grid = launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st); break;
     case 2: grid = launch_sell<V, MV, I, 2, 8>(A, k, src, epi, part, ctrl, step, st); break;

@@ -71,10 +71,11 @@ class CsrOperator:
         return self.ctx.device
 
     def layout(self):
-        """The device image: {"slices", "slots", "irregular", "compact"}."""
-        info = np.zeros(4, dtype=np.int64)
+        """The device image: {"slices", "slots", "irregular", "compact", "col_blocks"}."""
+        info = np.zeros(5, dtype=np.int64)
         check(lib.kry_csr_info(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
-        return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3])}
+        return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3]),
+                "col_blocks": int(info[4])}
 
     def matvec_device(self, x, y):
         """y = A x for DeviceVectors (no host traffic)."""

@@ -104,6 +104,69 @@ def test_compact_boundary_spread(monkeypatch):
         np.testing.assert_array_equal(op @ x, A @ x)
 
 
+def _scattered_csr(n, lens, seed, sort=True, dtype=np.float64):
+    """CSR with lens[i] uniform random columns in row i (scattered sparsity)."""
+    rng = np.random.default_rng(seed)
+    lens = np.asarray(lens, dtype=np.int64)
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    rows = np.repeat(np.arange(n), lens)
+    cols = rng.integers(0, n, indptr[-1])
+    if sort:
+        order = np.lexsort((cols, rows))
+        cols = cols[order]
+    vals = rng.standard_normal(indptr[-1]).astype(dtype)
+    A = scipy.sparse.csr_matrix((vals, cols.astype(np.int32), indptr.astype(np.int32)), shape=(n, n))
+    return A
+
+
+def test_column_blocked_cfg3_bitwise(monkeypatch):
+    """cfg3's scattered matrix gets the column-blocked image (8 blocks of
+    262144 columns); it and the SELL image both give SciPy's bits."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    R = problems.random_nonsym(2_000_000)
+    x = np.random.default_rng(5).standard_normal(R.shape[0])
+    ref = R @ x
+    A = krylov_amd.CsrOperator(R)
+    assert A.layout()["col_blocks"] == 8
+    np.testing.assert_array_equal(A @ x, ref)
+    monkeypatch.setenv("KRY_SPMV_CB", "0")
+    A0 = krylov_amd.CsrOperator(R)
+    assert A0.layout()["col_blocks"] == 0
+    np.testing.assert_array_equal(A0 @ x, ref)
+
+
+def test_column_blocked_long_segments_and_empty_rows():
+    """Segments longer than one LDS chunk (rows of 150 entries in the first
+    groups), empty rows, a ragged last group, float32 data."""
+    import krylov_amd
+
+    n = 1_200_003
+    lens = np.full(n, 6)
+    lens[:700] = 150
+    lens[1000:1300] = 0
+    for dt in (np.float64, np.float32):
+        A = _scattered_csr(n, lens, seed=11, dtype=dt)
+        op = krylov_amd.CsrOperator(A)
+        assert op.layout()["col_blocks"] == 5
+        x = np.random.default_rng(3).standard_normal(n).astype(dt)
+        np.testing.assert_array_equal(op @ x, A @ x)
+        x64 = np.random.default_rng(4).standard_normal(n)
+        np.testing.assert_array_equal(op @ x64, A @ x64)  # float32 matrix, float64 vector
+
+
+def test_column_blocked_not_built_for_unsorted_rows():
+    import krylov_amd
+
+    n = 1_200_000
+    A = _scattered_csr(n, np.full(n, 6), seed=2, sort=False)
+    op = krylov_amd.CsrOperator(A)
+    assert op.layout()["col_blocks"] == 0
+    x = np.random.default_rng(1).standard_normal(n)
+    np.testing.assert_array_equal(op @ x, A @ x)
+
+
 def test_spmv_mixed_f32_matrix_f64_vector():
     import krylov_amd
     from krylov_amd import problems

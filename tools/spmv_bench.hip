@@ -100,6 +100,61 @@ __global__ __launch_bounds__(256) void sell_stream_calib(const IX *__restrict__ 
 }
 
 
+
+// ---- prototype: compact SELL with the next slice's matrix stream issued
+// right after the current slice's gathers (software pipelining); w <= UNR.
+template <int UNR, int MINW>
+__global__ __launch_bounds__(256, MINW) void spmv_pf(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                     const uint16_t *__restrict__ sdelta,
+                                                     const int *__restrict__ scbase, const double *__restrict__ sval,
+                                                     int64_t nslices, int64_t n, const double *__restrict__ x,
+                                                     double *__restrict__ y) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  if (s_begin >= s_end) return;
+  unsigned dA[UNR], dB[UNR];
+  double aA[UNR], aB[UNR];
+  int bA[UNR], bB[UNR];
+  auto load = [&](int64_t s, unsigned(&d)[UNR], double(&a)[UNR], int(&b)[UNR]) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool in = u < w;
+      d[u] = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)u * 64 + lane) : 0xFFFFu;
+      a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)u * 64 + lane) : 0.0;
+      b[u] = in ? scbase[(base >> 6) + u] : 0;
+    }
+  };
+  load(s_begin, dA, aA, bA);
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    double xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) xv[u] = dA[u] != 0xFFFFu ? x[bA[u] + (int)dA[u]] : 0.0;
+    if (s + 1 < s_end) load(s + 1, dB, aB, bB);
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (dA[u] != 0xFFFFu) {
+        const double p = aA[u] * xv[u];
+        acc = acc + p;
+      }
+    const int64_t row = s * 64 + lane;
+    if (row < n) y[row] = acc;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      dA[u] = dB[u];
+      aA[u] = aB[u];
+      bA[u] = bB[u];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void pupdate_kernel(const double *__restrict__ r, const double *__restrict__ pold,
                                                       const double *__restrict__ om, double *__restrict__ p,
                                                       int64_t n) {
@@ -119,7 +174,138 @@ __global__ __launch_bounds__(256) void pupdate_kernel(const double *__restrict__
 }
 
 
+// Random gather study (cfg3 shape): n rows, 19 uniform random off-diagonal
+// columns in [0, span) plus the diagonal, sorted per row. span = n is the
+// cfg3 pattern (x = 16 MB, not L2-resident); a small span keeps x in L2.
+static int random_study(int64_t n, int reps) {
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  double *d_x, *d_y;
+  CK(hipMalloc(&d_x, n * 8));
+  CK(hipMalloc(&d_y, n * 8));
+  std::vector<double> xh(n, 1.0);
+  CK(hipMemcpy(d_x, xh.data(), n * 8, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int64_t span : {n, n / 2, n / 4, n / 8, n / 16, n / 64}) {
+    std::vector<int> ip(n + 1, 0), ix;
+    std::vector<double> dv;
+    ix.reserve(n * 20);
+    dv.reserve(n * 20);
+    uint64_t st = 0x9E3779B97F4A7C15ull;
+    std::vector<int> row;
+    for (int64_t r = 0; r < n; ++r) {
+      row.clear();
+      row.push_back((int)r);
+      for (int j = 0; j < 19; ++j) {
+        st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+        row.push_back((int)(st % (uint64_t)span));
+      }
+      std::sort(row.begin(), row.end());
+      for (int c : row) { ix.push_back(c); dv.push_back(0.5); }
+      ip[r + 1] = (int)ix.size();
+    }
+    const int64_t nnz = ix.size();
+    const double S = nnz * 12.0 + (n + 1) * 4.0 + 2.0 * n * 8.0;
+    for (int cbmode : {1, 0}) {
+    if (!cbmode) setenv("KRY_SPMV_CB", "0", 1);
+    kry_csr *A;
+    KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+    unsetenv("KRY_SPMV_CB");
+    auto launch = [&] {
+      launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr, nullptr,
+                                       nullptr, 0, 0);
+    };
+    launch();
+    CK(hipDeviceSynchronize());
+    float tot = 0;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      tot += ms;
+    }
+    printf("random n=%ld span=%ld (x window %.1f MB) compact=%d col_blocks=%ld: %.4f ms  %.0f GB/s (S)\n", n, span,
+           span * 8 / 1e6, (int)A->compact, A->cb_nb, tot / reps, S / (tot / reps) / 1e6);
+    KC(kry_csr_destroy(A));
+    if (span != n) break;
+    }
+  }
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
+
+// Column-blocked image tuning on the cfg3 pattern: block width x launch grid.
+static int cb_tune(int64_t n, int reps) {
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  double *d_x, *d_y;
+  CK(hipMalloc(&d_x, n * 8));
+  CK(hipMalloc(&d_y, n * 8));
+  std::vector<double> xh(n, 1.0);
+  CK(hipMemcpy(d_x, xh.data(), n * 8, hipMemcpyHostToDevice));
+  std::vector<int> ip(n + 1, 0), ix;
+  std::vector<double> dv;
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  std::vector<int> row;
+  for (int64_t r = 0; r < n; ++r) {
+    row.clear();
+    row.push_back((int)r);
+    for (int j = 0; j < 19; ++j) {
+      st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+      row.push_back((int)(st % (uint64_t)n));
+    }
+    std::sort(row.begin(), row.end());
+    for (int c : row) { ix.push_back(c); dv.push_back(0.5); }
+    ip[r + 1] = (int)ix.size();
+  }
+  const int64_t nnz = ix.size();
+  const double S = nnz * 12.0 + (n + 1) * 4.0 + 2.0 * n * 8.0;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (const char *cols : {"131072", "262144", "524288"}) {
+    setenv("KRY_CB_COLS", cols, 1);
+    kry_csr *A;
+    KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+    for (int grid : {1024, 2048, 4096, 8192}) {
+      auto launch = [&] {
+        for (int bb = 0; bb < (int)A->cb_nb; ++bb)
+          hipLaunchKernelGGL((spmv_cb_kernel<double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
+                             dim3(kBlock), 0, 0, bb, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr,
+                             (const uint16_t *)A->cb_roff, (const int *)A->cb_col, (const double *)A->cb_val,
+                             (double *)A->cb_y, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1},
+                             (double *)nullptr, (const Ctrl *)nullptr, 0);
+      };
+      launch();
+      CK(hipDeviceSynchronize());
+      float tot = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+      }
+      printf("cb cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
+             S / (tot / reps) / 1e6);
+    }
+    KC(kry_csr_destroy(A));
+  }
+  unsetenv("KRY_CB_COLS");
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "random") == 0) return random_study(argc > 2 ? atol(argv[2]) : 2000000, 10);
+  if (argc > 1 && strcmp(argv[1], "cbtune") == 0) return cb_tune(argc > 2 ? atol(argv[2]) : 2000000, 10);
   const int m = argc > 1 ? atoi(argv[1]) : 216;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
   std::vector<int> ip, ix;
@@ -242,6 +428,37 @@ int main(int argc, char **argv) {
                                        nullptr, 0, 0);
     });
     check(nm, d_ap, y2ref);
+  }
+#define PF(UNR, MINW, GRID)                                                                                  \
+  {                                                                                                          \
+    char nm[96];                                                                                             \
+    snprintf(nm, 96, "proto pipelined d16 U%d minw=%d grid=%d", UNR, MINW, GRID);                            \
+    report(nm, S, [&] {                                                                                      \
+      hipLaunchKernelGGL((spmv_pf<UNR, MINW>), dim3(GRID), dim3(256), 0, 0, (const int64_t *)A->sptr,          \
+                         (const int *)A->swidth, (const uint16_t *)A->sdelta, (const int *)A->scbase,           \
+                         (const double *)A->sval, A->nslices, n, d_x, d_y);                                    \
+    });                                                                                                      \
+    check(nm, d_y, yref);                                                                                    \
+  }
+  PF(16, 1, 8192)
+  PF(16, 1, 2048)
+  PF(16, 1, 1024)
+  PF(16, 2, 2048)
+  {
+    // the library kernel at other grid sizes (KRY_SPMV_GRID)
+    for (int gsz : {1024, 2048, 4096}) {
+      char nm[96];
+      snprintf(nm, 96, "SELL d16 y = A x grid=%d", gsz);
+      report(nm, S, [&] {
+        hipLaunchKernelGGL((spmv_sell_kernel<double, double, int, 1, 16, true, SrcPlain<double>, EpiStore<double>>),
+                           dim3(gsz), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                           (const int *)nullptr, (const uint16_t *)A->sdelta, (const int *)A->scbase,
+                           (const double *)A->sval, A->nslices, n, 1, (const int *)nullptr, (const int *)nullptr,
+                           (const double *)nullptr, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1},
+                           (double *)nullptr, (const Ctrl *)nullptr, 0);
+      });
+      check(nm, d_y, yref);
+    }
   }
   report("CG p pass p = r + om p_old (3 vectors)", 24.0 * n, [&] {
     hipLaunchKernelGGL(pupdate_kernel, dim3(4096), dim3(256), 0, 0, d_x, d_x, d_om, d_y, n);
