@@ -115,23 +115,38 @@ __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__r
   double acc[W];
 #pragma unroll
   for (int v = 0; v < W; ++v) acc[v] = 0.0;
-  for (int64_t gi = v0 + tid; gi < v1; gi += kBlock) {
-    const int64_t e = gi * W;
-    V wv[W], vj[W], qv[W];
-    VIO<V>::load(w, e, N, wv);
-    VIO<V>::load(Vj, e, N, vj);
-    if (q) VIO<V>::load(q, e, N, qv);
+  // U chunks per thread per round, every load issued before any store
+  constexpr int U = 4;
+  for (int64_t gb = v0 + tid; gb < v1; gb += U * kBlock) {
+    V wv[U][W], vj[U][W], qv[U][W];
 #pragma unroll
-    for (int v = 0; v < W; ++v) {
-      const V t = (V)alpha[(e + v) & (k - 1)] * vj[v];
-      wv[v] = wv[v] - t;  // Av -= alpha * P[j]
-      if (e + v < N) {
-        const double a = q ? (double)qv[v] : (double)wv[v];
-        const double b = (double)wv[v];
-        acc[v] += wt ? dterm_w(a, wt[(e + v) / k], b) : dterm(a, b);
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock;
+      if (gi < v1) {
+        const int64_t e = gi * W;
+        VIO<V>::load(w, e, N, wv[u]);
+        VIO<V>::load(Vj, e, N, vj[u]);
+        if (q) VIO<V>::load(q, e, N, qv[u]);
       }
     }
-    VIO<V>::store(w, e, N, wv);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock;
+      if (gi < v1) {
+        const int64_t e = gi * W;
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+          const V t = (V)alpha[(e + v) & (k - 1)] * vj[u][v];
+          wv[u][v] = wv[u][v] - t;  // Av -= alpha * P[j]
+          if (e + v < N) {
+            const double a = q ? (double)qv[u][v] : (double)wv[u][v];
+            const double b = (double)wv[u][v];
+            acc[v] += wt ? dterm_w(a, wt[(e + v) / k], b) : dterm(a, b);
+          }
+        }
+        VIO<V>::store(w, e, N, wv[u]);
+      }
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -410,7 +425,15 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     double *pbuf[2] = {s->part, s->part2};
     int flip = 0;
     const int64_t ngrp = (N + Vec16<V>::W - 1) / Vec16<V>::W;
-    const int Gm = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ngrp + 1023) / 1024));
+    static const int mgs_cap = [] {
+      const char *e = getenv("KRY_MGS_GRID");  // tuning override
+      return e ? std::max(1, std::min(atoi(e), kMaxGrid)) : 1024;
+    }();
+    static const int mgs_per = [] {
+      const char *e = getenv("KRY_MGS_PER");  // tuning override: chunks per block
+      return e ? std::max(64, atoi(e)) : 1024;
+    }();
+    const int Gm = (int)std::max<int64_t>(1, std::min<int64_t>(mgs_cap, (ngrp + mgs_per - 1) / mgs_per));
     for (int sw = 0; sw < s->sweeps; ++sw) {
       for (int j = 0; j <= col; ++j) {
         const V *Vj = basis<V>(s->V, s->vstride, j);
