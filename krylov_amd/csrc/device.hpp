@@ -469,6 +469,84 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
   }
 }
 
+// ---------------------------------------------- lane-group SELL SpMV (4 <= k <= 64)
+// For a block of k right-hand sides stored row-major (row i's k values are
+// contiguous), k lanes share a row and lane c owns column c: a wave covers
+// 64 / k rows of a slice per pass, and each gather instruction reads whole
+// contiguous rows of x (k * 8 bytes each) instead of one column-strided value
+// per lane. Same slot order, same per-(row, column) sequential sum, so the
+// result is bitwise the lane-per-row kernel's (and csr_matvecs').
+template <typename V, typename MV, typename I, int UNR, bool D16, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
+    const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
+    const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
+    int64_t nslices, int64_t n, int k, const I *__restrict__ indptr, const I *__restrict__ indices,
+    const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rows_per_pass = 64 / k;
+  const int rl0 = lane / k, c = lane & (k - 1);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const auto bs = src.template bind<1>(c);
+  double dacc = 0.0;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    for (int rl = rl0; rl < 64; rl += rows_per_pass) {
+      const int64_t row = s * 64 + rl;
+      V acc = V(0);
+      if (w >= 0) {
+        const I *ci = sidx + base + rl;
+        const uint16_t *cd = sdelta + base + rl;
+        const int *cb = scbase + (base >> 6);
+        const MV *cv = sval + base + rl;
+        for (int j0 = 0; j0 < w; j0 += UNR) {
+          I col[UNR];
+          V a[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const bool in = j0 + u < w;
+            if constexpr (D16) {
+              const unsigned d = in ? (unsigned)__builtin_nontemporal_load(cd + (int64_t)(j0 + u) * 64) : 0xFFFFu;
+              const int b = in ? cb[j0 + u] : 0;
+              col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
+            } else {
+              col[u] = in ? __builtin_nontemporal_load(ci + (int64_t)(j0 + u) * 64) : I(-1);
+            }
+            a[u] = in ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
+          }
+          V xv[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) xv[u] = col[u] >= 0 ? bs(col[u], 0) : V(0);
+#pragma unroll
+          for (int u = 0; u < UNR; ++u)
+            if (col[u] >= 0) {
+              const V p = a[u] * xv[u];
+              acc = acc + p;
+            }
+        }
+      } else if (row < n) {
+        for (I e = indptr[row]; e < indptr[row + 1]; ++e) {
+          const V p = (V)data[e] * bs(indices[e], 0);
+          acc = acc + p;
+        }
+      }
+      if (row < n) dacc += epi(row, c, acc, bs(row, 0));
+    }
+  }
+  if (part != nullptr) {
+    red[tid] = dacc;  // slot tid holds column tid % k
+    block_tree_reduce(red, kBlock, k);
+    if (tid < k) part[(int64_t)g * k + tid] = red[tid];
+  }
+}
+
 // ------------------------------------------- column-blocked SpMV (k = 1)
 // Pass b of cb_nb: each block takes 256-row groups; the group's entries with
 // columns in block b (stored in row order) are multiplied against the
@@ -591,6 +669,23 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
       if (grid_out) *grid_out = grid;
       return;
     }
+  }
+  if (k >= 4 && k <= 64) {
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->nslices + 3) / 4));
+    const bool d16 = sizeof(I) == 4 && A->compact;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->sptr),
+                         static_cast<const int *>(A->swidth), static_cast<const I *>(A->sidx),
+                         static_cast<const uint16_t *>(A->sdelta), static_cast<const int *>(A->scbase),
+                         static_cast<const MV *>(A->sval), A->nslices, A->n, k, static_cast<const I *>(A->indptr),
+                         static_cast<const I *>(A->indices), static_cast<const MV *>(A->data), src, epi, part, ctrl,
+                         step);
+    };
+    if (d16) go(spmv_sell_lg_kernel<V, MV, I, 8, true, Src, Epi>);
+    else go(spmv_sell_lg_kernel<V, MV, I, 8, false, Src, Epi>);
+    KRY_HIP(hipGetLastError());
+    if (grid_out) *grid_out = grid;
+    return;
   }
   switch (k) {
     case 1: grid = launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st); break;
