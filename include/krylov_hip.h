@@ -110,23 +110,30 @@ int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y);
 int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void *g,
               void *c, void *s, void *r);
 
-/* ---- CG (cg.py:16-259, M = Ml = I) --------------------------------------
- * start: r0 = b - A x0, rho0 = <r0, r0>_w; rho0 (k values) returned.
+/* ---- CG (cg.py:16-259) ----------------------------------------------------
+ * set_preconditioners: M and Ml as device operators (NULL = identity), before
+ *        start; the loop then applies Ml (A p) (Product(Ml, A), cg.py:110) and
+ *        z = M Ml_r with rho = <Ml_r, z> (cg.py:205-209).
+ * start: r0 = Ml (b - A x0), rho0 = <r0, M r0>_w; rho0 (k values) returned.
  * run:   executes up to max_steps iterations of cg.py:175-217 on device; stops
  *        early after the first iteration whose residual norms all satisfy
  *        resnorm <= criterion (the test at cg.py:156). Writes the new residual
  *        norms (steps_done x k) to resnorms.
- * residual: explicit ||b - A xk||_w with xk = x0 + yk (cg.py:158-160).
+ * residual: explicit ||M Ml (b - A xk)||_{M^-1} with xk = x0 + yk (cg.py:158-160).
  * get:   download xk (which = 0) or the updated residual r (which = 1). */
 int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out);
 int kry_cg_destroy(kry_cg *s);
+int kry_cg_set_preconditioners(kry_cg *s, kry_csr *M, kry_csr *Ml);
 int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0);
 int kry_cg_set_criterion(kry_cg *s, const double *criterion);
 int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnorms);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
 
-/* ---- GMRES (gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200, M = I) -------
+/* ---- GMRES (gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200) --------------
+ * set_preconditioners: M, Ml, Mr as device operators (NULL = identity); the
+ *         Arnoldi operator is Ml A Mr, M gives the second basis P (V = M P),
+ *         and xk = x0 + Mr (sum_i yy_i V_i) (gmres.py:97-99, 139).
  * create: workspace for up to `maxiter` Arnoldi steps with `sweeps` MGS
  *         passes per step ("mgs" = 1, "mgsK" = K).
  * start:  r0 = b - A x0, ||r0||, V0 = r0 / ||r0|| (guarded), y[0] = ||r0||.
@@ -139,6 +146,7 @@ int kry_cg_get(kry_cg *s, int which, void *host);
 int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t maxiter,
                      int32_t sweeps, kry_gmres **out);
 int kry_gmres_destroy(kry_gmres *s);
+int kry_gmres_set_preconditioners(kry_gmres *s, kry_csr *M, kry_csr *Ml, kry_csr *Mr);
 int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm);
 int kry_gmres_set_criterion(kry_gmres *s, const double *criterion);
 int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done,
@@ -147,11 +155,14 @@ int kry_gmres_solution(kry_gmres *s);
 int kry_gmres_residual(kry_gmres *s, double *resnorm);
 int kry_gmres_get(kry_gmres *s, int which, void *host);
 
-/* ---- MINRES (minres.py:28-253, ArnoldiLanczos arnoldi.py:203-281, M = I) --
+/* ---- MINRES (minres.py:28-253, ArnoldiLanczos arnoldi.py:203-281) --------
+ * set_preconditioners: M, Ml, Mr as device operators (NULL = identity);
+ * Lanczos on Ml A Mr with p / v = M p, xk = x0 + Mr yk (minres.py:95-98).
  * Same run protocol as CG; R, rotations, y, z and W are float64 as in the
  * reference under NumPy-2 promotion (minres.py:195,219). */
 int kry_minres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_minres **out);
 int kry_minres_destroy(kry_minres *s);
+int kry_minres_set_preconditioners(kry_minres *s, kry_csr *M, kry_csr *Ml, kry_csr *Mr);
 int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r0norm);
 int kry_minres_set_criterion(kry_minres *s, const double *criterion);
 int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done,

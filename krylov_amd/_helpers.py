@@ -90,9 +90,10 @@ class Problem:
         if len(A.shape) != 2 or A.shape[0] != A.shape[1] or A.shape[1] != b.shape[0]:
             raise AssertionError("A must be square with A.shape[1] == b.shape[0]")
         for name, op in (("M", M), ("Ml", Ml), ("Mr", Mr)):
-            if not _is_identity(op):
+            if not _is_identity(op) and len(getattr(op, "shape", ())) != 2:
                 raise NotImplementedError(
-                    f"preconditioner {name} is not on the MI355X path yet (SURVEY §8(f) rank 1)"
+                    f"preconditioner {name} must be None, Identity, a krylov_amd.CsrOperator, a scipy.sparse "
+                    f"matrix or a dense array on the MI355X path (got {type(op).__name__})"
                 )
         if np.iscomplexobj(b) or (x0 is not None and np.iscomplexobj(x0)):
             raise TypeError("complex right-hand sides are outside the MI355X path")
@@ -109,6 +110,16 @@ class Problem:
             )
         self.A = as_device_operator(A, device=device)
         self.ctx = self.A.ctx
+        # preconditioners as device operators (None = identity)
+        self.ops = {}
+        for name, op in (("M", M), ("Ml", Ml), ("Mr", Mr)):
+            if _is_identity(op):
+                self.ops[name] = None
+                continue
+            dop = as_device_operator(op, device=self.ctx.device)
+            if dop.shape != self.A.shape:
+                raise ValueError(f"preconditioner {name} has shape {dop.shape}, the operator {self.A.shape}")
+            self.ops[name] = dop
         self.b = b
         self.n = b.shape[0]
         self.tail = b.shape[1:]
@@ -119,6 +130,7 @@ class Problem:
         x0a = None if x0 is None else np.asarray(x0)
         # dtype of the reference's residual b - A x0 and of the device vectors
         rtypes = [self.A.dtype, b.dtype] + ([x0a.dtype] if x0a is not None else [])
+        rtypes += [op.dtype for op in self.ops.values() if op is not None]
         r0 = np.result_type(*rtypes)
         if r0 not in (np.float32, np.float64):
             r0 = np.dtype(np.float64)
@@ -159,6 +171,19 @@ class Problem:
         if len(self.tail) == 0:
             return v[0]
         return v.reshape(self.tail)
+
+    def op_handles(self, *names):
+        """ctypes handles of the named preconditioners (None = identity)."""
+        return [None if self.ops[nm] is None else self.ops[nm].handle for nm in names]
+
+    def has_precond(self):
+        return any(op is not None for op in self.ops.values())
+
+    def apply_host(self, name, x):
+        """op @ x for a preconditioner (identity: x itself, as the reference's
+        Identity returns the same object)."""
+        op = self.ops[name]
+        return x if op is None else op @ x
 
     def zeros_like_b(self):
         return np.zeros_like(self.b)

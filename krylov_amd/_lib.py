@@ -70,6 +70,9 @@ _SIGNATURES = {
     "kry_cg_run": [_vp, _i32, _ip32, _dp],
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
+    "kry_cg_set_preconditioners": [_vp, _vp, _vp],
+    "kry_gmres_set_preconditioners": [_vp, _vp, _vp, _vp],
+    "kry_minres_set_preconditioners": [_vp, _vp, _vp, _vp],
     "kry_gmres_create": [_vp, _vp, _i32, _int, _i32, _i32, _pvp],
     "kry_gmres_destroy": [_vp],
     "kry_gmres_start": [_vp, _vp, _vp, _vp, _dp],

@@ -25,6 +25,10 @@ class _CGState:
         check(lib.kry_cg_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype), ctypes.byref(h)))
         self.h = h
         self._fin = weakref.finalize(self, lib.kry_cg_destroy, h)
+        if prob.ops["Mr"] is not None:
+            raise TypeError("cg has no right preconditioner Mr")
+        if prob.has_precond():
+            check(lib.kry_cg_set_preconditioners(h, *prob.op_handles("M", "Ml")))
 
     def start(self):
         p = self.prob
@@ -66,7 +70,8 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
 
     ``A``: ``krylov_amd.CsrOperator``, scipy.sparse matrix or dense ndarray
     (uploaded once as CSR). ``inner``: ``None`` or ``WeightedInner``.
-    ``M``/``Ml``: ``None`` or ``Identity`` on the device path.
+    ``M``/``Ml``: ``None``/``Identity`` or an operator of the same kinds as
+    ``A`` (applied on the device as SpMVs, cg.py:70-90, 180, 207).
     """
     if return_arnoldi:
         raise NotImplementedError("return_arnoldi is not on the MI355X path yet")

@@ -1,4 +1,8 @@
-// CG device loop (reference cg.py:16-259 with M = Ml = I).
+// CG device loop (reference cg.py:16-259). Preconditioners M and Ml are
+// device CSR operators (kry_cg_set_preconditioners); without them the loop is
+// the five launches below. With Ml, step 1 is A p then Ml (A p); with M, the
+// update's <r, r> partials are replaced by z = M r with <r, z> (cg.py:207-209)
+// and the p pass reads z.
 //
 // One iteration = five launches on the context stream, no host sync:
 //   1. SpMV   Ap = A p, partial <p, Ap>                 cg.py:180-183
@@ -24,6 +28,9 @@ struct kry_cg {
   bool scalar_f32 = false;
   void *b = nullptr, *x0 = nullptr, *y = nullptr, *r = nullptr, *p = nullptr;
   void *Ap = nullptr, *xk = nullptr, *rt = nullptr;
+  kry_csr *M = nullptr, *Ml = nullptr;  // preconditioners (null = identity)
+  void *z = nullptr;                    // M Ml_r (with M)
+  void *t = nullptr;                    // A p / scratch (with Ml)
   double *w = nullptr;
   double *part = nullptr;  // 2 * kMaxGrid * k
   double *scal = nullptr;  // scalar slots, see S_* below
@@ -167,25 +174,47 @@ __global__ void cg_global_check(const double *gbuf, const double *gcrit, int tot
   if (all_le(gbuf, gcrit, total_k, &flag) && threadIdx.x == 0) ctrl->stop_at = step + 1;
 }
 
+// Ml r and M Ml r with <Ml r, M Ml r> partials for r = b - A src
+// (cg.py:70-90); returns the partial count. Leaves Ml r in `mlr` and M Ml r in
+// `z` (when M is set).
+template <typename V, typename MV, typename I>
+int cg_residual_chain(kry_cg *s, const V *src, V *raw, V *mlr) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  int P = 0;
+  const V *bb = static_cast<const V *>(s->b);
+  if (!s->Ml && !s->M) {
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, EpiResidual<V>{bb, mlr, s->w, k}, s->part, &P, nullptr, 0,
+                          st);
+    return P;
+  }
+  if (s->Ml) {
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, EpiResidual<V>{bb, raw, s->w, k}, s->part, &P, nullptr, 0,
+                          st);
+    launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{raw, k}, EpiStoreNorm<V>{mlr, s->w, k}, s->part, &P, nullptr, 0, st);
+  } else {
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, EpiResidual<V>{bb, mlr, s->w, k}, s->part, &P, nullptr, 0,
+                          st);
+  }
+  if (s->M)
+    launch_spmv_any<V>(s->M, k, SrcPlain<V>{mlr, k}, EpiStoreDot<V>{static_cast<V *>(s->z), mlr, s->w, k}, s->part,
+                       &P, nullptr, 0, st);
+  return P;
+}
+
 template <typename V, typename MV, typename I>
 void cg_start_impl(kry_cg *s) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
-  const V *x0 = static_cast<const V *>(s->x0);
-  const int64_t N = s->n * (int64_t)k;
   // r0 = b - A x0 (x0 = 0: r0 = b - A 0 evaluated the same way)
-  const V *src = x0;
+  const V *src = static_cast<const V *>(s->x0);
   if (!src) src = static_cast<const V *>(s->xk);  // zero-filled scratch
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->r), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  const int P = cg_residual_chain<V, MV, I>(s, src, static_cast<V *>(s->t), static_cast<V *>(s->r));
   if (s->scalar_f32)
     hipLaunchKernelGGL(cg_start_finalize<float>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
   else
     hipLaunchKernelGGL(cg_start_finalize<double>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
   KRY_HIP(hipGetLastError());
-  (void)N;
 }
 
 template <typename V, typename MV, typename I>
@@ -199,8 +228,15 @@ void cg_run_impl(kry_cg *s, int max_steps) {
     int PA, PB;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
-      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{p, k}, EpiApDot<V>{static_cast<V *>(s->Ap), s->w, k}, partA, &PA,
-                            s->ctrl, step, st);
+      if (s->Ml) {  // Ap = Ml (A p) (Product(Ml, A), cg.py:110,180)
+        V *t = static_cast<V *>(s->t);
+        launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{p, k}, EpiStore<V>{t, k}, nullptr, nullptr, s->ctrl, step, st);
+        launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{t, k}, EpiStoreDot<V>{static_cast<V *>(s->Ap), p, s->w, k}, partA,
+                           &PA, s->ctrl, step, st);
+      } else {
+        launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{p, k}, EpiApDot<V>{static_cast<V *>(s->Ap), s->w, k}, partA, &PA,
+                              s->ctrl, step, st);
+      }
     }
     if (s->scalar_f32)
       hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
@@ -211,7 +247,12 @@ void cg_run_impl(kry_cg *s, int max_steps) {
       PB = launch_elementwise<V>(N, k,
                                  OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), p,
                                                static_cast<const V *>(s->Ap), s->scal + S_ALPHA * k, s->w, k},
-                                 partB, s->ctrl, step, st);
+                                 s->M ? nullptr : partB, s->ctrl, step, st);
+    }
+    if (s->M) {  // M_Ml_rk = M Ml_rk and <Ml_rk, M_Ml_rk> (cg.py:207-209)
+      V *r = static_cast<V *>(s->r);
+      launch_spmv_any<V>(s->M, k, SrcPlain<V>{r, k}, EpiStoreDot<V>{static_cast<V *>(s->z), r, s->w, k}, partB, &PB,
+                         s->ctrl, step, st);
     }
     double *gb = s->comm ? s->gbuf : nullptr;
     if (s->scalar_f32)
@@ -223,8 +264,8 @@ void cg_run_impl(kry_cg *s, int max_steps) {
     KRY_HIP(hipGetLastError());
     {
       ProfScope ps(s->ctx, PROF_OTHER);
-      launch_elementwise<V>(N, k, OpCgP<V>{p, static_cast<const V *>(s->r), s->scal + S_OMEGA * k, k}, nullptr,
-                            s->ctrl, step, st);
+      const V *zv = static_cast<const V *>(s->M ? s->z : s->r);
+      launch_elementwise<V>(N, k, OpCgP<V>{p, zv, s->scal + S_OMEGA * k, k}, nullptr, s->ctrl, step, st);
     }
     if (s->comm) {
       // exactly one collective per iteration: the residual-norm vector
@@ -244,10 +285,9 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
   const int64_t N = s->n * (int64_t)k;
   launch_elementwise<V>(N, k, OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->y), static_cast<V *>(s->xk)},
                         nullptr, nullptr, 0, st);
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  // explicit ||M Ml (b - A xk)||: t and z are free between iterations
+  V *mlr = static_cast<V *>(s->Ml ? s->t : s->rt);
+  const int P = cg_residual_chain<V, MV, I>(s, static_cast<const V *>(s->xk), static_cast<V *>(s->rt), mlr);
   double *out = s->scal + S_TMP * k;
   hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
   KRY_HIP(hipGetLastError());
@@ -271,7 +311,7 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
   }
 
 static void cg_free(kry_cg *s) {
-  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p, s->Ap, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
+  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p, s->Ap, s->z, s->t, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
                   s->ctrl, s->gbuf, s->gcrit};
   for (void *b : bufs) dev_free(b);
 }
@@ -354,7 +394,8 @@ int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
   KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
   s->it = 0;
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
-  KRY_HIP(hipMemcpyAsync(s->p, s->r, vb, hipMemcpyDeviceToDevice, st));  // p0 = r0 (cg.py:138)
+  // p0 = M_Ml_r0 (cg.py:138)
+  KRY_HIP(hipMemcpyAsync(s->p, s->M ? s->z : s->r, vb, hipMemcpyDeviceToDevice, st));
   KRY_HIP(hipMemcpyAsync(rho0, s->scal + S_TMP * s->k, s->k * 8, hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
   s->started = true;
@@ -430,6 +471,32 @@ int kry_cg_get(kry_cg *s, int which, void *host) {
     KRY_HIP(hipMemcpyAsync(host, s->r, vb, hipMemcpyDeviceToHost, st));
   }
   KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+int kry_cg_set_preconditioners(kry_cg *s, kry_csr *M, kry_csr *Ml) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s, KRY_EINVAL, "null solver");
+  for (kry_csr *op : {M, Ml}) {
+    if (!op) continue;
+    KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
+    KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
+                "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+  }
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype);
+  s->M = M;
+  s->Ml = Ml;
+  if (M && !s->z) {
+    s->z = dev_alloc(vb);
+    KRY_HIP(hipMemsetAsync(s->z, 0, vb, s->ctx->stream));
+  }
+  if (Ml && !s->t) {
+    s->t = dev_alloc(vb);
+    KRY_HIP(hipMemsetAsync(s->t, 0, vb, s->ctx->stream));
+  }
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  s->started = false;
   KRY_API_END
 }
 

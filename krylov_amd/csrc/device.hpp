@@ -1,6 +1,8 @@
-// gfx950 kernel templates: CSR SpMV (LDS-staged streaming form for one RHS,
-// register form for row-major RHS blocks), fused elementwise passes with
-// deterministic per-column dot partials, partial reducers, LAPACK lartg.
+// gfx950 kernel templates: SpMV over the SELL-64 image (lane per row for one
+// or two RHS, lane groups for 4..64 row-major RHS, int32 or compact uint16
+// column deltas) and over the column-blocked image (scattered sparsity, one
+// RHS), fused elementwise passes with deterministic per-column dot partials,
+// partial reducers, LAPACK lartg.
 //
 // Numerics contract (compiled with -ffp-contract=off):
 //  * SpMV sums every row sequentially in stored nonzero order starting from 0,
@@ -11,6 +13,8 @@
 //    then a fixed LDS tree per block, then a fixed tree over block partials):
 //    reproducible run to run, though not in OpenBLAS's summation order.
 #pragma once
+
+#include <type_traits>
 
 #include "common.hpp"
 #include "objects.hpp"
@@ -110,6 +114,31 @@ struct EpiStoreDot {
     y[i * k + c] = s;
     const double qv = (double)q[i * k + c];
     return w ? dterm_w(qv, w[i], (double)s) : dterm(qv, (double)s);
+  }
+};
+
+// y = A x and <y, y> (weighted): a preconditioned residual M_l r and its norm.
+template <typename V>
+struct EpiStoreNorm {
+  V *y;
+  const double *w;
+  int k;
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
+    y[i * k + c] = s;
+    const double sv = (double)s;
+    return w ? dterm_w(sv, w[i], sv) : dterm(sv, sv);
+  }
+};
+
+// out = x0 + A y (gmres.py:97-99 / minres.py: x0 + Mr @ yk).
+template <typename V>
+struct EpiAddStore {
+  V *out;
+  const V *x0;  // may be null (x0 = 0)
+  int k;
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
+    out[i * k + c] = x0 ? x0[i * k + c] + s : s;
+    return 0.0;
   }
 };
 
@@ -695,6 +724,22 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   }
   KRY_HIP(hipGetLastError());
   if (grid_out) *grid_out = grid;
+}
+
+// SpMV with an operator of any stored type (preconditioners M, Ml, Mr): the
+// matrix value type may be float under double vectors (exact upcast).
+template <typename V, class Src, class Epi>
+void launch_spmv_any(const kry_csr *Op, int k, Src src, Epi epi, double *part, int *grid_out, const Ctrl *ctrl,
+                     int step, hipStream_t st) {
+  const bool f64 = Op->dtype == KRY_F64, i32 = Op->itype == KRY_I32;
+  if constexpr (std::is_same<V, double>::value) {
+    if (f64 && i32) return launch_spmv<V, double, int32_t>(Op, k, src, epi, part, grid_out, ctrl, step, st);
+    if (f64) return launch_spmv<V, double, int64_t>(Op, k, src, epi, part, grid_out, ctrl, step, st);
+  } else {
+    KRY_REQUIRE(!f64, KRY_EINVAL, "a float64 operator cannot act on float32 vectors");
+  }
+  if (i32) return launch_spmv<V, float, int32_t>(Op, k, src, epi, part, grid_out, ctrl, step, st);
+  return launch_spmv<V, float, int64_t>(Op, k, src, epi, part, grid_out, ctrl, step, st);
 }
 
 template <typename V, class Op>

@@ -1,5 +1,8 @@
-// GMRES device loop (reference gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200,
-// M = Ml = Mr = I, which makes the P and V bases identical).
+// GMRES device loop (reference gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200).
+// Preconditioners are device CSR operators (kry_gmres_set_preconditioners):
+// the Arnoldi operator is Ml A Mr (Product, gmres.py:139), M splits the basis
+// into P (MGS subtraction) and V = M P (MGS inner products, solution), and
+// h[k+1] = sqrt(<w, M w>) (arnoldi.py:185); without M the bases coincide.
 //
 // One Arnoldi step k (sweeps = 1 for "mgs", K for "mgsK"):
 //   SpMV      w = A V_k, partial <V_0, w>                      arnoldi.py:176
@@ -26,6 +29,11 @@ struct kry_gmres {
   int sweeps = 1;
   size_t vstride = 0;  // elements per basis vector (padded)
   void *b = nullptr, *x0 = nullptr, *V = nullptr, *wv = nullptr, *xk = nullptr, *rt = nullptr;
+  kry_csr *M = nullptr, *Ml = nullptr, *Mr = nullptr;  // preconditioners (null = identity)
+  void *P = nullptr;    // (maxiter + 1) basis vectors P_j (with M; else P = V)
+  void *mw = nullptr;   // M w (with M)
+  void *t1 = nullptr;   // Mr v / solution scratch (with Mr)
+  void *t2 = nullptr;   // A Mr v / raw residual (with Ml)
   double *w = nullptr;
   double *part = nullptr, *part1 = nullptr, *part2 = nullptr;  // partial rows (MGS ping-pong)
   double *scal = nullptr;  // alpha[k], hsafe[k], crit[k], tmp[k]
@@ -51,34 +59,6 @@ template <typename V>
 __host__ __device__ __forceinline__ V *basis(void *Vb, size_t stride, int i) {
   return static_cast<V *>(Vb) + stride * (size_t)i;
 }
-
-template <typename V>
-struct OpMgs {
-  V *w;
-  const V *Vj;
-  const V *q;  // next inner-product partner, or null for <w, w>
-  const double *alpha;
-  const double *wt;
-  int k;
-  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
-    constexpr int W = Vec16<V>::W;
-    V wv[W], vj[W], qv[W];
-    VIO<V>::load(w, e, N, wv);
-    VIO<V>::load(Vj, e, N, vj);
-    if (q) VIO<V>::load(q, e, N, qv);
-#pragma unroll
-    for (int v = 0; v < W; ++v) {
-      const V t = (V)alpha[(e + v) & (k - 1)] * vj[v];
-      wv[v] = wv[v] - t;  // Av -= alpha * P[j]   (arnoldi.py:162)
-      if (e + v < N) {
-        const double a = q ? (double)qv[v] : (double)wv[v];
-        const double b = (double)wv[v];
-        acc[v] += wt ? dterm_w(a, wt[(e + v) / k], b) : dterm(a, b);
-      }
-    }
-    VIO<V>::store(w, e, N, wv);
-  }
-};
 
 // One MGS pass j (arnoldi.py:159-162) in a single launch: every block first
 // reduces the previous pass's partials into alpha_j = <V_j, w> (fixed order,
@@ -384,21 +364,61 @@ __global__ void gm_trsv_big_kernel(const double *R, const double *y, double *yy,
   }
 }
 
+// w = Ml (A (Mr v)) (Product(Ml, A, Mr), gmres.py:139), `epi` on the last product.
+template <typename V, typename MV, typename I, class Epi>
+void gm_apply_op(kry_gmres *s, const V *v, Epi epi, double *part, int *P, const Ctrl *ctrl, int step) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const V *src = v;
+  if (s->Mr) {
+    V *t1 = static_cast<V *>(s->t1);
+    launch_spmv_any<V>(s->Mr, k, SrcPlain<V>{v, k}, EpiStore<V>{t1, k}, nullptr, nullptr, ctrl, step, st);
+    src = t1;
+  }
+  if (s->Ml) {
+    V *t2 = static_cast<V *>(s->t2);
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, EpiStore<V>{t2, k}, nullptr, nullptr, ctrl, step, st);
+    launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{t2, k}, epi, part, P, ctrl, step, st);
+  } else {
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, epi, part, P, ctrl, step, st);
+  }
+}
+
+// Ml (b - A z) -> mlr, M Ml (b - A z) -> mw (with M), and the partials of
+// <Ml r, M Ml r> (gmres.py:111-118); returns the partial count.
+template <typename V, typename MV, typename I>
+int gm_residual_chain(kry_gmres *s, const V *z, V *mlr) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  int P = 0;
+  V *raw = s->Ml ? static_cast<V *>(s->t2) : mlr;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{z, k}, EpiResidual<V>{static_cast<const V *>(s->b), raw, s->w, k},
+                        s->part, &P, nullptr, 0, st);
+  if (s->Ml)
+    launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{raw, k}, EpiStoreNorm<V>{mlr, s->w, k}, s->part, &P, nullptr, 0, st);
+  if (s->M)
+    launch_spmv_any<V>(s->M, k, SrcPlain<V>{mlr, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), mlr, s->w, k},
+                       s->part, &P, nullptr, 0, st);
+  return P;
+}
+
 template <typename V, typename MV, typename I>
 void gm_start_impl(kry_gmres *s) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   const V *src = s->x0 ? static_cast<const V *>(s->x0) : static_cast<const V *>(s->xk);  // xk zero-filled
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->wv), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  V *wv = static_cast<V *>(s->wv);
+  const int P = gm_residual_chain<V, MV, I>(s, src, wv);
   hipLaunchKernelGGL(gm_start_finalize<V>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal, s->y);
   KRY_HIP(hipGetLastError());
-  launch_elementwise<V>(N, k,
-                        OpScaleDiv<V>{static_cast<const V *>(s->wv), static_cast<V *>(s->V), s->scal + G_HSAFE * k, k},
-                        nullptr, nullptr, 0, st);
+  // P_0 = Ml r0 / norm, V_0 = M Ml r0 / norm (arnoldi.py:147-150)
+  if (s->M)
+    launch_elementwise<V>(N, k, OpScaleDiv<V>{wv, static_cast<V *>(s->P), s->scal + G_HSAFE * k, k}, nullptr, nullptr,
+                          0, st);
+  const V *v0src = s->M ? static_cast<const V *>(s->mw) : wv;
+  launch_elementwise<V>(N, k, OpScaleDiv<V>{v0src, static_cast<V *>(s->V), s->scal + G_HSAFE * k, k}, nullptr,
+                        nullptr, 0, st);
 }
 
 template <typename V, typename MV, typename I>
@@ -415,7 +435,7 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     int P;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
-      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{Vk, k}, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step, st);
+      gm_apply_op<V, MV, I>(s, Vk, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step);
     }
     // the SpMV's partials of <V_0, w> -> one value per column, so every MGS
     // block reduces a single partial row for its first coefficient
@@ -436,11 +456,11 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     const int Gm = (int)std::max<int64_t>(1, std::min<int64_t>(mgs_cap, (ngrp + mgs_per - 1) / mgs_per));
     for (int sw = 0; sw < s->sweeps; ++sw) {
       for (int j = 0; j <= col; ++j) {
-        const V *Vj = basis<V>(s->V, s->vstride, j);
+        const V *Pj = basis<V>(s->M ? s->P : s->V, s->vstride, j);  // Av -= alpha P_j (arnoldi.py:162)
         const V *q = j < col ? basis<V>(s->V, s->vstride, j + 1) : (sw + 1 < s->sweeps ? V0 : nullptr);
         double *pout = pbuf[flip];
         ProfScope ps(s->ctx, PROF_MGS);
-        hipLaunchKernelGGL(gm_mgs_kernel<V>, dim3(Gm), dim3(kBlock), 0, st, N, k, w, Vj, q, pin, Pin, pout, s->h, j,
+        hipLaunchKernelGGL(gm_mgs_kernel<V>, dim3(Gm), dim3(kBlock), 0, st, N, k, w, Pj, q, pin, Pin, pout, s->h, j,
                            sw == 0 ? 1 : 0, s->w, s->ctrl, step);
         pin = pout;
         Pin = Gm;
@@ -448,13 +468,23 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
       }
     }
     P = Pin;
+    if (s->M) {  // MAv = M Av, h[k+1] = sqrt(<Av, MAv>) (arnoldi.py:184-185)
+      launch_spmv_any<V>(s->M, k, SrcPlain<V>{w, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), w, s->w, k}, s->part,
+                         &P, s->ctrl, step, st);
+      pin = s->part;
+    }
     hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, pin, P, k, s->scal, s->h, s->R, s->y,
                        s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
     KRY_HIP(hipGetLastError());
-    // V_{col+1} = w / guard(h[col+1]) unless invariant; the kernel runs for
-    // this step even when the QR kernel just raised stop_at to step + 1.
+    // P_{col+1} = w / guard(h[col+1]), V_{col+1} = M w / guard(h[col+1]) unless
+    // invariant; these run for this step even when the QR kernel just raised
+    // stop_at to step + 1 (arnoldi.py:191-196).
+    if (s->M)
+      launch_elementwise<V>(N, k, OpScaleDiv<V>{w, basis<V>(s->P, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
+                            nullptr, s->ctrl, step, st);
+    const V *vsrc = s->M ? static_cast<const V *>(s->mw) : w;
     launch_elementwise<V>(N, k,
-                          OpScaleDiv<V>{w, basis<V>(s->V, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
+                          OpScaleDiv<V>{vsrc, basis<V>(s->V, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
                           nullptr, s->ctrl, step, st);
   }
 }
@@ -473,20 +503,27 @@ void gm_solution_impl(kry_gmres *s) {
                          s->ctrl);
     KRY_HIP(hipGetLastError());
   }
-  launch_elementwise<V>(N, k,
-                        OpBasisCombo<V>{static_cast<const V *>(s->V), s->vstride, m, s->yy,
-                                        static_cast<const V *>(s->x0), static_cast<V *>(s->xk), k},
+  if (!s->Mr) {
+    launch_elementwise<V>(N, k,
+                          OpBasisCombo<V>{static_cast<const V *>(s->V), s->vstride, m, s->yy,
+                                          static_cast<const V *>(s->x0), static_cast<V *>(s->xk), k},
+                          nullptr, nullptr, 0, st);
+    return;
+  }
+  // xk = x0 + Mr (sum_i yy_i V_i) (gmres.py:97-99)
+  V *t1 = static_cast<V *>(s->t1);
+  launch_elementwise<V>(N, k, OpBasisCombo<V>{static_cast<const V *>(s->V), s->vstride, m, s->yy, nullptr, t1, k},
                         nullptr, nullptr, 0, st);
+  launch_spmv_any<V>(s->Mr, k, SrcPlain<V>{t1, k},
+                     EpiAddStore<V>{static_cast<V *>(s->xk), static_cast<const V *>(s->x0), k}, nullptr, nullptr,
+                     nullptr, 0, st);
 }
 
 template <typename V, typename MV, typename I>
 void gm_residual_impl(kry_gmres *s, double *norm2) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  const int P = gm_residual_chain<V, MV, I>(s, static_cast<const V *>(s->xk), static_cast<V *>(s->rt));
   double *out = s->scal + G_TMP * k;
   hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
   KRY_HIP(hipGetLastError());
@@ -495,8 +532,8 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 }
 
 void gm_free(kry_gmres *s) {
-  void *bufs[] = {s->b, s->x0, s->V, s->wv, s->xk, s->rt, s->w, s->part, s->part1, s->part2, s->scal, s->h, s->R, s->y,
-                  s->Gc, s->Gs, s->yy, s->hist, s->ctrl};
+  void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
+                  s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -564,6 +601,37 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     throw;
   }
   *out = s;
+  KRY_API_END
+}
+
+int kry_gmres_set_preconditioners(kry_gmres *s, kry_csr *M, kry_csr *Ml, kry_csr *Mr) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s, KRY_EINVAL, "null solver");
+  for (kry_csr *op : {M, Ml, Mr}) {
+    if (!op) continue;
+    KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
+    KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
+                "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+  }
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  const size_t vb = s->vstride * dsize(s->dtype);
+  auto need = [&](void *&buf, size_t bytes) {
+    if (!buf) {
+      buf = dev_alloc(bytes);
+      KRY_HIP(hipMemsetAsync(buf, 0, bytes, s->ctx->stream));
+    }
+  };
+  s->M = M;
+  s->Ml = Ml;
+  s->Mr = Mr;
+  if (M) {
+    need(s->P, vb * ((size_t)s->maxiter + 1));
+    need(s->mw, vb);
+  }
+  if (Mr) need(s->t1, vb);
+  if (Ml) need(s->t2, vb);
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  s->started = false;
   KRY_API_END
 }
 

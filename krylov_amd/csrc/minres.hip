@@ -1,5 +1,8 @@
 // MINRES device loop (reference minres.py:28-253 with the Lanczos process of
-// arnoldi.py:203-281, M = Ml = Mr = I).
+// arnoldi.py:203-281). Preconditioners are device CSR operators
+// (kry_minres_set_preconditioners): the Lanczos operator is Ml A Mr, M splits
+// the Lanczos vectors into p and v = M p with h[2] = sqrt(<w, M w>)
+// (arnoldi.py:268-277), and x = x0 + Mr yk (minres.py:95-98).
 //
 // One iteration = five launches, no host sync:
 //   SpMV   w = A v - h0 p_old, partial <v, w>             arnoldi.py:244-252
@@ -28,6 +31,10 @@ struct kry_minres {
   void *b = nullptr, *x0 = nullptr, *yk = nullptr, *wv = nullptr, *xk = nullptr, *rt = nullptr;
   void *P[3] = {nullptr, nullptr, nullptr};  // ring: p_old, p (= v), p_new
   double *W[2] = {nullptr, nullptr};         // float64 W ring
+  kry_csr *M = nullptr, *Ml = nullptr, *Mr = nullptr;  // preconditioners (null = identity)
+  void *Vr[2] = {nullptr, nullptr};  // v = M p ring (with M; else v = p)
+  void *mw = nullptr;                // M w (with M)
+  void *t1 = nullptr, *t2 = nullptr; // Mr v (with Mr), A Mr v / raw residual (with Ml)
   double *w = nullptr;
   double *part = nullptr;
   double *scal = nullptr;
@@ -223,24 +230,83 @@ __global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int
   }
 }
 
+// w = Ml (A (Mr v)) (Product(Ml, A, Mr), minres.py:151), `epi` on the last product.
+template <typename V, typename MV, typename I, class Epi>
+void mr_apply_op(kry_minres *s, const V *v, Epi epi, double *part, int *P, const Ctrl *ctrl, int step) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const V *src = v;
+  if (s->Mr) {
+    V *t1 = static_cast<V *>(s->t1);
+    launch_spmv_any<V>(s->Mr, k, SrcPlain<V>{v, k}, EpiStore<V>{t1, k}, nullptr, nullptr, ctrl, step, st);
+    src = t1;
+  }
+  if (s->Ml) {
+    V *t2 = static_cast<V *>(s->t2);
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, EpiStore<V>{t2, k}, nullptr, nullptr, ctrl, step, st);
+    launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{t2, k}, epi, part, P, ctrl, step, st);
+  } else {
+    launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k}, epi, part, P, ctrl, step, st);
+  }
+}
+
+// Ml (b - A z) -> mlr, M Ml (b - A z) -> mw (with M), partials of
+// <Ml r, M Ml r> (minres.py:105-118, 131-136); returns the partial count.
+template <typename V, typename MV, typename I>
+int mr_residual_chain(kry_minres *s, const V *z, V *mlr) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  int P = 0;
+  V *raw = s->Ml ? static_cast<V *>(s->t2) : mlr;
+  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{z, k}, EpiResidual<V>{static_cast<const V *>(s->b), raw, s->w, k},
+                        s->part, &P, nullptr, 0, st);
+  if (s->Ml)
+    launch_spmv_any<V>(s->Ml, k, SrcPlain<V>{raw, k}, EpiStoreNorm<V>{mlr, s->w, k}, s->part, &P, nullptr, 0, st);
+  if (s->M)
+    launch_spmv_any<V>(s->M, k, SrcPlain<V>{mlr, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), mlr, s->w, k},
+                       s->part, &P, nullptr, 0, st);
+  return P;
+}
+
+// xk = x0 + Mr yk (minres.py:95-98)
+template <typename V>
+void mr_compute_xk(kry_minres *s) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  if (s->Mr)
+    launch_spmv_any<V>(s->Mr, k, SrcPlain<V>{static_cast<const V *>(s->yk), k},
+                       EpiAddStore<V>{static_cast<V *>(s->xk), static_cast<const V *>(s->x0), k}, nullptr, nullptr,
+                       nullptr, 0, st);
+  else
+    launch_elementwise<V>(N, k,
+                          OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->yk),
+                                  static_cast<V *>(s->xk)},
+                          nullptr, nullptr, 0, st);
+}
+
 template <typename V, typename MV, typename I>
 void mr_start_impl(kry_minres *s) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   const V *src = s->x0 ? static_cast<const V *>(s->x0) : static_cast<const V *>(s->xk);
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{src, k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->wv), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  V *wv = static_cast<V *>(s->wv);
+  const int P = mr_residual_chain<V, MV, I>(s, src, wv);
   if (s->inner_f32)
     hipLaunchKernelGGL((mr_start_finalize<V, float>), dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
   else
     hipLaunchKernelGGL((mr_start_finalize<V, double>), dim3(1), dim3(kBlock), 0, st, s->part, P, k, s->scal);
   KRY_HIP(hipGetLastError());
-  // p = v = r0 / guard(||r0||) (arnoldi.py:480-481 analogue, ArnoldiLanczos.__init__)
-  launch_elementwise<V>(N, k, OpDivInto<V>{static_cast<const V *>(s->wv), static_cast<V *>(s->P[0]), s->scal + M_HSAFE * k, k},
-                        nullptr, nullptr, 0, st);
+  // p = Ml r0 / guard(norm), v = M Ml r0 / guard(norm) (ArnoldiLanczos.__init__,
+  // arnoldi.py:220-230)
+  launch_elementwise<V>(N, k, OpDivInto<V>{wv, static_cast<V *>(s->P[0]), s->scal + M_HSAFE * k, k}, nullptr, nullptr,
+                        0, st);
+  if (s->M)
+    launch_elementwise<V>(N, k,
+                          OpDivInto<V>{static_cast<const V *>(s->mw), static_cast<V *>(s->Vr[0]),
+                                       s->scal + M_HSAFE * k, k},
+                          nullptr, nullptr, 0, st);
 }
 
 template <typename V, typename S, typename MV, typename I>
@@ -252,18 +318,21 @@ void mr_run_typed(kry_minres *s, int max_steps) {
   double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
   for (int step = 0; step < max_steps; ++step) {
     const int64_t i = s->it + step;
-    const V *v = static_cast<const V *>(s->P[i % 3]);
+    const V *p = static_cast<const V *>(s->P[i % 3]);
+    const V *v = s->M ? static_cast<const V *>(s->Vr[i % 2]) : p;
     const V *pold = i > 0 ? static_cast<const V *>(s->P[(i + 2) % 3]) : nullptr;
     V *pnew = static_cast<V *>(s->P[(i + 1) % 3]);
     int PA, PB;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
-      launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{v, k}, EpiLanczos<V>{w, v, pold, s->scal + M_H0 * k, s->w, k}, partA,
-                        &PA, s->ctrl, step, st);
+      mr_apply_op<V, MV, I>(s, v, EpiLanczos<V>{w, v, pold, s->scal + M_H0 * k, s->w, k}, partA, &PA, s->ctrl, step);
     }
     hipLaunchKernelGGL((mr_alpha_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
-    PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, v, s->scal + M_ALPHA * k, s->w, k}, partB, s->ctrl,
-                               step, st);
+    PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, p, s->scal + M_ALPHA * k, s->w, k},
+                               s->M ? nullptr : partB, s->ctrl, step, st);
+    if (s->M)  // MAv = M Av, h[2] = sqrt(<Av, MAv>) (arnoldi.py:268-269)
+      launch_spmv_any<V>(s->M, k, SrcPlain<V>{w, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), w, s->w, k}, partB, &PB,
+                         s->ctrl, step, st);
     hipLaunchKernelGGL((mr_qr_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, i >= 1 ? 1 : 0,
                        i >= 2 ? 1 : 0, s->hist, s->ctrl, step);
     KRY_HIP(hipGetLastError());
@@ -275,6 +344,11 @@ void mr_run_typed(kry_minres *s, int max_steps) {
                                               s->scal, k},
                             nullptr, s->ctrl, step, st);
     }
+    if (s->M)  // v = MAv / guard(h[2]) (arnoldi.py:277)
+      launch_elementwise<V>(N, k,
+                            OpDivInto<V>{static_cast<const V *>(s->mw), static_cast<V *>(s->Vr[(i + 1) % 2]),
+                                         s->scal + M_HSAFE * k, k},
+                            nullptr, s->ctrl, step, st);
   }
 }
 
@@ -290,13 +364,8 @@ template <typename V, typename MV, typename I>
 void mr_residual_impl(kry_minres *s, double *norm2) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
-  const int64_t N = s->n * (int64_t)k;
-  launch_elementwise<V>(N, k, OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->yk), static_cast<V *>(s->xk)},
-                        nullptr, nullptr, 0, st);
-  int P;
-  launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{static_cast<const V *>(s->xk), k},
-                    EpiResidual<V>{static_cast<const V *>(s->b), static_cast<V *>(s->rt), s->w, k}, s->part, &P,
-                    nullptr, 0, st);
+  mr_compute_xk<V>(s);
+  const int P = mr_residual_chain<V, MV, I>(s, static_cast<const V *>(s->xk), static_cast<V *>(s->rt));
   double *out = s->scal + M_TMP * k;
   hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, k, out);
   KRY_HIP(hipGetLastError());
@@ -305,8 +374,8 @@ void mr_residual_impl(kry_minres *s, double *norm2) {
 }
 
 void mr_free(kry_minres *s) {
-  void *bufs[] = {s->b, s->x0, s->yk, s->wv, s->xk, s->rt, s->P[0], s->P[1], s->P[2], s->W[0], s->W[1],
-                  s->w, s->part, s->scal, s->hist, s->ctrl};
+  void *bufs[] = {s->b,  s->x0,   s->yk,   s->wv,   s->xk,    s->rt,  s->P[0], s->P[1], s->P[2], s->W[0],
+                  s->W[1], s->w, s->part, s->scal, s->hist, s->ctrl, s->Vr[0], s->Vr[1], s->mw, s->t1, s->t2};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -365,6 +434,38 @@ int kry_minres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_minres
     throw;
   }
   *out = s;
+  KRY_API_END
+}
+
+int kry_minres_set_preconditioners(kry_minres *s, kry_csr *M, kry_csr *Ml, kry_csr *Mr) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s, KRY_EINVAL, "null solver");
+  for (kry_csr *op : {M, Ml, Mr}) {
+    if (!op) continue;
+    KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
+    KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
+                "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+  }
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype);
+  auto need = [&](void *&buf) {
+    if (!buf) {
+      buf = dev_alloc(vb);
+      KRY_HIP(hipMemsetAsync(buf, 0, vb, s->ctx->stream));
+    }
+  };
+  s->M = M;
+  s->Ml = Ml;
+  s->Mr = Mr;
+  if (M) {
+    need(s->Vr[0]);
+    need(s->Vr[1]);
+    need(s->mw);
+  }
+  if (Mr) need(s->t1);
+  if (Ml) need(s->t2);
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  s->started = false;
   KRY_API_END
 }
 
@@ -472,11 +573,9 @@ int kry_minres_get(kry_minres *s, int which, void *host) {
   hipStream_t st = s->ctx->stream;
   const int64_t N = s->n * (int64_t)s->k;
   if (s->dtype == KRY_F64)
-    launch_elementwise<double>(N, s->k, OpXk<double>{static_cast<const double *>(s->x0), static_cast<const double *>(s->yk), static_cast<double *>(s->xk)},
-                               nullptr, nullptr, 0, st);
+    mr_compute_xk<double>(s);
   else
-    launch_elementwise<float>(N, s->k, OpXk<float>{static_cast<const float *>(s->x0), static_cast<const float *>(s->yk), static_cast<float *>(s->xk)},
-                              nullptr, nullptr, 0, st);
+    mr_compute_xk<float>(s);
   KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END

@@ -25,6 +25,8 @@ class _GmresState:
                                    int(maxiter), int(sweeps), ctypes.byref(h)))
         self.h = h
         self._fin = weakref.finalize(self, lib.kry_gmres_destroy, h)
+        if prob.has_precond():
+            check(lib.kry_gmres_set_preconditioners(h, *prob.op_handles("M", "Ml", "Mr")))
 
     def start(self):
         p = self.prob
@@ -75,8 +77,8 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
     rn0 = st.start()
     resnorms = [prob.colvals(rn0)]
     if callback is not None:
-        # the reference passes Ml_r0 = b - A x0 here (gmres.py:143-144)
-        callback(x0_host, prob.b - prob.A @ x0_host)
+        # the reference passes Ml_r0 = Ml (b - A x0) here (gmres.py:143-144)
+        callback(x0_host, prob.apply_host("Ml", prob.b - prob.A @ x0_host))
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))
 

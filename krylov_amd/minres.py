@@ -21,6 +21,8 @@ class _MinresState:
                                     ctypes.byref(h)))
         self.h = h
         self._fin = weakref.finalize(self, lib.kry_minres_destroy, h)
+        if prob.has_precond():
+            check(lib.kry_minres_set_preconditioners(h, *prob.op_handles("M", "Ml", "Mr")))
 
     def start(self):
         p = self.prob

@@ -4,8 +4,10 @@ This module is the checker, never the product: only ``tests/``,
 ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
 it. The MI355X path (``krylov_amd``) never calls into ``oracle/``.
 
-It restates, for real dtypes and M = Ml = Mr = I, the iteration of
-``ju-liu/krylov`` 0.0.3 (``/root/reference/src/krylov``):
+It restates, for real dtypes, the iteration of ``ju-liu/krylov`` 0.0.3
+(``/root/reference/src/krylov``), including the preconditioners M, Ml, Mr
+(``None`` = identity; otherwise anything with ``@``, e.g. scipy.sparse),
+applied in the reference's order and with its identity aliasing:
 
 * ``cg``      — ``cg.py:16-259`` (loop ``cg.py:155-234``)
 * ``gmres``   — ``gmres.py:41-251`` with ``ArnoldiMGS`` ``arnoldi.py:107-200``
@@ -56,6 +58,11 @@ def _real_norm2(v):
     return v.real
 
 
+def _apply(op, x):
+    """``op @ x``; the reference's Identity returns x itself (_helpers.py:26-36)."""
+    return x if op is None else op @ x
+
+
 def givens(X):
     """givens.py:5-47 — one LAPACK lartg call per trailing column."""
     assert X.shape[0] == 2
@@ -75,8 +82,8 @@ def _rot(G, v):
     return np.einsum("ij...,j...->i...", G, v)
 
 
-def cg(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
-    """Restates cg.py:16-259 with M = Ml = I (no Lanczos return)."""
+def cg(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None, Ml=None):
+    """Restates cg.py:16-259 (no Lanczos return)."""
     b = np.asarray(b)
     assert A.shape[0] == A.shape[1] == b.shape[0]
     inner = default_inner(b.shape) if inner is None else inner
@@ -85,16 +92,19 @@ def cg(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=N
 
     def residual(z):  # cg.py:71-95
         r = b - A @ z
-        return r, _real_norm2(inner(r, r))
+        Ml_r = _apply(Ml, r)
+        M_Ml_r = _apply(M, Ml_r)
+        return M_Ml_r, Ml_r, _real_norm2(inner(Ml_r, M_Ml_r))
 
-    r, rho = residual(x0)
+    M_Ml_r0, Ml_r0, rho = residual(x0)
     if callback is not None:
-        callback(x0, r)
+        callback(x0, Ml_r0)
     resnorms = [np.sqrt(rho)]
-    y = np.zeros(x0.shape, dtype=r.dtype)
+    y = np.zeros(x0.shape, dtype=M_Ml_r0.dtype)
     rho_prev, rho_cur = None, rho
-    r = r.copy()
-    p = r.copy()
+    Ml_rk = Ml_r0.copy()
+    M_Ml_rk = M_Ml_r0.copy()
+    p = M_Ml_rk.copy()  # cg.py:138
     xk = None
     k = 0
     success = False
@@ -102,23 +112,24 @@ def cg(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=N
     while True:
         if np.all(resnorms[-1] <= criterion):  # cg.py:156-164
             xk = x0 + y if xk is None else xk
-            resnorms[-1] = np.sqrt(residual(xk)[1])
+            resnorms[-1] = np.sqrt(residual(xk)[2])
             if np.all(resnorms[-1] <= criterion):
                 success = True
                 break
         if k == maxiter:
             break
         if k > 0:  # cg.py:175-178
-            p = r + (rho_cur / _safe(rho_prev)) * p
-        Ap = A @ p
+            p = M_Ml_rk + (rho_cur / _safe(rho_prev)) * p
+        Ap = _apply(Ml, A @ p)  # Product(Ml, A) (cg.py:110, 180)
         alpha = rho_cur / _safe(inner(p, Ap))  # cg.py:183-185
         y += alpha * p
         xk = None
-        r -= alpha * Ap
+        Ml_rk -= alpha * Ap
         if callback is not None:
             xk = x0 + y
-            callback(xk, r)
-        rr = _real_norm2(inner(r, r))
+            callback(xk, Ml_rk)
+        M_Ml_rk = _apply(M, Ml_rk)  # cg.py:205-209
+        rr = _real_norm2(inner(Ml_rk, M_Ml_rk))
         rho_prev, rho_cur = rho_cur, rr
         resnorms.append(np.sqrt(rr))
         k += 1
@@ -141,8 +152,9 @@ def _trisolve_columns(R, y):
     return np.array(cols).T.reshape([k] + list(R.shape[2:]))
 
 
-def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
-    """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200), M = I."""
+def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None,
+          Ml=None, Mr=None):
+    """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200)."""
     b = np.asarray(b)
     assert A.shape[0] == A.shape[1] == b.shape[0]
     assert ortho.startswith("mgs")
@@ -151,18 +163,24 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
     maxiter = A.shape[0] if maxiter is None else maxiter
     x0 = np.zeros_like(b) if x0 is None else np.asarray(x0)
 
-    def resnorm_of(z):
-        r = b - A @ z
-        return np.sqrt(_real_norm2(inner(r, r)))
+    def resid(z):  # gmres.py:105-118
+        Ml_r = _apply(Ml, b - A @ z)
+        M_Ml_r = _apply(M, Ml_r)
+        return M_Ml_r, Ml_r, np.sqrt(_real_norm2(inner(Ml_r, M_Ml_r)))
 
-    r0 = b - A @ x0
-    r0norm = np.sqrt(_real_norm2(inner(r0, r0)))
+    def resnorm_of(z):
+        return resid(z)[2]
+
+    M_Ml_r0, Ml_r0, r0norm = resid(x0)
+    r0 = M_Ml_r0
     resnorms = [r0norm]
     if callback is not None:
-        callback(x0, r0)
+        callback(x0, Ml_r0)
 
     hdtype = np.result_type(A.dtype, r0.dtype)
-    V = [r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
+    # ArnoldiMGS.__init__ with Mv = M_Ml_r0 (arnoldi.py:136-150): P = Ml r0, V = M Ml r0
+    P = [Ml_r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
+    V = [M_Ml_r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
     invariant = False
     steps = 0
     R = np.zeros([maxiter + 1, maxiter] + list(b.shape[1:]), dtype=r0.dtype)
@@ -176,7 +194,7 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
         if steps > 0:
             coef = _trisolve_columns(R[:steps, :steps], yv)
             acc = sum(c * v for c, v in zip(coef, V))
-            return x0 + acc
+            return x0 + _apply(Mr, acc)
         return x0
 
     yk = None
@@ -196,18 +214,21 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
         # --- Arnoldi MGS step (arnoldi.py:167-200) ---
         if invariant:
             raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
-        w = A @ V[steps]
+        w = _apply(Ml, A @ _apply(Mr, V[steps]))  # Product(Ml, A, Mr)
         h = np.zeros([steps + 2] + list(b.shape[1:]), dtype=hdtype)
         for _ in range(sweeps):
             for j in range(steps + 1):
                 a = inner(V[j], w)
                 h[j] += a
-                w -= a * V[j]
-        h[steps + 1] = np.sqrt(inner(w, w))
+                w -= a * P[j]
+        Mw = _apply(M, w)
+        h[steps + 1] = np.sqrt(inner(w, Mw))
         if np.all(h[steps + 1] <= 1.0e-14):
             invariant = True
         else:
-            V.append(w / np.where(h[steps + 1] != 0.0, h[steps + 1], 1.0))
+            hk = np.where(h[steps + 1] != 0.0, h[steps + 1], 1.0)
+            P.append(w / hk)
+            V.append(Mw / hk)
         steps += 1
         # --- Givens QR update (gmres.py:206-221) ---
         R[: k + 2, k] = h[: k + 2]
@@ -233,8 +254,8 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
     return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)
 
 
-def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
-    """Restates minres.py:28-253 with Lanczos (arnoldi.py:203-281), M = I.
+def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None, Ml=None, Mr=None):
+    """Restates minres.py:28-253 with Lanczos (arnoldi.py:203-281).
 
     Precision follows the reference under NumPy-2 promotion: the Lanczos
     scalars ``h`` are kept in the vector dtype, while ``R``, the rotations, ``y``
@@ -246,19 +267,21 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
     maxiter = A.shape[0] if maxiter is None else maxiter
     x0 = np.zeros_like(b) if x0 is None else x0
 
-    def resnorm_of(z):
-        r = b - A @ z
-        return np.sqrt(_real_norm2(inner(r, r)))
+    def resnorm_of(z):  # minres.py:105-118
+        Ml_r = _apply(Ml, b - A @ z)
+        return np.sqrt(_real_norm2(inner(Ml_r, _apply(M, Ml_r))))
 
     r = b - A @ x0
-    rnorm = np.sqrt(_real_norm2(inner(r, r)))
-    dtype = r.dtype
-    hdtype = np.result_type(A.dtype, r.dtype)
-    # Lanczos state (arnoldi.py:203-235)
+    Ml_r = _apply(Ml, r)
+    M_Ml_r = _apply(M, Ml_r)
+    rnorm = np.sqrt(_real_norm2(inner(Ml_r, _apply(M, Ml_r))))
+    dtype = M_Ml_r.dtype
+    hdtype = np.result_type(A.dtype, M_Ml_r.dtype)
+    # Lanczos state (arnoldi.py:203-235): p = Ml r, v = M Ml r
     lz_h = np.zeros([3] + list(b.shape[1:]), dtype=hdtype)
     lz_scale = np.where(rnorm != 0.0, rnorm, 1.0)
-    lz_v = r / lz_scale
-    lz_p = r / lz_scale
+    lz_v = M_Ml_r / lz_scale
+    lz_p = Ml_r / lz_scale
     lz_pold = None
     lz_iter = 0
     invariant = False
@@ -277,7 +300,7 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
     criterion = np.maximum(tol * resnorms[0], atol)
     while True:
         if np.all(resnorms[-1] <= criterion):
-            xk = x0 + yk if xk is None else xk
+            xk = x0 + _apply(Mr, yk) if xk is None else xk
             resnorms[-1] = resnorm_of(xk)
             if np.all(resnorms[-1] <= criterion):
                 success = True
@@ -288,14 +311,15 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
         # --- Lanczos step (arnoldi.py:237-281) ---
         if invariant:
             raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
-        w = A @ lz_v
+        w = _apply(Ml, A @ _apply(Mr, lz_v))  # Product(Ml, A, Mr)
         if lz_iter > 0:
             lz_h[0] = lz_h[2]
             w -= lz_h[0] * lz_pold
         a = inner(lz_v, w)
         lz_h[1] = a
         w -= a * lz_p
-        lz_h[2] = np.sqrt(inner(w, w))
+        Mw = _apply(M, w)
+        lz_h[2] = np.sqrt(inner(w, Mw))
         if np.all(lz_h[2] <= 1.0e-14):
             invariant = True
             lz_v = lz_p = None
@@ -303,7 +327,7 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
             s = np.where(lz_h[2] != 0.0, lz_h[2], 1.0)
             lz_pold = lz_p
             lz_p = w / s
-            lz_v = w / s
+            lz_v = Mw / s
         lz_iter += 1
         h = lz_h.real
         # --- QR update (minres.py:193-224) ---
@@ -327,11 +351,11 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
         y = np.array([y[1], np.zeros_like(y[1])])
         rn = np.array(np.abs(y[0]))
         if callback is not None:
-            xk = x0 + yk
+            xk = x0 + _apply(Mr, yk)
             callback(xk, rn)
         resnorms.append(rn[()])
         k += 1
     if xk is None:
-        xk = x0 + yk
+        xk = x0 + _apply(Mr, yk)
     ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 4 + 8 * k}
     return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)

@@ -15,6 +15,7 @@ Outputs (``tests/golden/``):
   spmv.npz        SciPy csr_matvec / csr_matvecs on adversarial CSR (bitwise)
   lartg.npz       scipy dlartg / slartg and krylov.givens on edge-case pairs
   solvers.npz     cg / gmres / minres histories and solutions on small problems
+  precond.npz     the same with preconditioners M, Ml, Mr (make_precond)
   problems.json   SHA-256 of the generated BASELINE matrices
 """
 import contextlib
@@ -219,6 +220,20 @@ def make_solvers(krylov):
     np.savez_compressed(os.path.join(HERE, "solvers.npz"), **out)
 
 
+def make_precond(krylov):
+    from tests import precond_cases
+
+    out = {}
+    quiet = contextlib.redirect_stdout(io.StringIO())
+    q = precond_cases.inputs()
+    for case in precond_cases.CASES:
+        solver, A, b, kw = precond_cases.build(case, q)
+        with quiet:
+            sol, info = getattr(krylov, solver)(A, b, **kw)
+        _info_arrays(case[0], sol, info, out)
+    np.savez_compressed(os.path.join(HERE, "precond.npz"), **out)
+
+
 def make_problem_hashes():
     out = {}
     for name, fn in (
@@ -240,9 +255,13 @@ def make_problem_hashes():
 
 if __name__ == "__main__":
     krylov = _import_reference()
+    if "--only-precond" in sys.argv:
+        make_precond(krylov)
+        sys.exit(0)
     make_spmv()
     make_lartg(krylov)
     make_solvers(krylov)
+    make_precond(krylov)
     if "--no-large" not in sys.argv:
         make_problem_hashes()
     print("golden fixtures written to", HERE)

@@ -1,0 +1,62 @@
+"""Preconditioned solver cases shared by the fixture generator
+(tests/golden/make_golden.py -> tests/golden/precond.npz), the oracle tests
+and the GPU parity tests. Inputs are rebuilt identically from seeds."""
+import numpy as np
+import scipy.sparse as sp
+
+from krylov_amd import problems
+
+
+def inputs():
+    """A variable-coefficient SPD matrix with its Jacobi and symmetric-scaling
+    diagonals, a random nonsymmetric matrix with |Jacobi| (SPD) and Jacobi
+    diagonals, and a 3-column right-hand side."""
+    P = problems.poisson2d(32)
+    n = P.shape[0]
+    shift = np.random.default_rng(7).uniform(0.0, 2.0, n)
+    Pvar = (P + sp.diags(shift)).tocsr()
+    d = Pvar.diagonal()
+    R = problems.random_nonsym(3000, seed=4)
+    dr = R.diagonal()
+    return {
+        "Pvar": Pvar,
+        "Mj": sp.diags(1.0 / d).tocsr(),
+        "S": sp.diags(1.0 / np.sqrt(d)).tocsr(),
+        "R": R,
+        "RMabs": sp.diags(1.0 / np.abs(dr)).tocsr(),
+        "RMj": sp.diags(1.0 / dr).tocsr(),
+        "B3": np.random.default_rng(8).standard_normal((n, 3)),
+    }
+
+
+# (fixture prefix, solver, operator, right-hand side, keyword arguments);
+# string values of M / Ml / Mr name entries of inputs()
+CASES = [
+    ("cg_M", "cg", "Pvar", "ones", dict(M="Mj", tol=1e-8)),
+    ("cg_Ml", "cg", "Pvar", "ones", dict(Ml="Mj", tol=0.0, maxiter=25)),
+    ("cg_M_Ml", "cg", "Pvar", "ones", dict(M="Mj", Ml="S", tol=0.0, maxiter=25)),
+    ("cg_M_blk3", "cg", "Pvar", "B3", dict(M="Mj", tol=1e-8)),
+    ("gmres_M", "gmres", "R", "ones", dict(M="RMabs", tol=0.0, maxiter=30)),
+    ("gmres_Ml", "gmres", "R", "ones", dict(Ml="RMj", tol=0.0, maxiter=30)),
+    ("gmres_Mr", "gmres", "R", "ones", dict(Mr="RMj", tol=0.0, maxiter=30)),
+    ("gmres_all", "gmres", "R", "ones", dict(M="RMabs", Ml="RMj", Mr="RMj", tol=0.0, maxiter=30)),
+    ("gmres_M_mgs2", "gmres", "R", "ones", dict(M="RMabs", ortho="mgs2", tol=0.0, maxiter=20)),
+    ("minres_M", "minres", "Pvar", "ones", dict(M="Mj", tol=1e-8)),
+    ("minres_MlMr", "minres", "Pvar", "ones", dict(Ml="S", Mr="S", tol=1e-8)),
+    ("minres_all", "minres", "Pvar", "ones", dict(M="Mj", Ml="S", Mr="S", tol=0.0, maxiter=40)),
+]
+
+
+def build(case, q=None, wrap=None):
+    """-> (solver name, A, b, kwargs) with the named matrices substituted;
+    `wrap` maps each operator (e.g. to a device operator) if given."""
+    q = inputs() if q is None else q
+    prefix, solver, a, b, kw = case
+    A = q[a]
+    bb = np.ones(A.shape[0]) if b == "ones" else q[b]
+    out = {}
+    for key, val in kw.items():
+        if key in ("M", "Ml", "Mr"):
+            val = q[val] if wrap is None else wrap(q[val])
+        out[key] = val
+    return solver, (A if wrap is None else wrap(A)), bb, out

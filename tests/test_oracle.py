@@ -152,3 +152,15 @@ def test_generators_match_pinned_hashes(name, fn):
     A = fn()
     assert A.nnz == pinned[name]["nnz"]
     assert problems.csr_sha256(A) == pinned[name]["sha256"]
+
+
+@pytest.mark.parametrize("case", __import__("tests.precond_cases", fromlist=["CASES"]).CASES, ids=lambda c: c[0])
+def test_oracle_preconditioned(case):
+    """M / Ml / Mr restated in the reference's order: bitwise the reference."""
+    from oracle import krylov_ref as K
+    from tests import precond_cases
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "precond.npz"))
+    solver, A, b, kw = precond_cases.build(case)
+    sol, info = getattr(K, solver)(A, b, **kw)
+    _check(case[0], sol, info, d)
