@@ -120,7 +120,11 @@ int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void 
  *        resnorm <= criterion (the test at cg.py:156). Writes the new residual
  *        norms (steps_done x k) to resnorms.
  * residual: explicit ||M Ml (b - A xk)||_{M^-1} with xk = x0 + yk (cg.py:158-160).
- * get:   download xk (which = 0) or the updated residual r (which = 1). */
+ * get:   download xk (which = 0), the updated residual Ml_r (which = 1) or
+ *        M Ml_r (which = 2).
+ * scalars: the current [rho, rho_prev, alpha, omega] (4 x k values) of the
+ *        recurrence, for the Lanczos relation of return_arnoldi
+ *        (cg.py:218-233). */
 int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out);
 int kry_cg_destroy(kry_cg *s);
 int kry_cg_set_preconditioners(kry_cg *s, kry_csr *M, kry_csr *Ml);
@@ -129,6 +133,7 @@ int kry_cg_set_criterion(kry_cg *s, const double *criterion);
 int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnorms);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
+int kry_cg_scalars(kry_cg *s, double *out);
 
 /* ---- GMRES (gmres.py:41-251, ArnoldiMGS arnoldi.py:107-200) --------------
  * set_preconditioners: M, Ml, Mr as device operators (NULL = identity); the

@@ -70,6 +70,7 @@ _SIGNATURES = {
     "kry_cg_run": [_vp, _i32, _ip32, _dp],
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
+    "kry_cg_scalars": [_vp, _dp],
     "kry_cg_set_preconditioners": [_vp, _vp, _vp],
     "kry_gmres_set_preconditioners": [_vp, _vp, _vp, _vp],
     "kry_minres_set_preconditioners": [_vp, _vp, _vp, _vp],

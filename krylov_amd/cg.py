@@ -59,6 +59,12 @@ class _CGState:
         check(lib.kry_cg_get(self.h, which, _lib.ptr(out)))
         return out
 
+    def scalars(self):
+        """[rho, rho_prev, alpha, omega] rows (kpad values each)."""
+        out = np.zeros((4, self.prob.kpad))
+        check(lib.kry_cg_scalars(self.h, _lib.dptr(out)))
+        return out
+
 
 def _norm_from_sq(prob, sq):
     return np.sqrt(np.asarray(sq[: prob.kc]).astype(prob.inner_dtype))
@@ -73,8 +79,6 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     ``M``/``Ml``: ``None``/``Identity`` or an operator of the same kinds as
     ``A`` (applied on the device as SpMVs, cg.py:70-90, 180, 207).
     """
-    if return_arnoldi:
-        raise NotImplementedError("return_arnoldi is not on the MI355X path yet")
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter
@@ -88,6 +92,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     resnorms = [prob.colvals(rn0)]
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))
+    lanczos = _Lanczos(prob, st, resnorms[0], maxiter) if return_arnoldi else None
 
     k = 0
     success = False
@@ -100,10 +105,12 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
                 break
         if k == maxiter:
             break
-        steps = 1 if callback is not None else min(_helpers.CHUNK, maxiter - k)
+        steps = 1 if (callback is not None or lanczos is not None) else min(_helpers.CHUNK, maxiter - k)
         hist = st.run(steps)
         for row in hist:
             resnorms.append(prob.colvals(row))
+            if lanczos is not None:
+                lanczos.step(k, resnorms[-1])
             k += 1
         if callback is not None and len(hist):
             callback(prob.unpad_vec(st.get(0), prob.r0_dtype), prob.unpad_vec(st.get(1), prob.r0_dtype))
@@ -117,4 +124,44 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         "inner": 2 + 2 * k,
         "axpy": 2 + 2 * k,
     }
-    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)
+    arnoldi = lanczos.result(k) if lanczos is not None else None
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, arnoldi=arnoldi)
+
+
+class _Lanczos:
+    """The Lanczos relation CG returns with ``return_arnoldi`` (cg.py:140-148,
+    218-233): V_k = (-1)^k M Ml r_k / ||.||, P_k the same with Ml r_k, and the
+    tridiagonal H built from alpha, omega and the rho ratios read back from the
+    device after every step (one step per run in this mode)."""
+
+    def __init__(self, prob, st, norm0, maxiter):
+        self.prob, self.st = prob, st
+        nz = np.where(np.asarray(norm0) > 0.0, norm0, 1.0)
+        self.V = [self._vec(2) / nz]
+        self.P = [self._vec(1) / nz]
+        self.H = np.zeros([maxiter + 1, maxiter] + list(prob.tail), dtype=float)
+        self.alpha_old = 0
+        self.omega = None
+
+    def _vec(self, which):
+        return self.prob.unpad_vec(self.st.get(which), self.prob.r0_dtype)
+
+    def _sc(self, row):
+        return self.prob.colvals(row)
+
+    def step(self, k, norm):
+        rho, rho_prev, alpha, omega_next = (self._sc(r) for r in self.st.scalars())
+        sign = (-1) ** (k + 1)
+        self.V.append(sign * self._vec(2) / norm)
+        self.P.append(sign * self._vec(1) / norm)
+        H = self.H
+        H[k, k] = 1.0 / alpha
+        if k > 0:
+            H[k - 1, k] = H[k, k - 1]
+            H[k, k] += self.omega / self.alpha_old
+        H[k + 1, k] = np.sqrt(rho / rho_prev) / alpha
+        self.alpha_old = alpha
+        self.omega = omega_next  # the omega of the next iteration's p update (cg.py:177)
+
+    def result(self, k):
+        return [self.V, self.H[: k + 1, :k], self.P]

@@ -454,7 +454,7 @@ int kry_cg_residual(kry_cg *s, double *norm2) {
 
 int kry_cg_get(kry_cg *s, int which, void *host) {
   KRY_API_BEGIN
-  KRY_REQUIRE(s && host && (which == 0 || which == 1), KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s && host && which >= 0 && which <= 2, KRY_EINVAL, "bad argument");
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   const size_t vb = (size_t)s->n * s->k * dsize(s->dtype);
@@ -468,9 +468,22 @@ int kry_cg_get(kry_cg *s, int which, void *host) {
                                 nullptr, nullptr, 0, st);
     KRY_HIP(hipMemcpyAsync(host, s->xk, vb, hipMemcpyDeviceToHost, st));
   } else {
-    KRY_HIP(hipMemcpyAsync(host, s->r, vb, hipMemcpyDeviceToHost, st));
+    // 1: Ml_rk; 2: M_Ml_rk (= Ml_rk without M)
+    KRY_HIP(hipMemcpyAsync(host, which == 2 && s->M ? s->z : s->r, vb, hipMemcpyDeviceToHost, st));
   }
   KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+int kry_cg_scalars(kry_cg *s, double *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && out, KRY_EINVAL, "null argument");
+  const int k = s->k;
+  const int slots[4] = {S_RHO, S_RHO_PREV, S_ALPHA, S_OMEGA};
+  for (int i = 0; i < 4; ++i)
+    KRY_HIP(hipMemcpyAsync(out + (size_t)i * k, s->scal + (size_t)slots[i] * k, k * 8, hipMemcpyDeviceToHost,
+                           s->ctx->stream));
+  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
   KRY_API_END
 }
 

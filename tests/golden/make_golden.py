@@ -16,6 +16,7 @@ Outputs (``tests/golden/``):
   lartg.npz       scipy dlartg / slartg and krylov.givens on edge-case pairs
   solvers.npz     cg / gmres / minres histories and solutions on small problems
   precond.npz     the same with preconditioners M, Ml, Mr (make_precond)
+  arnoldi.npz     cg(return_arnoldi=True) Lanczos relations (make_arnoldi)
   problems.json   SHA-256 of the generated BASELINE matrices
 """
 import contextlib
@@ -234,6 +235,30 @@ def make_precond(krylov):
     np.savez_compressed(os.path.join(HERE, "precond.npz"), **out)
 
 
+def make_arnoldi(krylov):
+    """cg(..., return_arnoldi=True): the Lanczos relation [V, H, P]
+    (cg.py:140-148, 218-258) on the reference's test problem
+    (tests/test_solvers.py:41-50) and on Poisson 16^2 with a Jacobi M."""
+    import scipy.sparse as sp
+
+    out = {}
+    a = np.linspace(1.0, 2.0, 5)
+    a[-1] = 1e-2
+    cases = [("diag_1d", np.diag(a), np.ones(5), {}), ("diag_blk3", np.diag(a), np.ones((5, 3)), {})]
+    P = problems.poisson2d(16)
+    d = P.diagonal() + np.random.default_rng(3).uniform(0.0, 1.0, P.shape[0])
+    Pv = (P + sp.diags(d - P.diagonal())).tocsr()
+    cases.append(("pvar16_M", Pv, np.ones(Pv.shape[0]), {"M": sp.diags(1.0 / d).tocsr()}))
+    for name, A, b, kw in cases:
+        _, info = krylov.cg(A, b, tol=1.0e-7, return_arnoldi=True, **kw)
+        V, H, Pb = info.arnoldi
+        _info_arrays(f"arnoldi_{name}", None if not info.success else info.xk, info, out)
+        out[f"arnoldi_{name}_V"] = np.array(V)
+        out[f"arnoldi_{name}_H"] = np.asarray(H)
+        out[f"arnoldi_{name}_P"] = np.array(Pb)
+    np.savez_compressed(os.path.join(HERE, "arnoldi.npz"), **out)
+
+
 def make_problem_hashes():
     out = {}
     for name, fn in (
@@ -257,11 +282,13 @@ if __name__ == "__main__":
     krylov = _import_reference()
     if "--only-precond" in sys.argv:
         make_precond(krylov)
+        make_arnoldi(krylov)
         sys.exit(0)
     make_spmv()
     make_lartg(krylov)
     make_solvers(krylov)
     make_precond(krylov)
+    make_arnoldi(krylov)
     if "--no-large" not in sys.argv:
         make_problem_hashes()
     print("golden fixtures written to", HERE)

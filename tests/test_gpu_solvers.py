@@ -250,3 +250,48 @@ def test_device_matches_oracle_on_metric_shape_small():
     assert got.numsteps == ref.numsteps
     r, g = np.asarray(ref.resnorms), np.asarray(got.resnorms)
     assert np.all(np.abs(g[:-1] - r[:-1]) <= 1e-10 * np.abs(r[:-1]))
+
+
+@pytest.mark.parametrize("name", ["diag_1d", "diag_blk3", "pvar16_M"])
+def test_return_arnoldi(name):
+    """cg(return_arnoldi=True) returns the reference's Lanczos relation
+    [V, H, P] (cg.py:140-148, 218-258; tests/test_solvers.py:41-50)."""
+    import os
+
+    import scipy.sparse as sp
+
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "arnoldi.npz"))
+    a = np.linspace(1.0, 2.0, 5)
+    a[-1] = 1e-2
+    kw = {}
+    if name == "diag_1d":
+        A, b = np.diag(a), np.ones(5)
+    elif name == "diag_blk3":
+        A, b = np.diag(a), np.ones((5, 3))
+    else:
+        P = problems.poisson2d(16)
+        dg = P.diagonal() + np.random.default_rng(3).uniform(0.0, 1.0, P.shape[0])
+        A = (P + sp.diags(dg - P.diagonal())).tocsr()
+        b = np.ones(A.shape[0])
+        kw["M"] = sp.diags(1.0 / dg).tocsr()
+    _, info = krylov_amd.cg(A, b, tol=1.0e-7, return_arnoldi=True, **kw)
+    p = f"arnoldi_{name}"
+    if name.startswith("diag"):
+        assert np.all(info.resnorms[-1] < 1.0e-7)  # the reference test's own check
+    assert info.success == bool(d[p + "_success"])
+    assert info.numsteps == int(d[p + "_numsteps"])
+    V, H, Pb = info.arnoldi
+    # Lanczos vectors r_k / ||r_k|| are compared where r_k is above round-off:
+    # once CG has converged to machine precision (the 5 x 5 diagonal case
+    # reaches r_5 ~ 1e-17), r_k is rounding noise in both runs
+    res = np.asarray(d[p + "_resnorms"]).reshape(len(V), -1)
+    live = np.all(res > 1e-12 * res[0], axis=1)
+    for got, ref in ((np.array(V), d[p + "_V"]), (np.array(Pb), d[p + "_P"])):
+        assert got.shape == ref.shape
+        np.testing.assert_allclose(got[live], ref[live], rtol=1e-8, atol=1e-10 * np.abs(ref).max())
+    Hg, Hr = np.asarray(H), d[p + "_H"]
+    assert Hg.shape == Hr.shape
+    np.testing.assert_allclose(Hg, Hr, rtol=1e-8, atol=1e-8 * np.abs(Hr).max())
