@@ -140,7 +140,9 @@ int kry_cg_scalars(kry_cg *s, double *out);
  *         Arnoldi operator is Ml A Mr, M gives the second basis P (V = M P),
  *         and xk = x0 + Mr (sum_i yy_i V_i) (gmres.py:97-99, 139).
  * create: workspace for up to `maxiter` Arnoldi steps with `sweeps` MGS
- *         passes per step ("mgs" = 1, "mgsK" = K).
+ *         passes per step ("mgs" = 1, "mgsK" = K), or sweeps = 0 for
+ *         Householder Arnoldi (ortho="householder", arnoldi.py:33-104; k = 1,
+ *         default inner, no M).
  * start:  r0 = b - A x0, ||r0||, V0 = r0 / ||r0|| (guarded), y[0] = ||r0||.
  * run:    up to max_steps Arnoldi + Givens steps; stops early after a step
  *         whose |y[k+1]| all satisfy the criterion or that found the space

@@ -34,6 +34,12 @@ struct kry_gmres {
   void *mw = nullptr;   // M w (with M)
   void *t1 = nullptr;   // Mr v / solution scratch (with Mr)
   void *t2 = nullptr;   // A Mr v / raw residual (with Ml)
+  // Householder Arnoldi (sweeps == 0, one right-hand side): reflector vectors
+  // U_j (zero below j) and their scalars (householder.py:8-53)
+  bool householder = false;
+  void *U = nullptr;      // (maxiter + 2) vectors
+  void *vnew = nullptr;   // the next basis vector under construction
+  double *hh = nullptr;   // (maxiter + 2) x HH_COUNT
   double *w = nullptr;
   double *part = nullptr, *part1 = nullptr, *part2 = nullptr;  // partial rows (MGS ping-pong)
   double *scal = nullptr;  // alpha[k], hsafe[k], crit[k], tmp[k]
@@ -221,16 +227,17 @@ __global__ void gm_coef_kernel(const double *part, int P, int k, double *scal, d
 // (gmres.py:206-221); resnorm |y[col+1]|; stop test.
 template <typename S>
 __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, double *h, double *R, double *y,
-                             double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step) {
+                             double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step,
+                             int hgiven = 0) {
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock];
   __shared__ double rn[kMaxCols];
   __shared__ int flag;
-  reduce_partials(part, P, k, red);
+  if (!hgiven) reduce_partials(part, P, k, red);  // else h[k+1] is already in h (Householder)
   const int c = threadIdx.x;
   const int64_t ld = (int64_t)maxiter * k;  // R row stride
   if (c < k) {
-    const S hk1 = sqrt((S)red[c]);
+    const S hk1 = hgiven ? (S)h[(int64_t)(col + 1) * k + c] : sqrt((S)red[c]);
     h[(int64_t)(col + 1) * k + c] = (double)hk1;
     red[c] = (double)hk1;
   }
@@ -364,6 +371,164 @@ __global__ void gm_trsv_big_kernel(const double *R, const double *y, double *yy,
   }
 }
 
+// ------------------------------------------------ Householder Arnoldi
+// ArnoldiHouseholder (arnoldi.py:33-104) with Householder(x) of
+// householder.py:8-53, one right-hand side. Reflector j is stored as a full
+// vector U_j (zeros below index j) with scalars beta (0 or 2), alpha, and the
+// values it was built from. Applying it to x[j:] is x - (beta * u) * <u, x>,
+// each a streaming pass whose <u, x> arrives as block partials from the pass
+// before (fixed-order reduction in every block, as in the MGS passes).
+enum { HH_BETA = 0, HH_ALPHA = 1, HH_V0 = 2, HH_NRM = 3, HH_COUNT = 4 };
+
+// Householder(x[j:]): gamma = x[j], sigma2 = <x[j+1:], x[j+1:]> from the partials
+// (arithmetic in the vector dtype, as the reference's arrays)
+template <typename S>
+__global__ void hh_make_kernel(const S *x, int64_t j, const double *part, int P, double *hh, const Ctrl *ctrl,
+                               int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  reduce_partials(part, P, 1, red);
+  if (threadIdx.x != 0) return;
+  const S g = x[j];
+  const S sig2 = (S)red[0];
+  const S ag = fabs(g);
+  S xnorm = sqrt(ag * ag + sig2);
+  S beta, alpha, v0 = S(1);
+  if (sig2 == S(0)) {
+    beta = S(0);
+    xnorm = ag;
+    alpha = g == S(0) ? S(1) : g / xnorm;
+  } else {
+    beta = S(2);
+    if (g == S(0)) {
+      v0 = -sqrt(sig2);
+      alpha = S(1);
+    } else {
+      const S t = g / ag * xnorm;
+      v0 = g + t;
+      alpha = -g / ag;
+    }
+  }
+  const S av0 = fabs(v0);
+  const S nrm = sqrt(av0 * av0 + sig2);
+  hh[HH_BETA] = (double)beta;
+  hh[HH_ALPHA] = (double)alpha;
+  hh[HH_V0] = (double)v0;
+  hh[HH_NRM] = (double)nrm;
+}
+
+// U_j = (v0 at j, x[i] beyond) / nrm, zero below j; partials of <U_j, x>.
+template <typename V>
+__global__ __launch_bounds__(kBlock) void hh_vec_kernel(int64_t N, const V *__restrict__ x, V *__restrict__ u,
+                                                        int64_t j, const double *hh, double *__restrict__ part,
+                                                        const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  const V v0 = (V)hh[HH_V0], nrm = (V)hh[HH_NRM];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+    V ui = V(0);
+    const V xi = x[i];
+    if (i >= j) {
+      ui = (i == j ? v0 : xi) / nrm;
+      acc += (double)ui * (double)xi;
+    }
+    u[i] = ui;
+  }
+  red[threadIdx.x] = acc;
+  block_tree_reduce(red, kBlock, 1);
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// x[j:] = x[j:] - (beta U_j) s, s = <U_j, x> (from part_in, or *s_direct
+// when P_in == 0); optionally x[j] *= alpha_j (arnoldi.py:75-77). Emits the
+// partials of the next inner product: <q, x_new> over i >= qoff (q = x_new
+// itself when q_is_x), if qoff >= 0. With `out`, writes x_new * (*scale) to out.
+template <typename V>
+__global__ __launch_bounds__(kBlock) void hh_apply_kernel(int64_t N, V *__restrict__ x, const V *__restrict__ u,
+                                                          int64_t j, const double *hh, const double *part_in,
+                                                          int P_in, const V *s_direct, int apply_alpha,
+                                                          const V *__restrict__ q, int q_is_x, int64_t qoff,
+                                                          double *__restrict__ part_out, V *__restrict__ out,
+                                                          const double *scale, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  V sv;
+  if (P_in > 0) {
+    reduce_partials(part_in, P_in, 1, red);
+    sv = (V)red[0];
+    __syncthreads();
+  } else {
+    sv = *s_direct;
+  }
+  const V beta = (V)hh[HH_BETA], alpha = (V)hh[HH_ALPHA];
+  const V sc = out ? (V)*scale : V(1);
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+    V xi = x[i];
+    if (i >= j && beta != V(0)) {
+      const V bu = beta * u[i];
+      const V t = bu * sv;
+      xi = xi - t;
+    }
+    if (apply_alpha && i == j) xi = xi * alpha;
+    if (out) out[i] = xi * sc;
+    else x[i] = xi;
+    if (qoff >= 0 && i >= qoff) acc += (double)(q_is_x ? xi : q[i]) * (double)xi;
+  }
+  if (qoff >= 0) {
+    red[threadIdx.x] = acc;
+    block_tree_reduce(red, kBlock, 1);
+    if (threadIdx.x == 0) part_out[blockIdx.x] = red[0];
+  }
+}
+
+// The Hessenberg column of step k: h[:k+1] = w[:k+1] after the forward
+// reflections; h[k+1] = |(w[k+1] - (beta u) s) alpha| for the new reflector
+// (arnoldi.py:79-86), or 0 when k + 1 == N (the space is exhausted).
+template <typename V>
+__global__ void hh_col_kernel(const V *w, const V *u, int64_t k, int64_t N, const double *hh, const double *part,
+                              int P, double *h, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  if (k + 1 < N) reduce_partials(part, P, 1, red);
+  for (int64_t i = threadIdx.x; i <= k; i += kBlock) h[i] = (double)w[i];
+  if (threadIdx.x == 0) {
+    V hk1 = V(0);
+    if (k + 1 < N) {
+      const V beta = (V)hh[HH_BETA], alpha = (V)hh[HH_ALPHA];
+      V xi = w[k + 1];
+      if (beta != V(0)) {
+        const V bu = beta * u[k + 1];
+        const V t = bu * (V)red[0];
+        xi = xi - t;
+      }
+      hk1 = fabs(xi * alpha);
+    }
+    h[k + 1] = (double)hk1;
+  }
+}
+
+template <typename V>
+__global__ void hh_unit_kernel(V *x, int64_t i, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  if (threadIdx.x == 0 && blockIdx.x == 0) x[i] = V(1);
+}
+
+template <typename V>
+struct OpSuffixSq {  // partials of <x[off:], x[off:]> (householder.py:32)
+  const V *x;
+  int64_t off;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V a[W];
+    VIO<V>::load(x, e, N, a);
+#pragma unroll
+    for (int v = 0; v < W; ++v)
+      if (e + v < N && e + v >= off) acc[v] += (double)a[v] * (double)a[v];
+  }
+};
+
 // w = Ml (A (Mr v)) (Product(Ml, A, Mr), gmres.py:139), `epi` on the last product.
 template <typename V, typename MV, typename I, class Epi>
 void gm_apply_op(kry_gmres *s, const V *v, Epi epi, double *part, int *P, const Ctrl *ctrl, int step) {
@@ -419,10 +584,93 @@ void gm_start_impl(kry_gmres *s) {
   const V *v0src = s->M ? static_cast<const V *>(s->mw) : wv;
   launch_elementwise<V>(N, k, OpScaleDiv<V>{v0src, static_cast<V *>(s->V), s->scal + G_HSAFE * k, k}, nullptr,
                         nullptr, 0, st);
+  if (s->householder) {  // houses = [Householder(Ml r0)] (arnoldi.py:51)
+    const int Ps = launch_elementwise<V>(N, 1, OpSuffixSq<V>{wv, 1}, s->part, nullptr, 0, st);
+    hipLaunchKernelGGL(hh_make_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const V *)wv, (int64_t)0,
+                       (const double *)s->part, Ps, s->hh, (const Ctrl *)nullptr, 0);
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (N + 4 * kBlock - 1) / (4 * kBlock)));
+    hipLaunchKernelGGL(hh_vec_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, (const V *)wv, static_cast<V *>(s->U),
+                       (int64_t)0, (const double *)s->hh, s->part2, (const Ctrl *)nullptr, 0);
+    KRY_HIP(hipGetLastError());
+  }
+}
+
+// One Householder Arnoldi step per iteration (arnoldi.py:65-104).
+template <typename V, typename MV, typename I>
+void hh_run_impl(kry_gmres *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int64_t N = s->n;
+  V *w = static_cast<V *>(s->wv);
+  V *vnew = static_cast<V *>(s->vnew);
+  auto U = [&](int64_t j) { return basis<V>(s->U, s->vstride, (int)j); };
+  auto hh = [&](int64_t j) { return s->hh + j * HH_COUNT; };
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (N + 4 * kBlock - 1) / (4 * kBlock)));
+  for (int step = 0; step < max_steps; ++step) {
+    const int64_t k = s->steps + step;
+    if (k >= s->maxiter) break;
+    int P;
+    {
+      ProfScope ps(s->ctx, PROF_SPMV);  // Av = A V_k with <U_0, Av> partials
+      gm_apply_op<V, MV, I>(s, basis<V>(s->V, s->vstride, (int)k), EpiStoreDot<V>{w, U(0), nullptr, 1}, s->part, &P,
+                            s->ctrl, step);
+    }
+    hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, st, s->part, P, 1, s->part1);
+    const double *pin = s->part1;
+    int Pin = 1;
+    double *pbuf[2] = {s->part, s->part2};
+    int flip = 0;
+    // Av[j:] = H_j Av[j:]; Av[j] *= alpha_j for j = 0..k (arnoldi.py:74-77)
+    for (int64_t j = 0; j <= k; ++j) {
+      const bool last = j == k;
+      double *pout = pbuf[flip];
+      ProfScope ps(s->ctx, PROF_MGS);
+      hipLaunchKernelGGL(hh_apply_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, w, (const V *)U(j), j,
+                         (const double *)hh(j), pin, Pin, (const V *)nullptr, 1, last ? (const V *)nullptr : (const V *)U(j + 1),
+                         last ? 1 : 0, last ? k + 2 : j + 1, pout, (V *)nullptr, (const double *)nullptr, s->ctrl, step);
+      pin = pout;
+      Pin = G;
+      flip ^= 1;
+    }
+    const bool more = k + 1 < N;
+    double *pout = pbuf[flip];
+    if (more) {  // the new reflector from Av[k+1:] (arnoldi.py:79-81)
+      hipLaunchKernelGGL(hh_make_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const V *)w, k + 1, pin, Pin, hh(k + 1),
+                         s->ctrl, step);
+      hipLaunchKernelGGL(hh_vec_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, (const V *)w, U(k + 1), k + 1,
+                         (const double *)hh(k + 1), pout, s->ctrl, step);
+    }
+    hipLaunchKernelGGL(hh_col_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const V *)w,
+                       more ? (const V *)U(k + 1) : (const V *)nullptr, k, N, (const double *)hh(more ? k + 1 : 0),
+                       (const double *)pout, G, s->h, s->ctrl, step);
+    hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const double *)nullptr, 0, 1, s->scal, s->h,
+                       s->R, s->y, s->Gc, s->Gs, (int)k, s->maxiter, s->hist, s->ctrl, step, 1);
+    KRY_HIP(hipGetLastError());
+    if (!more) continue;  // invariant: no new basis vector
+    // vnew = e_{k+1}; vnew[j:] = H_j vnew[j:] for j = k+1..0; V_{k+1} = vnew alpha_{k+1}
+    // (arnoldi.py:91-95)
+    KRY_HIP(hipMemsetAsync(vnew, 0, (size_t)N * sizeof(V), st));
+    hipLaunchKernelGGL(hh_unit_kernel<V>, dim3(1), dim3(64), 0, st, vnew, k + 1, s->ctrl, step);
+    double *po = pbuf[flip ^ 1];
+    hipLaunchKernelGGL(hh_apply_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, vnew, (const V *)U(k + 1), k + 1,
+                       (const double *)hh(k + 1), (const double *)nullptr, 0, (const V *)(U(k + 1) + (k + 1)), 0,
+                       (const V *)U(k), 0, k, po, (V *)nullptr, (const double *)nullptr, s->ctrl, step);
+    pin = po;
+    for (int64_t j = k; j >= 0; --j) {
+      const bool last = j == 0;
+      double *pn = (pin == pbuf[0]) ? pbuf[1] : pbuf[0];
+      hipLaunchKernelGGL(hh_apply_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, vnew, (const V *)U(j), j,
+                         (const double *)hh(j), pin, G, (const V *)nullptr, 0, last ? (const V *)nullptr : (const V *)U(j - 1),
+                         0, last ? (int64_t)-1 : j - 1, pn, last ? basis<V>(s->V, s->vstride, (int)k + 1) : (V *)nullptr,
+                         last ? (const double *)(hh(k + 1) + HH_ALPHA) : (const double *)nullptr, s->ctrl, step);
+      pin = pn;
+    }
+    KRY_HIP(hipGetLastError());
+  }
 }
 
 template <typename V, typename MV, typename I>
 void gm_run_impl(kry_gmres *s, int max_steps) {
+  if (s->householder) return hh_run_impl<V, MV, I>(s, max_steps);
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
@@ -533,7 +781,8 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 
 void gm_free(kry_gmres *s) {
   void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
-                  s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2};
+                  s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2,
+                  s->U, s->vnew, s->hh};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -561,7 +810,8 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
   KRY_REQUIRE(is_pow2(k) && k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   KRY_REQUIRE(dtype == A->dtype || (dtype == KRY_F64 && A->dtype == KRY_F32), KRY_EINVAL,
               "vectors must have the operator dtype (or float64 over a float32 operator)");
-  KRY_REQUIRE(maxiter >= 0 && sweeps >= 1, KRY_EINVAL, "bad maxiter / sweeps");
+  KRY_REQUIRE(maxiter >= 0 && sweeps >= 0, KRY_EINVAL, "bad maxiter / sweeps");
+  KRY_REQUIRE(sweeps >= 1 || k == 1, KRY_EUNSUPPORTED, "Householder Arnoldi works on one right-hand side");
   KRY_HIP(hipSetDevice(ctx->device));
   auto *s = new kry_gmres();
   try {
@@ -579,6 +829,12 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     s->xk = dev_alloc(vb);
     s->rt = dev_alloc(vb);
     s->V = dev_alloc(vb * ((size_t)maxiter + 1));
+    if (sweeps == 0) {
+      s->householder = true;
+      s->U = dev_alloc(vb * ((size_t)maxiter + 2));
+      s->vnew = dev_alloc(vb);
+      s->hh = static_cast<double *>(dev_alloc(((size_t)maxiter + 2) * HH_COUNT * 8));
+    }
     KRY_HIP(hipMemsetAsync(s->xk, 0, vb, ctx->stream));
     KRY_HIP(hipMemsetAsync(s->wv, 0, vb, ctx->stream));
     s->part = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
@@ -613,6 +869,7 @@ int kry_gmres_set_preconditioners(kry_gmres *s, kry_csr *M, kry_csr *Ml, kry_csr
     KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
                 "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
   }
+  KRY_REQUIRE(!(M && s->householder), KRY_EINVAL, "Householder Arnoldi does not take M (gmres.py:160)");
   KRY_HIP(hipSetDevice(s->ctx->device));
   const size_t vb = s->vstride * dsize(s->dtype);
   auto need = [&](void *&buf, size_t bytes) {
@@ -651,6 +908,7 @@ int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r
   check_vec(b, s->n, s->k, s->dtype, "b");
   if (x0) check_vec(x0, s->n, s->k, s->dtype, "x0");
   check_weights(w, s->n);
+  KRY_REQUIRE(!(w && s->householder), KRY_EINVAL, "Householder Arnoldi needs the Euclidean inner product");
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   const size_t vb = b->bytes();

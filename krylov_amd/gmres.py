@@ -63,12 +63,24 @@ class _GmresState:
 
 def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1.0e-15,
           maxiter=None, callback=None):
-    """Preconditioned GMRES, reference signature (``gmres.py:41-54``)."""
-    if not ortho.startswith("mgs"):
-        if ortho == "householder":
-            raise NotImplementedError("ortho='householder' is not on the MI355X path yet (SURVEY §8(f) rank 2)")
+    """Preconditioned GMRES, reference signature (``gmres.py:41-54``).
+
+    ``ortho``: "mgs", "mgsK" (K MGS sweeps) or "householder" (Householder
+    Arnoldi, arnoldi.py:33-104, one right-hand side, default inner, no M)."""
+    if ortho.startswith("mgs"):
+        sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    elif ortho == "householder":
+        # gmres.py:158-161 and householder.py:19-22: Euclidean inner product,
+        # no M, one (quasi-1-D) right-hand side
+        assert inner is None, "ortho='householder' needs the default inner product"
+        assert _helpers._is_identity(M), "ortho='householder' does not take M"
+        bs = np.shape(b)
+        assert len(bs) == 1 or (len(bs) == 2 and bs[1] == 1), (
+            "Householder only works for quasi-1D vectors for now. " f"Input vector has shape {bs}."
+        )
+        sweeps = 0
+    else:
         raise ValueError(f"unknown ortho {ortho!r}")
-    sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
     x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0

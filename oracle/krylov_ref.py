@@ -58,6 +58,17 @@ def _real_norm2(v):
     return v.real
 
 
+class _Prod:
+    """Product(Ml, A, Mr) (_helpers.py:39-48): applies right to left."""
+
+    def __init__(self, Ml, A, Mr):
+        self.Ml, self.A, self.Mr = Ml, A, Mr
+        self.shape = A.shape
+
+    def __matmul__(self, x):
+        return _apply(self.Ml, self.A @ _apply(self.Mr, x))
+
+
 def _apply(op, x):
     """``op @ x``; the reference's Identity returns x itself (_helpers.py:26-36)."""
     return x if op is None else op @ x
@@ -152,13 +163,93 @@ def _trisolve_columns(R, y):
     return np.array(cols).T.reshape([k] + list(R.shape[2:]))
 
 
+class _House:
+    """householder.py:6-65 (real case): H x = alpha ||x|| e_1."""
+
+    def __init__(self, x):
+        v = x.copy()
+        gamma = v[0].copy()
+        v[0] = 1
+        sigma2 = np.dot(v[1:].conj(), v[1:]) if v.ndim == 1 else np.einsum("i...,i...->...", v[1:].conj(), v[1:])
+        xnorm = np.sqrt(np.abs(gamma) ** 2 + sigma2)
+        if sigma2 == 0:
+            beta = 0
+            xnorm = np.abs(gamma)
+            alpha = 1 if gamma == 0 else gamma / xnorm
+        else:
+            beta = 2
+            if gamma == 0:
+                v[0] = -np.sqrt(sigma2)
+                alpha = 1
+            else:
+                v[0] = gamma + gamma / np.abs(gamma) * xnorm
+                alpha = -gamma / np.abs(gamma)
+        self.v = v / np.sqrt(np.abs(v[0]) ** 2 + sigma2)
+        self.alpha = alpha
+        self.beta = beta
+        self.inner = default_inner(x.shape)
+
+    def __matmul__(self, x):
+        if self.beta == 0:
+            return x
+        return x - self.beta * self.v * self.inner(self.v, x)
+
+
+class _ArnoldiHouseholder:
+    """arnoldi.py:33-104."""
+
+    def __init__(self, A, v):
+        self.A = A
+        self.v = v
+        self.iter = 0
+        self.is_invariant = False
+        self.houses = [_House(v)]
+        vnorm = np.linalg.norm(v, 2)
+        self.V = [v / np.where(vnorm != 0.0, vnorm, 1.0)]
+
+    def __next__(self):
+        if self.is_invariant:
+            raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
+        k = self.iter
+        Av = self.A @ self.V[k]
+        for j in range(k + 1):
+            Av[j:] = self.houses[j] @ Av[j:]
+            Av[j] *= np.conj(self.houses[j].alpha)
+        N = self.v.shape[0]
+        if k < N - 1:
+            house = _House(Av[k + 1:])
+            self.houses.append(house)
+            Av[k + 1:] = (house @ Av[k + 1:]) * np.conj(house.alpha)
+            h = Av[: k + 2]
+            h[-1] = np.abs(h[-1])
+            if h[-1] <= 1.0e-14:
+                self.is_invariant = True
+                v = None
+            else:
+                vnew = np.zeros_like(self.v)
+                vnew[k + 1] = 1
+                for j in range(k + 1, -1, -1):
+                    vnew[j:] = self.houses[j] @ vnew[j:]
+                v = vnew * self.houses[-1].alpha
+                self.V.append(v)
+        else:
+            h = np.zeros([len(Av) + 1] + list(self.v.shape[1:]), Av.dtype)
+            h[:-1] = Av
+            self.is_invariant = True
+            v = None
+        self.iter += 1
+        return v, h
+
+
 def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None,
           Ml=None, Mr=None):
-    """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200)."""
+    """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200) or
+    Householder (arnoldi.py:33-104)."""
     b = np.asarray(b)
     assert A.shape[0] == A.shape[1] == b.shape[0]
-    assert ortho.startswith("mgs")
-    sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    house = ortho == "householder"
+    assert house or ortho.startswith("mgs")
+    sweeps = 1 if ortho in ("mgs", "householder") else int(ortho[3:])
     inner = default_inner(b.shape) if inner is None else inner
     maxiter = A.shape[0] if maxiter is None else maxiter
     x0 = np.zeros_like(b) if x0 is None else np.asarray(x0)
@@ -181,6 +272,10 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
     # ArnoldiMGS.__init__ with Mv = M_Ml_r0 (arnoldi.py:136-150): P = Ml r0, V = M Ml r0
     P = [Ml_r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
     V = [M_Ml_r0 / np.where(r0norm != 0.0, r0norm, 1.0)]
+    if house:  # ArnoldiHouseholder(Ml_A_Mr, Ml_r0) (gmres.py:158-161)
+        op = _Prod(Ml, A, Mr)
+        hh = _ArnoldiHouseholder(op, Ml_r0)
+        V = hh.V
     invariant = False
     steps = 0
     R = np.zeros([maxiter + 1, maxiter] + list(b.shape[1:]), dtype=r0.dtype)
@@ -214,6 +309,29 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
         # --- Arnoldi MGS step (arnoldi.py:167-200) ---
         if invariant:
             raise InvariantError("Krylov subspace was found to be invariant in the previous iteration.")
+        if house:
+            _, h = next(hh)
+            steps += 1
+            if hh.is_invariant:
+                invariant = True
+            # --- Givens QR update (gmres.py:206-221) ---
+            R[: k + 2, k] = h[: k + 2]
+            for i in range(k):
+                R[i : i + 2, k] = _rot(G[i], R[i : i + 2, k])
+            g, rr = givens(R[k : k + 2, k])
+            G.append(g)
+            R[k, k] = rr
+            R[k + 1, k] = 0.0
+            y[k : k + 2] = _rot(G[k], y[k : k + 2])
+            yk = y[: k + 1]
+            xk = None
+            rn = np.array(np.abs(y[k + 1]))
+            if callback is not None:
+                xk = solution(yk)
+                callback(xk, rn)
+            resnorms.append(rn[()])
+            k += 1
+            continue
         w = _apply(Ml, A @ _apply(Mr, V[steps]))  # Product(Ml, A, Mr)
         h = np.zeros([steps + 2] + list(b.shape[1:]), dtype=hdtype)
         for _ in range(sweeps):

@@ -18,7 +18,16 @@ def inputs():
     d = Pvar.diagonal()
     R = problems.random_nonsym(3000, seed=4)
     dr = R.diagonal()
+    # the reference's Householder test problem (tests/test_solvers.py:12-26) in real arithmetic
+    a = np.linspace(1.0, 2.0, 5)
+    a[-1] = 1e-3
+    small5 = np.diag(a)
+    small5[-1, 0] = 10.0
+    small5[0, -1] = -10.0
     return {
+        "small5": small5,
+        "diag10": np.diag(np.arange(1.0, 11.0)),
+        "b10": np.random.default_rng(9).standard_normal(10),
         "Pvar": Pvar,
         "Mj": sp.diags(1.0 / d).tocsr(),
         "S": sp.diags(1.0 / np.sqrt(d)).tocsr(),
@@ -44,6 +53,12 @@ CASES = [
     ("minres_M", "minres", "Pvar", "ones", dict(M="Mj", tol=1e-8)),
     ("minres_MlMr", "minres", "Pvar", "ones", dict(Ml="S", Mr="S", tol=1e-8)),
     ("minres_all", "minres", "Pvar", "ones", dict(M="Mj", Ml="S", Mr="S", tol=0.0, maxiter=40)),
+    # Householder Arnoldi (arnoldi.py:33-104)
+    ("gmres_hh", "gmres", "R", "ones", dict(ortho="householder", tol=0.0, maxiter=30)),
+    ("gmres_hh_MlMr", "gmres", "R", "ones", dict(ortho="householder", Ml="RMj", Mr="RMj", tol=0.0, maxiter=20)),
+    ("gmres_hh_small5", "gmres", "small5", "ones", dict(ortho="householder", tol=1e-12)),
+    ("gmres_hh_small5_nx1", "gmres", "small5", "ones_nx1", dict(ortho="householder", tol=1e-12)),
+    ("gmres_hh_diag10", "gmres", "diag10", "b10", dict(ortho="householder", tol=1e-15, atol=0.0)),
 ]
 
 
@@ -53,7 +68,12 @@ def build(case, q=None, wrap=None):
     q = inputs() if q is None else q
     prefix, solver, a, b, kw = case
     A = q[a]
-    bb = np.ones(A.shape[0]) if b == "ones" else q[b]
+    if b == "ones":
+        bb = np.ones(A.shape[0])
+    elif b == "ones_nx1":
+        bb = np.ones((A.shape[0], 1))
+    else:
+        bb = q[b]
     out = {}
     for key, val in kw.items():
         if key in ("M", "Ml", "Mr"):

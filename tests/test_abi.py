@@ -148,5 +148,7 @@ def test_unsupported_inputs_are_rejected_before_any_device_work():
         krylov_amd.cg(np.eye(3), np.ones(3), M=lambda x: x)  # host callbacks cannot run on the device
     with pytest.raises(TypeError):
         krylov_amd.cg(np.eye(3), np.ones(3, dtype=complex))
-    with pytest.raises(NotImplementedError):
-        krylov_amd.gmres(np.eye(3), np.ones(3), ortho="householder")
+    with pytest.raises(AssertionError):  # as the reference (gmres.py:159-161)
+        krylov_amd.gmres(np.eye(3), np.ones((3, 2)), ortho="householder")
+    with pytest.raises(ValueError):
+        krylov_amd.gmres(np.eye(3), np.ones(3), ortho="cgs")
