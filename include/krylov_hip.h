@@ -105,6 +105,17 @@ int kry_spmv(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y);
 int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out);
 /* y = alpha[c] * x + y  (the reference's `y += alpha * x`, e.g. cg.py:196). */
 int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y);
+/* z = one of the reference's vector expressions, per column c (k <= 64),
+ * evaluated exactly as its NumPy expression tree; stream-ordered (no sync):
+ *   form 0: z = x + a[c] * y             (x += alpha * p, bicgstab.py:120)
+ *   form 1: z = x + a[c] * (y + b[c] * w)  (cgs.py:88)
+ *   form 2: z = x + a[c] * (y - b[c] * w)  (bicgstab.py:109)
+ *   form 3: z = x / a[c]   form 4: z = x - y   form 5: z = x + y
+ *   form 6: z = x          form 7: z = a[c] * x
+ * z may alias x, y or w. Replaces the AXPY-type lines of the host-driven
+ * solvers (bicgstab.py, cgs.py, cgr.py, gcr.py; krylov_amd/extra.py). */
+int kry_vec_lincomb(kry_ctx *ctx, int form, kry_vec *z, kry_vec *x, kry_vec *y, kry_vec *w,
+                    const double *a, const double *b);
 /* Batched LAPACK >= 3.10 ?lartg on device (givens.py:35-40); host arrays of
  * `count` values of `dtype`. Bitwise equal to scipy.linalg.lapack ?lartg. */
 int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void *g,

@@ -1,5 +1,6 @@
 """krylov_amd — MI355X-native inner loop for the Krylov solvers of
-``ju-liu/krylov`` (cg / gmres / minres with the reference call signatures).
+``ju-liu/krylov`` (cg / gmres / minres with the reference call signatures;
+bicgstab / cgs / cgr / gcr as host-driven loops over the same device kernels).
 
 The per-iteration work (CSR SpMV, AXPY/scale updates, inner products and
 norms, GMRES modified Gram-Schmidt + Givens, the MINRES Lanczos/QR
@@ -10,6 +11,7 @@ fallback: importing this package without the built library raises.
 from ._helpers import Identity, Info, WeightedInner, aslinearoperator, get_default_inner
 from .cg import cg
 from .errors import ArgumentError
+from .extra import bicgstab, cgr, cgs, gcr
 from .givens import givens, lartg
 from .gmres import gmres, gmres_restarted
 from .minres import minres
@@ -22,6 +24,10 @@ __all__ = [
     "gmres",
     "gmres_restarted",
     "minres",
+    "bicgstab",
+    "cgs",
+    "cgr",
+    "gcr",
     "givens",
     "lartg",
     "CsrOperator",

@@ -71,6 +71,7 @@ _SIGNATURES = {
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
     "kry_cg_scalars": [_vp, _dp],
+    "kry_vec_lincomb": [_vp, _int, _vp, _vp, _vp, _vp, _dp, _dp],
     "kry_cg_set_preconditioners": [_vp, _vp, _vp],
     "kry_gmres_set_preconditioners": [_vp, _vp, _vp, _vp],
     "kry_minres_set_preconditioners": [_vp, _vp, _vp, _vp],

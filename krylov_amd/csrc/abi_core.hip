@@ -28,6 +28,18 @@ void dev_free(void *p) {
   if (p) (void)hipFree(p);
 }
 
+double *ctx_scratch(kry_ctx *ctx, size_t bytes) {
+  if (ctx->scratch_bytes < bytes) {
+    KRY_HIP(hipStreamSynchronize(ctx->stream));  // the old buffer may still be in use
+    dev_free(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    ctx->scratch = static_cast<double *>(dev_alloc(bytes));
+    ctx->scratch_bytes = bytes;
+  }
+  return ctx->scratch;
+}
+
 ProfScope::ProfScope(kry_ctx *c, int kernel_id) : ctx(c), id(kernel_id) {
   if (!ctx->profile) return;
   if (ctx->ev_used == ctx->ev_pool.size()) {
@@ -210,6 +222,7 @@ int kry_ctx_destroy(kry_ctx *ctx) {
   }
   (void)hipEventDestroy(ctx->t0);
   (void)hipEventDestroy(ctx->t1);
+  dev_free(ctx->scratch);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   KRY_API_END
@@ -581,7 +594,7 @@ int kry_spmv(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y) {
     launch_spmv<V, MV, I>(A, k, SrcPlain<V>{static_cast<const V *>(x->d), k},
                       EpiStore<V>{static_cast<V *>(y->d), k}, nullptr, nullptr, nullptr, 0, ctx->stream);
   });
-  KRY_HIP(hipStreamSynchronize(ctx->stream));
+  KRY_HIP(hipGetLastError());  // stream-ordered: a download or reduction of y waits for it
   KRY_API_END
 }
 
@@ -595,8 +608,8 @@ int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out) {
   KRY_HIP(hipSetDevice(ctx->device));
   const int k = x->k;
   const int64_t N = x->n * (int64_t)k;
-  double *part = static_cast<double *>(dev_alloc((kMaxGrid + 1) * (size_t)k * 8));
-  try {
+  double *part = ctx_scratch(ctx, (kMaxGrid + 1) * (size_t)k * 8);
+  {
     int P;
     const double *wd = w ? static_cast<const double *>(w->d) : nullptr;
     if (x->dtype == KRY_F64)
@@ -610,11 +623,7 @@ int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out) {
     KRY_HIP(hipGetLastError());
     KRY_HIP(hipMemcpyAsync(out, res, k * 8, hipMemcpyDeviceToHost, ctx->stream));
     KRY_HIP(hipStreamSynchronize(ctx->stream));
-  } catch (...) {
-    dev_free(part);
-    throw;
   }
-  dev_free(part);
   KRY_API_END
 }
 

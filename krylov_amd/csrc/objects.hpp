@@ -19,6 +19,9 @@ struct kry_ctx {
   int64_t prof_count[4] = {0, 0, 0, 0};
   double prof_ms[4] = {0, 0, 0, 0};
   std::vector<int> ev_ids;
+  // scratch for one-shot reductions and scalar staging (blas.hip, kry_dot)
+  double *scratch = nullptr;
+  size_t scratch_bytes = 0;
 };
 
 struct kry_csr {
@@ -71,6 +74,7 @@ inline size_t isize(int itype) { return itype == KRY_I64 ? 8 : 4; }
 
 void *dev_alloc(size_t bytes);
 void dev_free(void *p);
+double *ctx_scratch(kry_ctx *ctx, size_t bytes);  // grown on demand, owned by the context
 
 // Event-timed launch bracket used by the solvers around their SpMV launches.
 struct ProfScope {

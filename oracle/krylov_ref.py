@@ -477,3 +477,223 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
         xk = x0 + _apply(Mr, yk)
     ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 4 + 8 * k}
     return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)
+
+
+# --------------------------------------------------------------------------
+# The reference's other Krylov solvers, restated.
+
+
+def _start_xr(A, b, x0, copy_x0):
+    if x0 is None:
+        return np.zeros_like(b), b.copy()
+    x = np.array(x0) if copy_x0 else np.asarray(x0)
+    return x, b - A @ x
+
+
+def bicgstab(A, b, Ml=None, Mr=None, x0=None, inner=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates bicgstab.py:24-144 (including the mid-step test on the
+    explicit residual of x, bicgstab.py:123-127)."""
+    b = np.asarray(b)
+    inner = default_inner(b.shape) if inner is None else inner
+
+    def _norm(x):
+        return np.sqrt(_real_norm2(inner(x, _apply(Ml, x))))
+
+    x, r0 = _start_xr(A, b, x0, copy_x0=False)
+    r0_ = r0
+    r = r0.copy()
+    if callback is not None:
+        callback(x, r)
+    resnorms = [_norm(r0)]
+    rho = 1.0
+    alpha = 1.0
+    omega = 1.0
+    p = np.zeros_like(b)
+    v = np.zeros_like(b)
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            resnorms[-1] = _norm(b - A @ x)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        rho_old = rho
+        rho = inner(r0_, r)
+        rho_old_omega = rho_old * omega
+        beta = rho * alpha / np.where(rho_old_omega != 0.0, rho_old_omega, 1.0)
+        p = r + beta * (p - omega * v)
+        y = _apply(Mr, _apply(Ml, p))
+        v = A @ y
+        r0v = inner(r0_, v)
+        alpha = rho / np.where(r0v != 0.0, r0v, 1.0)
+        s = r - alpha * v
+        h = x + alpha * y
+        resnorm_h = _norm(_apply(Ml, b - A @ x))
+        if np.all(resnorm_h <= criterion):
+            resnorms[-1] = resnorm_h
+            success = True
+            break
+        Ml_s = _apply(Ml, s)
+        z = _apply(Mr, Ml_s)
+        t = A @ z
+        Ml_t = _apply(Ml, t)
+        tt = inner(Ml_t, Ml_t)
+        omega = inner(Ml_t, Ml_s) / np.where(tt != 0.0, tt, 1.0)
+        x = h + omega * z
+        r = s - omega * t
+        if callback is not None:
+            callback(x, r)
+        resnorms.append(_norm(r))
+        k += 1
+    return x if success else None, Info(success, x, k, resnorms)
+
+
+def cgs(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates cgs.py:24-117."""
+    b = np.asarray(b)
+    inner = default_inner(b.shape) if inner is None else inner
+
+    def _norm(x):
+        return np.sqrt(_real_norm2(inner(x, _apply(M, x))))
+
+    x, r0 = _start_xr(A, b, x0, copy_x0=True)
+    rp = r0
+    r = r0.copy()
+    if callback:
+        callback(x, r)
+    resnorms = [_norm(r)]
+    rho = 1.0
+    p = np.zeros_like(b)
+    q = np.zeros_like(b)
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            resnorms[-1] = _norm(b - A @ x)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        rho_old = rho
+        rho = inner(rp, r)
+        beta = rho / np.where(rho_old != 0.0, rho_old, 1.0)
+        u = r + beta * q
+        p = u + beta * (q + beta * p)
+        v = A @ _apply(M, p)
+        s = inner(rp, v)
+        alpha = rho / np.where(s != 0.0, s, 1.0)
+        q = u - alpha * v
+        u_ = _apply(M, u + q)
+        x += alpha * u_
+        r -= alpha * (A @ u_)
+        if callback:
+            callback(x, r)
+        resnorms.append(_norm(r))
+        k += 1
+    return x if success else None, Info(success, x, k, resnorms)
+
+
+def cgr(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates cgr.py:16-100."""
+    b = np.asarray(b)
+    if x0 is None:
+        x = np.zeros_like(b)
+        r = b.copy()
+    else:
+        x = np.array(x0)
+        r = b - A @ x0
+    r = _apply(M, r)
+    inner = default_inner(b.shape) if inner is None else inner
+
+    def _norm(x):
+        return np.sqrt(_real_norm2(inner(x, x)))
+
+    Ar = A @ r
+    rAr = inner(r, Ar)
+    resnorms = [_norm(r)]
+    if callback is not None:
+        callback(x, r)
+    p = r.copy()
+    Ap = Ar.copy()
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            resnorms[-1] = _norm(b - A @ x)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        MAp = _apply(M, Ap)
+        ApMAp = inner(Ap, MAp)
+        alpha = rAr / np.where(ApMAp != 0.0, ApMAp, 1.0)
+        x += alpha * p
+        r -= alpha * MAp
+        Ar = A @ r
+        rAr_old = rAr
+        rAr = inner(r, Ar)
+        beta = rAr / np.where(rAr_old != 0.0, rAr_old, 1.0)
+        p = r + beta * p
+        Ap = Ar + beta * Ap
+        if callback is not None:
+            callback(x, r)
+        resnorms.append(_norm(r))
+        k += 1
+    return x if success else None, Info(success, x, k, resnorms)
+
+
+def gcr(A, b, x0=None, inner=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None):
+    """Restates gcr.py:18-97."""
+    b = np.asarray(b)
+    if x0 is None:
+        x = np.zeros_like(b)
+        r = b.copy()
+    else:
+        x = np.array(x0)
+        r = b - A @ x0
+    inner = default_inner(b.shape) if inner is None else inner
+
+    def _norm(x):
+        return np.sqrt(_real_norm2(inner(x, x)))
+
+    if callback is not None:
+        callback(x, r)
+    resnorms = [_norm(r)]
+    s = []
+    v = []
+    k = 0
+    success = False
+    criterion = np.maximum(tol * resnorms[0], atol)
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            resnorms[-1] = _norm(b - A @ x)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        s.append(r.copy())
+        v.append(A @ s[-1])
+        for i in range(k):
+            alpha = inner(v[-1], v[i])
+            v[-1] -= alpha * v[i]
+            s[-1] -= alpha * s[i]
+        beta = _norm(v[-1])
+        v[-1] /= np.where(beta != 0.0, beta, 1.0)
+        s[-1] /= np.where(beta != 0.0, beta, 1.0)
+        gamma = inner(b, v[-1])
+        x += gamma * s[-1]
+        r -= gamma * v[-1]
+        if callback is not None:
+            callback(x, r)
+        resnorms.append(_norm(r))
+        k += 1
+    return x if success else None, Info(success, x, k, resnorms)

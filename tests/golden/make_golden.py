@@ -130,7 +130,10 @@ def _info_arrays(prefix, sol, info, out):
     out[f"{prefix}_xk"] = np.asarray(info.xk)
     out[f"{prefix}_sol_is_none"] = np.array(sol is None)
     ops = info.num_operations
-    out[f"{prefix}_ops"] = np.array([ops[k] for k in ("A", "M", "Ml", "Mr", "inner", "axpy")], dtype=np.float64)
+    if ops is None:  # bicgstab / cgs / cgr / gcr report none
+        out[f"{prefix}_ops"] = np.full(6, np.nan)
+    else:
+        out[f"{prefix}_ops"] = np.array([ops[k] for k in ("A", "M", "Ml", "Mr", "inner", "axpy")], dtype=np.float64)
 
 
 def make_solvers(krylov):
@@ -222,13 +225,13 @@ def make_solvers(krylov):
 
 
 def make_precond(krylov):
-    from tests import precond_cases
+    from tests import solver_cases
 
     out = {}
     quiet = contextlib.redirect_stdout(io.StringIO())
-    q = precond_cases.inputs()
-    for case in precond_cases.CASES:
-        solver, A, b, kw = precond_cases.build(case, q)
+    q = solver_cases.inputs()
+    for case in solver_cases.CASES:
+        solver, A, b, kw = solver_cases.build(case, q)
         with quiet:
             sol, info = getattr(krylov, solver)(A, b, **kw)
         _info_arrays(case[0], sol, info, out)

@@ -1,4 +1,5 @@
-"""Preconditioned solver cases shared by the fixture generator
+"""Solver cases (preconditioners M/Ml/Mr, Householder Arnoldi, and the other
+solvers bicgstab/cgs/cgr/gcr) shared by the fixture generator
 (tests/golden/make_golden.py -> tests/golden/precond.npz), the oracle tests
 and the GPU parity tests. Inputs are rebuilt identically from seeds."""
 import numpy as np
@@ -25,6 +26,7 @@ def inputs():
     small5[-1, 0] = 10.0
     small5[0, -1] = -10.0
     return {
+        "x0R": np.random.default_rng(10).standard_normal(R.shape[0]),
         "small5": small5,
         "diag10": np.diag(np.arange(1.0, 11.0)),
         "b10": np.random.default_rng(9).standard_normal(10),
@@ -59,6 +61,19 @@ CASES = [
     ("gmres_hh_small5", "gmres", "small5", "ones", dict(ortho="householder", tol=1e-12)),
     ("gmres_hh_small5_nx1", "gmres", "small5", "ones_nx1", dict(ortho="householder", tol=1e-12)),
     ("gmres_hh_diag10", "gmres", "diag10", "b10", dict(ortho="householder", tol=1e-15, atol=0.0)),
+    # the other solvers (bicgstab.py, cgs.py, cgr.py, gcr.py)
+    ("bicgstab_R", "bicgstab", "R", "ones", dict(tol=0.0, maxiter=20)),
+    ("bicgstab_R_MlMr", "bicgstab", "R", "ones", dict(Ml="RMj", Mr="RMj", tol=0.0, maxiter=15)),
+    ("bicgstab_Pvar", "bicgstab", "Pvar", "ones", dict(tol=1e-8)),
+    ("bicgstab_R_x0", "bicgstab", "R", "ones", dict(x0="x0R", tol=0.0, maxiter=10)),
+    ("cgs_R", "cgs", "R", "ones", dict(tol=0.0, maxiter=12)),
+    ("cgs_Pvar_M", "cgs", "Pvar", "ones", dict(M="Mj", tol=1e-8)),
+    ("cgr_Pvar", "cgr", "Pvar", "ones", dict(tol=1e-8)),
+    ("cgr_Pvar_M", "cgr", "Pvar", "ones", dict(M="Mj", tol=1e-8)),
+    ("cgr_Pvar_blk3", "cgr", "Pvar", "B3", dict(tol=1e-8)),
+    ("gcr_R", "gcr", "R", "ones", dict(tol=0.0, maxiter=25)),
+    ("gcr_Pvar_blk3", "gcr", "Pvar", "B3", dict(tol=1e-8)),
+    ("gcr_R_x0", "gcr", "R", "ones", dict(x0="x0R", tol=0.0, maxiter=10)),
 ]
 
 
@@ -78,5 +93,7 @@ def build(case, q=None, wrap=None):
     for key, val in kw.items():
         if key in ("M", "Ml", "Mr"):
             val = q[val] if wrap is None else wrap(q[val])
+        elif key == "x0":
+            val = q[val]
         out[key] = val
     return solver, (A if wrap is None else wrap(A)), bb, out

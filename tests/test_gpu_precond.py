@@ -1,5 +1,5 @@
 """Preconditioned solves (M, Ml, Mr as device CSR operators) against the
-reference's own results (tests/golden/precond.npz, tests/precond_cases.py)
+reference's own results (tests/golden/precond.npz, tests/solver_cases.py)
 and the reference's preconditioner tests (tests/test_solvers.py:90-120)."""
 import os
 
@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from tests import gpu_helpers as H
-from tests import precond_cases
+from tests import solver_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -19,21 +19,25 @@ def fixtures():
     return np.load(os.path.join(HERE, "golden", "precond.npz"))
 
 
-@pytest.mark.parametrize("case", precond_cases.CASES, ids=lambda c: c[0])
+@pytest.mark.parametrize("case", solver_cases.CASES, ids=lambda c: c[0])
 def test_preconditioned_parity(fixtures, case):
     import krylov_amd
 
-    solver, A, b, kw = precond_cases.build(case)
+    solver, A, b, kw = solver_cases.build(case)
     _, info = getattr(krylov_amd, solver)(A, b, **kw)
-    H.assert_parity(info, fixtures, case[0])
+    # bicgstab / cgs / cgr / gcr form their residuals by cancellation
+    # (r = s - omega t, ...): their attainable relative accuracy at step k is
+    # ~eps ||r_0|| / ||r_k||, hence an absolute floor of 1e-14 ||r_0||
+    floor = 1e-14 if solver in ("bicgstab", "cgs", "cgr", "gcr") else 0.0
+    H.assert_parity(info, fixtures, case[0], floor=floor)
 
 
-@pytest.mark.parametrize("case", precond_cases.CASES[:4], ids=lambda c: c[0])
+@pytest.mark.parametrize("case", solver_cases.CASES[:4], ids=lambda c: c[0])
 def test_preconditioners_as_device_operators(fixtures, case):
     """The same with every operator uploaded once as a CsrOperator."""
     import krylov_amd
 
-    solver, A, b, kw = precond_cases.build(case, wrap=krylov_amd.CsrOperator)
+    solver, A, b, kw = solver_cases.build(case, wrap=krylov_amd.CsrOperator)
     _, info = getattr(krylov_amd, solver)(A, b, **kw)
     H.assert_parity(info, fixtures, case[0])
 
@@ -78,7 +82,7 @@ def test_preconditioned_matches_oracle_block_and_callback():
     import krylov_amd
     from oracle import krylov_ref as K
 
-    q = precond_cases.inputs()
+    q = solver_cases.inputs()
     A, B, Mj, S = q["Pvar"], q["B3"], q["Mj"], q["S"]
     seen = []
     _, got = krylov_amd.cg(A, B, M=Mj, Ml=S, tol=0.0, maxiter=15, callback=lambda x, r: seen.append(r.copy()))
