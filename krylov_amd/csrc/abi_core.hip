@@ -414,6 +414,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
   sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
+  A->max_width = 0;
+  for (int32_t w : width) A->max_width = std::max(A->max_width, w);
   std::vector<I> sidx;
   std::vector<MV> sval;
   sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);

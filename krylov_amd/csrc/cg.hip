@@ -4,13 +4,18 @@
 // update's <r, r> partials are replaced by z = M r with <r, z> (cg.py:207-209)
 // and the p pass reads z.
 //
-// One iteration = five launches on the context stream, no host sync:
+// One iteration (no M, k <= 8) = four launches on the context stream, no
+// host sync:
 //   1. SpMV   Ap = A p, partial <p, Ap>                 cg.py:180-183
 //   2. tiny   alpha = rho / guard(<p, Ap>)              cg.py:185
-//   3. update y += alpha p, r -= alpha Ap, partial <r, r>   cg.py:196-209
-//   4. tiny   rho shift, omega, resnorm = sqrt(rho) -> history, stop test
-//             np.all(resnorm <= criterion) -> ctrl.stop_at  cg.py:156,214-217
-//   5. p pass p = r + omega p for the next iteration    cg.py:175-178
+//   3. r pass r -= alpha Ap, partial <r, r>             cg.py:200-209
+//   4. yp     every block finishes <r, r> itself: omega; y += alpha p and
+//             p = r + omega p for the next iteration; block 0 shifts rho,
+//             writes resnorm = sqrt(rho) to the history and the stop test
+//             np.all(resnorm <= criterion) -> ctrl.stop_at
+//                                                       cg.py:156,175-178,196,214-217
+// With M (or k > 8) steps 3-4 are the update pass (y and r), z = M r, a
+// one-block rho kernel and a p pass.
 // (+ with an attached communicator: one ncclAllReduce of the zero-padded
 //  residual-norm vector and a tiny global stop test.)
 // The p update is its own streaming pass (not folded into the SpMV's gather):
@@ -48,7 +53,9 @@ struct kry_cg {
 
 namespace {
 
-enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_COUNT = 6 };
+enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_RHO_OLD = 6, S_COUNT = 7 };
+
+constexpr int kCgUpdateGrid = 1024;  // update-pass blocks: the <r, r> partials every yp block re-reduces
 
 template <typename V>
 struct OpCgUpdate {
@@ -78,6 +85,34 @@ struct OpCgUpdate {
     }
     VIO<V>::store_nt(y, e, N, yv);
     VIO<V>::store(r, e, N, rv);  // r and p are the next SpMV's gather sources
+  }
+};
+
+// Ml_rk -= alpha * Ap (cg.py:200) with <r, r> partials (cg.py:209); the y
+// update moves to the yp pass, which reads p anyway.
+template <typename V>
+struct OpCgR {
+  V *r;
+  const V *Ap;
+  const double *alpha;
+  const double *w;
+  int k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V rv[W], av[W];
+    VIO<V>::load(r, e, N, rv);
+    VIO<V>::load_nt(Ap, e, N, av);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const V a = (V)alpha[(e + v) & (k - 1)];
+      const V t2 = a * av[v];
+      rv[v] = rv[v] - t2;
+      if (e + v < N) {
+        const double rd = (double)rv[v];
+        acc[v] += w ? dterm_w(rd, w[(e + v) / k], rd) : dterm(rd, rd);
+      }
+    }
+    VIO<V>::store(r, e, N, rv);
   }
 };
 
@@ -129,6 +164,7 @@ __global__ void cg_alpha_kernel(const double *part, int P, int k, double *scal, 
     const S pAp = (S)red[c];
     const S rho = (S)scal[S_RHO * k + c];
     scal[S_ALPHA * k + c] = (double)(rho / safe<S>(pAp));
+    scal[S_RHO_OLD * k + c] = (double)rho;  // stable copy for the yp pass (S_RHO is rewritten there)
   }
 }
 
@@ -177,6 +213,75 @@ __global__ void cg_global_check(const double *gbuf, const double *gcrit, int tot
 // Ml r and M Ml r with <Ml r, M Ml r> partials for r = b - A src
 // (cg.py:70-90); returns the partial count. Leaves Ml r in `mlr` and M Ml r in
 // `z` (when M is set).
+// Steps 4-5 fused (no preconditioner): every block finishes <r, r> from the
+// update pass's partials in the same fixed order, derives omega, and applies
+// yk += alpha p (cg.py:196) and p = r + omega p (cg.py:178) to its span; block
+// 0 also shifts rho, writes the history and the stop word (cg.py:156,
+// 209-217). Saves the one-block rho launch and one pass over p.
+template <typename V, typename S>
+__global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__restrict__ y, V *__restrict__ p,
+                                                       const V *__restrict__ r, const double *__restrict__ part,
+                                                       int P, double *scal, double *hist, Ctrl *ctrl, int step,
+                                                       double *gbuf, int col_offset, int total_k) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  __shared__ double red[kBlock];
+  __shared__ double sh_a[kMaxCols], sh_om[kMaxCols], rn[kMaxCols];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  reduce_partials(part, P, k, red);
+  if (tid < k) {
+    const S rr = (S)red[tid];
+    const S old = (S)scal[S_RHO_OLD * k + tid];
+    const S om = rr / safe<S>(old);
+    sh_om[tid] = (double)om;
+    sh_a[tid] = scal[S_ALPHA * k + tid];
+    const S nrm = sqrt(rr);
+    rn[tid] = (double)nrm;
+    if (g == 0) {
+      scal[S_RHO_PREV * k + tid] = (double)old;
+      scal[S_RHO * k + tid] = (double)rr;
+      scal[S_OMEGA * k + tid] = (double)om;
+      if (!gbuf) hist[(int64_t)step * k + tid] = (double)nrm;
+    }
+  }
+  __syncthreads();
+  const int64_t ngrp = (N + W - 1) / W;
+  const int64_t per = ((ngrp + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+  const int64_t v0 = per * g;
+  const int64_t v1 = v0 + per < ngrp ? v0 + per : ngrp;
+  for (int64_t gi = v0 + tid; gi < v1; gi += kBlock) {
+    const int64_t e = gi * W;
+    V yv[W], pv[W], rv[W];
+    VIO<V>::load_nt(y, e, N, yv);
+    VIO<V>::load(p, e, N, pv);
+    VIO<V>::load(r, e, N, rv);
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      const int c = (int)((e + u) & (k - 1));
+      const V a = (V)sh_a[c];
+      const V t1 = a * pv[u];
+      yv[u] = yv[u] + t1;
+      const V om = (V)sh_om[c];
+      const V t = om * pv[u];
+      pv[u] = rv[u] + t;
+    }
+    VIO<V>::store_nt(y, e, N, yv);
+    VIO<V>::store(p, e, N, pv);
+  }
+  if (g == 0) {
+    if (gbuf) {
+      for (int t = tid; t < total_k; t += kBlock) {
+        const int lc = t - col_offset;
+        gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
+      }
+    } else if (all_le(rn, scal + S_CRIT * k, k, &flag) && tid == 0) {
+      ctrl->stop_at = step + 1;
+    }
+  }
+}
+
 template <typename V, typename MV, typename I>
 int cg_residual_chain(kry_cg *s, const V *src, V *raw, V *mlr) {
   hipStream_t st = s->ctx->stream;
@@ -242,30 +347,52 @@ void cg_run_impl(kry_cg *s, int max_steps) {
       hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
     else
       hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
-    {
-      ProfScope ps(s->ctx, PROF_UPDATE);
-      PB = launch_elementwise<V>(N, k,
-                                 OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), p,
-                                               static_cast<const V *>(s->Ap), s->scal + S_ALPHA * k, s->w, k},
-                                 s->M ? nullptr : partB, s->ctrl, step, st);
-    }
-    if (s->M) {  // M_Ml_rk = M Ml_rk and <Ml_rk, M_Ml_rk> (cg.py:207-209)
-      V *r = static_cast<V *>(s->r);
-      launch_spmv_any<V>(s->M, k, SrcPlain<V>{r, k}, EpiStoreDot<V>{static_cast<V *>(s->z), r, s->w, k}, partB, &PB,
-                         s->ctrl, step, st);
-    }
     double *gb = s->comm ? s->gbuf : nullptr;
-    if (s->scalar_f32)
-      hipLaunchKernelGGL(cg_rho_kernel<float>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
-                         s->ctrl, step, gb, s->col_offset, s->total_k);
-    else
-      hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
-                         s->ctrl, step, gb, s->col_offset, s->total_k);
-    KRY_HIP(hipGetLastError());
-    {
+    if (!s->M && k <= 8) {  // r pass, then the fused rho / y / p pass
+      {
+        ProfScope ps(s->ctx, PROF_UPDATE);
+        PB = launch_elementwise<V>(N, k,
+                                   OpCgR<V>{static_cast<V *>(s->r), static_cast<const V *>(s->Ap),
+                                            s->scal + S_ALPHA * k, s->w, k},
+                                   partB, s->ctrl, step, st, kCgUpdateGrid);
+      }
       ProfScope ps(s->ctx, PROF_OTHER);
-      const V *zv = static_cast<const V *>(s->M ? s->z : s->r);
-      launch_elementwise<V>(N, k, OpCgP<V>{p, zv, s->scal + S_OMEGA * k, k}, nullptr, s->ctrl, step, st);
+      constexpr int W = Vec16<V>::W;
+      const int G = grid_for((N + W - 1) / W, kBlock * 2);
+      if (s->scalar_f32)
+        hipLaunchKernelGGL((cg_yp_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
+                           static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
+                           s->col_offset, s->total_k);
+      else
+        hipLaunchKernelGGL((cg_yp_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
+                           static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
+                           s->col_offset, s->total_k);
+      KRY_HIP(hipGetLastError());
+    } else {  // update pass, [z = M r], one-block rho kernel, p pass
+      {
+        ProfScope ps(s->ctx, PROF_UPDATE);
+        PB = launch_elementwise<V>(N, k,
+                                   OpCgUpdate<V>{static_cast<V *>(s->y), static_cast<V *>(s->r), p,
+                                                 static_cast<const V *>(s->Ap), s->scal + S_ALPHA * k, s->w, k},
+                                   s->M ? nullptr : partB, s->ctrl, step, st);
+      }
+      if (s->M) {  // M_Ml_rk = M Ml_rk and <Ml_rk, M_Ml_rk> (cg.py:207-209)
+        V *r = static_cast<V *>(s->r);
+        launch_spmv_any<V>(s->M, k, SrcPlain<V>{r, k}, EpiStoreDot<V>{static_cast<V *>(s->z), r, s->w, k}, partB,
+                           &PB, s->ctrl, step, st);
+      }
+      if (s->scalar_f32)
+        hipLaunchKernelGGL(cg_rho_kernel<float>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
+                           s->ctrl, step, gb, s->col_offset, s->total_k);
+      else
+        hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
+                           s->ctrl, step, gb, s->col_offset, s->total_k);
+      KRY_HIP(hipGetLastError());
+      {
+        ProfScope ps(s->ctx, PROF_OTHER);
+        const V *zv = static_cast<const V *>(s->M ? s->z : s->r);
+        launch_elementwise<V>(N, k, OpCgP<V>{p, zv, s->scal + S_OMEGA * k, k}, nullptr, s->ctrl, step, st);
+      }
     }
     if (s->comm) {
       // exactly one collective per iteration: the residual-norm vector

@@ -717,7 +717,10 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
     return;
   }
   switch (k) {
-    case 1: grid = launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st); break;
+    case 1:  // one pass over a slice's slot columns when they all fit the unroll
+      grid = A->max_width <= 8 ? launch_sell<V, MV, I, 1, 8>(A, k, src, epi, part, ctrl, step, st)
+                               : launch_sell<V, MV, I, 1, 16>(A, k, src, epi, part, ctrl, step, st);
+      break;
     case 2: grid = launch_sell<V, MV, I, 2, 8>(A, k, src, epi, part, ctrl, step, st); break;
     case 4: grid = launch_sell<V, MV, I, 4, 4>(A, k, src, epi, part, ctrl, step, st); break;
     default: grid = launch_sell<V, MV, I, 8, 4>(A, k, src, epi, part, ctrl, step, st); break;
@@ -744,9 +747,10 @@ void launch_spmv_any(const kry_csr *Op, int k, Src src, Epi epi, double *part, i
 
 template <typename V, class Op>
 int launch_elementwise(int64_t N, int k, Op op, double *part, const Ctrl *ctrl, int step,
-                       hipStream_t st) {
+                       hipStream_t st, int max_grid = kMaxGrid) {
   constexpr int W = Vec16<V>::W;
-  const int grid = grid_for((N + W - 1) / W, kBlock * 2);
+  int grid = grid_for((N + W - 1) / W, kBlock * 2);
+  if (grid > max_grid) grid = max_grid;
   hipLaunchKernelGGL((elementwise_kernel<V, Op>), dim3(grid), dim3(kBlock), 0, st, N, k, op, part,
                      ctrl, step);
   KRY_HIP(hipGetLastError());

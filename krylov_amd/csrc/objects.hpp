@@ -30,6 +30,7 @@ struct kry_csr {
   int dtype = 0, itype = 0;
   // SELL-64 image (device): slice s covers rows [64 s, 64 s + 64)
   int64_t nslices = 0, nslots = 0, nirregular = 0;
+  int max_width = 0;        // widest regular slice (picks the SpMV unroll)
   void *sptr = nullptr;     // int64, nslices + 1 slot offsets
   void *swidth = nullptr;   // int32, slice width, -1 = irregular (CSR walk)
   void *sidx = nullptr;     // itype, nslots (+ pad), -1 = padding
