@@ -645,6 +645,84 @@ __global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t 
   }
 }
 
+// Single-launch form of the column-blocked SpMV: block `blk` owns groups
+// blk, blk + G, ... (at most kCbMaxOwn of them) and walks the column blocks
+// in order for all of them, keeping every row's running sum in a register, so
+// there is no cb_y traffic and one launch instead of cb_nb. Blocks never wait
+// for each other (no residency assumption); they stay roughly in step on the
+// column blocks because their work per block is similar, which is what keeps
+// the current x block L2-resident. Same per-row summation order => bitwise.
+constexpr int kCbMaxOwn = 16;
+constexpr int kCbPersistGrid = 1024;  // 4 blocks per CU: all resident, so they start together
+template <typename V, typename MV, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int64_t ng,
+                                                          const int64_t *__restrict__ gptr,
+                                                          const uint16_t *__restrict__ roff,
+                                                          const int *__restrict__ col, const MV *__restrict__ val,
+                                                          Src src, Epi epi, double *__restrict__ part,
+                                                          const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ V prod[kCbCap];
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const auto bs = src.template bind<1>(0);
+  V acc[kCbMaxOwn];
+#pragma unroll
+  for (int o = 0; o < kCbMaxOwn; ++o) acc[o] = V(0);
+  for (int b = 0; b < nb; ++b) {
+#pragma unroll
+    for (int o = 0; o < kCbMaxOwn; ++o) {
+      const int64_t g = (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
+      if (g >= ng) break;
+      const int64_t s0 = gptr[(int64_t)b * ng + g];
+      const int len = (int)(gptr[(int64_t)b * ng + g + 1] - s0);
+      const int64_t row = g * kCbRows + tid;
+      const bool has = row < n;
+      int r0 = 0, r1 = 0;
+      if (has) {
+        r0 = roff[(int64_t)b * n + row];
+        r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
+      }
+      for (int c0 = 0; c0 < len; c0 += kCbCap) {
+        const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
+        __syncthreads();
+        constexpr int U = kCbCap / kBlock;
+        int j[U];
+        V a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = c0 + tid + u * kBlock;
+          j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
+          a[u] = e < c1 ? (V)__builtin_nontemporal_load(val + s0 + e) : V(0);
+        }
+        V xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xj[u] = j[u] >= 0 ? bs(j[u], 0) : V(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (j[u] >= 0) prod[tid + u * kBlock] = a[u] * xj[u];
+        __syncthreads();
+        const int lo = r0 > c0 ? r0 : c0, hi = r1 < c1 ? r1 : c1;
+        for (int e = lo; e < hi; ++e) acc[o] = acc[o] + prod[e - c0];
+      }
+    }
+  }
+  double dacc = 0.0;
+#pragma unroll
+  for (int o = 0; o < kCbMaxOwn; ++o) {
+    const int64_t g = (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
+    if (g >= ng) break;
+    const int64_t row = g * kCbRows + tid;
+    if (row < n) dacc += epi(row, 0, acc[o], bs(row, 0));
+  }
+  if (part != nullptr) {
+    __syncthreads();
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[blockIdx.x] = red[0];
+  }
+}
+
 // -------------------------------------------------------- host launchers
 template <typename V, typename MV, typename I, int KT, int UNR, bool D16, class Src, class Epi>
 int launch_sell_img(const kry_csr *A, int k, Src src, Epi epi, double *part, const Ctrl *ctrl, int step,
@@ -682,7 +760,17 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
   if constexpr (sizeof(I) == 4) {
-    if (k == 1 && A->cb_nb > 0) {
+    if (k == 1 && A->cb_nb > 0 && A->cb_ng <= (int64_t)kCbPersistGrid * kCbMaxOwn) {
+      grid = (int)std::min<int64_t>(A->cb_ng, kCbPersistGrid);
+      hipLaunchKernelGGL((spmv_cbp_kernel<V, MV, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n,
+                         A->cb_ng, static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
+                         static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val), src, epi, part, ctrl,
+                         step);
+      KRY_HIP(hipGetLastError());
+      if (grid_out) *grid_out = grid;
+      return;
+    }
+    if (k == 1 && A->cb_nb > 0) {  // larger matrices: one launch per column block
       static const int cb_grid = [] {
         const char *e = getenv("KRY_CB_GRID");  // tuning override
         return e ? std::max(1, std::min(atoi(e), kMaxGrid)) : kMaxGrid;

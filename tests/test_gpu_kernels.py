@@ -156,6 +156,19 @@ def test_column_blocked_long_segments_and_empty_rows():
         np.testing.assert_array_equal(op @ x64, A @ x64)  # float32 matrix, float64 vector
 
 
+def test_column_blocked_multipass_for_large_n():
+    """Past 16 groups per persistent block (n > 4,194,304) the column-blocked
+    SpMV runs one launch per column block, with running sums in HBM."""
+    import krylov_amd
+
+    n = 4_300_001
+    A = _scattered_csr(n, np.full(n, 4), seed=13)
+    op = krylov_amd.CsrOperator(A)
+    assert op.layout()["col_blocks"] == 16
+    x = np.random.default_rng(6).standard_normal(n)
+    np.testing.assert_array_equal(op @ x, A @ x)
+
+
 def test_column_blocked_not_built_for_unsorted_rows():
     import krylov_amd
 

@@ -246,7 +246,8 @@ static int cb_tune(int64_t n, int reps) {
   double *d_x, *d_y;
   CK(hipMalloc(&d_x, n * 8));
   CK(hipMalloc(&d_y, n * 8));
-  std::vector<double> xh(n, 1.0);
+  std::vector<double> xh(n);
+  for (int64_t i = 0; i < n; ++i) xh[i] = 1.0 + 1e-3 * (double)((i * 2654435761u) % 1000);
   CK(hipMemcpy(d_x, xh.data(), n * 8, hipMemcpyHostToDevice));
   std::vector<int> ip(n + 1, 0), ix;
   std::vector<double> dv;
@@ -260,7 +261,7 @@ static int cb_tune(int64_t n, int reps) {
       row.push_back((int)(st % (uint64_t)n));
     }
     std::sort(row.begin(), row.end());
-    for (int c : row) { ix.push_back(c); dv.push_back(0.5); }
+    for (int c : row) { ix.push_back(c); dv.push_back(0.25 + 1e-3 * (double)(c % 997)); }
     ip[r + 1] = (int)ix.size();
   }
   const int64_t nnz = ix.size();
@@ -268,6 +269,22 @@ static int cb_tune(int64_t n, int reps) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  std::vector<double> yref(n);
+  for (int64_t r = 0; r < n; ++r) {
+    double sum = 0;
+    for (int e = ip[r]; e < ip[r + 1]; ++e) {
+      const double pr = dv[e] * xh[ix[e]];
+      sum = sum + pr;
+    }
+    yref[r] = sum;
+  }
+  auto verify = [&](const char *what) {
+    std::vector<double> h(n);
+    CK(hipMemcpy(h.data(), d_y, n * 8, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += memcmp(&h[i], &yref[i], 8) != 0;
+    printf("  %s: bitwise mismatches %ld\n", what, bad);
+  };
   for (const char *cols : {"131072", "262144", "524288"}) {
     setenv("KRY_CB_COLS", cols, 1);
     kry_csr *A;
@@ -295,6 +312,30 @@ static int cb_tune(int64_t n, int reps) {
       }
       printf("cb cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
              S / (tot / reps) / 1e6);
+    }
+    for (int grid : {1024, 1536, 2048}) {
+      if (A->cb_ng > (int64_t)grid * kCbMaxOwn) continue;
+      auto launch = [&] {
+        hipLaunchKernelGGL((spmv_cbp_kernel<double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
+                           dim3(kBlock), 0, 0, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr,
+                           (const uint16_t *)A->cb_roff, (const int *)A->cb_col, (const double *)A->cb_val,
+                           SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, (double *)nullptr, (const Ctrl *)nullptr, 0);
+      };
+      launch();
+      CK(hipDeviceSynchronize());
+      float tot = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+      }
+      printf("cb persistent cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
+             S / (tot / reps) / 1e6);
+      verify("persistent");
     }
     KC(kry_csr_destroy(A));
   }
