@@ -90,6 +90,33 @@ struct SrcCgP {
   }
 };
 
+// x = w / hsafe (GMRES: the next basis vector V_{k+1} = w / guard(h[k+1]),
+// arnoldi.py:191-196, formed on the fly at every gather of the next SpMV).
+template <typename V>
+struct SrcScaled {
+  const V *w;
+  const double *hs;
+  int k;
+  __device__ __forceinline__ V operator()(int64_t j, int c) const { return w[j * k + c] / (V)hs[c]; }
+  template <int KT>
+  struct Bound {
+    const V *w;
+    V h[KT];
+    int k, c0;
+    __device__ __forceinline__ V operator()(int64_t j, int c) const { return w[j * k + c0 + c] / h[c]; }
+  };
+  template <int KT>
+  __device__ __forceinline__ Bound<KT> bind(int c0) const {
+    Bound<KT> b;
+    b.w = w;
+    b.k = k;
+    b.c0 = c0;
+#pragma unroll
+    for (int c = 0; c < KT; ++c) b.h[c] = (V)hs[c0 + c];
+    return b;
+  }
+};
+
 // -------------------------------------------------------------- epilogues
 // store(row, c, sum) writes the SpMV result and returns this row/column's
 // contribution to the fused inner product (0 if the epilogue has none).
@@ -139,6 +166,23 @@ struct EpiAddStore {
   __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     out[i * k + c] = x0 ? x0[i * k + c] + s : s;
     return 0.0;
+  }
+};
+
+// EpiStoreDot that also stores the row's source value: with SrcScaled the
+// SpMV materialises V_{k+1} = w / guard(h[k+1]) while it multiplies by it.
+template <typename V>
+struct EpiStoreDotV {
+  V *y;
+  const V *q;
+  V *vout;
+  const double *w;
+  int k;
+  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
+    vout[i * k + c] = xi;
+    y[i * k + c] = s;
+    const double qv = (double)q[i * k + c];
+    return w ? dterm_w(qv, w[i], (double)s) : dterm(qv, (double)s);
   }
 };
 

@@ -34,6 +34,11 @@ struct kry_gmres {
   void *mw = nullptr;   // M w (with M)
   void *t1 = nullptr;   // Mr v / solution scratch (with Mr)
   void *t2 = nullptr;   // A Mr v / raw residual (with Ml)
+  // normalisation fused into the next SpMV (no preconditioners, MGS): w is
+  // double-buffered; vpending = V_steps is still w[wcur] / hsafe
+  void *wv2 = nullptr;
+  int wcur = 0;
+  bool vpending = false;
   // Householder Arnoldi (sweeps == 0, one right-hand side): reflector vectors
   // U_j (zero below j) and their scalars (householder.py:8-53)
   bool householder = false;
@@ -252,19 +257,20 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
   if (c < k) {
     const S hk1 = (S)red[c];
     scal[G_HSAFE * k + c] = (double)safe<S>(hk1);
-    // R[:col+2, col] = h[:col+2]
-    for (int i = 0; i < col + 2; ++i) R[i * ld + (int64_t)col * k + c] = h[(int64_t)i * k + c];
-    // apply the previous rotations
+    // R[:col+2, col] = h[:col+2], then the previous rotations (gmres.py:208-210).
+    // Rotation i finalises R[i] and hands R[i+1] on: carry it in a register
+    // so the chain is arithmetic only (same operations, same bits).
+    S carry = (S)h[c];
     for (int i = 0; i < col; ++i) {
       const S cc = (S)Gc[(int64_t)i * k + c], ss = (S)Gs[(int64_t)i * k + c];
-      const S r0 = (S)R[i * ld + (int64_t)col * k + c], r1 = (S)R[(i + 1) * ld + (int64_t)col * k + c];
+      const S r0 = carry, r1 = (S)h[(int64_t)(i + 1) * k + c];
       const S a0 = cc * r0, a1 = ss * r1;
       const S b0 = -ss * r0, b1 = cc * r1;
       R[i * ld + (int64_t)col * k + c] = (double)(a0 + a1);
-      R[(i + 1) * ld + (int64_t)col * k + c] = (double)(b0 + b1);
+      carry = b0 + b1;
     }
     S cs, sn, rr;
-    lartg<S>((S)R[col * ld + (int64_t)col * k + c], (S)R[(col + 1) * ld + (int64_t)col * k + c], cs, sn, rr);
+    lartg<S>(carry, (S)h[(int64_t)(col + 1) * k + c], cs, sn, rr);
     Gc[(int64_t)col * k + c] = (double)cs;
     Gs[(int64_t)col * k + c] = (double)sn;
     R[col * ld + (int64_t)col * k + c] = (double)rr;
@@ -674,16 +680,28 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
-  V *w = static_cast<V *>(s->wv);
+  V *wb[2] = {static_cast<V *>(s->wv), static_cast<V *>(s->wv2)};
+  const bool fuse_norm = !s->M && !s->Ml && !s->Mr;
   for (int step = 0; step < max_steps; ++step) {
     const int col = s->steps + step;
     if (col >= s->maxiter) break;
-    const V *Vk = basis<V>(s->V, s->vstride, col);
+    V *Vk = basis<V>(s->V, s->vstride, col);
     const V *V0 = basis<V>(s->V, s->vstride, 0);
     int P;
+    V *w;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
-      gm_apply_op<V, MV, I>(s, Vk, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step);
+      if (s->vpending) {  // V_k = w_prev / hsafe, formed in the gather and stored by the epilogue
+        const V *wprev = wb[s->wcur];
+        w = wb[s->wcur ^ 1];
+        launch_spmv<V, MV, I>(s->A, k, SrcScaled<V>{wprev, s->scal + G_HSAFE * k, k},
+                              EpiStoreDotV<V>{w, V0, Vk, s->w, k}, s->part, &P, s->ctrl, step, st);
+        s->wcur ^= 1;
+        s->vpending = false;
+      } else {
+        w = wb[s->wcur];
+        gm_apply_op<V, MV, I>(s, Vk, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step);
+      }
     }
     // the SpMV's partials of <V_0, w> -> one value per column, so every MGS
     // block reduces a single partial row for its first coefficient
@@ -727,6 +745,10 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     // P_{col+1} = w / guard(h[col+1]), V_{col+1} = M w / guard(h[col+1]) unless
     // invariant; these run for this step even when the QR kernel just raised
     // stop_at to step + 1 (arnoldi.py:191-196).
+    if (fuse_norm && col + 1 < s->maxiter) {
+      s->vpending = true;  // V_{col+1} is formed by the next step's SpMV
+      continue;
+    }
     if (s->M)
       launch_elementwise<V>(N, k, OpScaleDiv<V>{w, basis<V>(s->P, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
                             nullptr, s->ctrl, step, st);
@@ -782,7 +804,7 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 void gm_free(kry_gmres *s) {
   void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
                   s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2,
-                  s->U, s->vnew, s->hh};
+                  s->U, s->vnew, s->hh, s->wv2};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -826,6 +848,7 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     const size_t vb = s->vstride * dsize(dtype);
     s->b = dev_alloc(vb);
     s->wv = dev_alloc(vb);
+    s->wv2 = dev_alloc(vb);
     s->xk = dev_alloc(vb);
     s->rt = dev_alloc(vb);
     s->V = dev_alloc(vb * ((size_t)maxiter + 1));
@@ -837,6 +860,7 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     }
     KRY_HIP(hipMemsetAsync(s->xk, 0, vb, ctx->stream));
     KRY_HIP(hipMemsetAsync(s->wv, 0, vb, ctx->stream));
+    KRY_HIP(hipMemsetAsync(s->wv2, 0, vb, ctx->stream));
     s->part = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
     s->part1 = static_cast<double *>(dev_alloc((size_t)k * 8));
     s->part2 = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
@@ -936,6 +960,8 @@ int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r
   s->steps = 0;
   s->invariant = false;
   s->have_solution = false;
+  s->wcur = 0;
+  s->vpending = false;
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
   KRY_HIP(hipMemcpyAsync(r0norm, s->scal + G_TMP * k, k * 8, hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
