@@ -55,6 +55,12 @@ struct kry_gmres {
   double *yy = nullptr;    // maxiter x k triangular-solve result
   double *hist = nullptr;
   Ctrl *ctrl = nullptr;
+  // grid-barrier words of the persistent MGS kernel: 16 per chunk step,
+  // zeroed once per chunk (kry_gmres_run)
+  unsigned *bar = nullptr;
+  int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
+  int mgsp_grid = 0;
+  double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
   int chunk_cap = 0;
   int steps = 0;           // Arnoldi iterations done (arnoldi.iter)
   bool invariant = false;
@@ -88,28 +94,15 @@ __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__r
   __shared__ double red[kBlock * W];
   __shared__ double alpha[kMaxCols];
   const int tid = threadIdx.x;
-  reduce_partials(part_in, P_in, k, red);
-  if (tid < k) {
-    const V a = (V)red[tid];
-    alpha[tid] = (double)a;
-    if (blockIdx.x == 0) {
-      const V prev = first_sweep ? V(0) : (V)h[(int64_t)j * k + tid];
-      h[(int64_t)j * k + tid] = (double)(prev + a);
-    }
-  }
-  __syncthreads();
   const int g = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t ngrp = (N + W - 1) / W;
   const int64_t per = ((ngrp + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
   const int64_t v0 = per * g;
   const int64_t v1 = v0 + per < ngrp ? v0 + per : ngrp;
-  double acc[W];
-#pragma unroll
-  for (int v = 0; v < W; ++v) acc[v] = 0.0;
   // U chunks per thread per round, every load issued before any store
   constexpr int U = 4;
-  for (int64_t gb = v0 + tid; gb < v1; gb += U * kBlock) {
-    V wv[U][W], vj[U][W], qv[U][W];
+  V wv[U][W], vj[U][W], qv[U][W];
+  auto load_round = [&](int64_t gb) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t gi = gb + (int64_t)u * kBlock;
@@ -120,6 +113,25 @@ __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__r
         if (q) VIO<V>::load(q, e, N, qv[u]);
       }
     }
+  };
+  // the first round's vector loads do not depend on alpha_j: they are in
+  // flight while the previous pass's partials are read and reduced
+  int64_t gb = v0 + tid;
+  if (gb < v1) load_round(gb);
+  reduce_partials(part_in, P_in, k, red);
+  if (tid < k) {
+    const V a = (V)red[tid];
+    alpha[tid] = (double)a;
+    if (blockIdx.x == 0) {
+      const V prev = first_sweep ? V(0) : (V)h[(int64_t)j * k + tid];
+      h[(int64_t)j * k + tid] = (double)(prev + a);
+    }
+  }
+  __syncthreads();
+  double acc[W];
+#pragma unroll
+  for (int v = 0; v < W; ++v) acc[v] = 0.0;
+  for (; gb < v1; gb += U * kBlock) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t gi = gb + (int64_t)u * kBlock;
@@ -138,12 +150,238 @@ __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__r
         VIO<V>::store(w, e, N, wv[u]);
       }
     }
+    if (gb + U * kBlock < v1) load_round(gb + U * kBlock);
   }
   __syncthreads();
 #pragma unroll
   for (int v = 0; v < W; ++v) red[tid * W + v] = acc[v];
   block_tree_reduce(red, kBlock * W, k);
   if (tid < k) part_out[(int64_t)g * k + tid] = red[tid];
+}
+
+// ---------------------------------------------- persistent MGS (one launch)
+// All k + 1 MGS passes of Arnoldi step k (times the sweeps) in ONE launch of
+// at most one 512-thread block per CU, so every block is resident and a
+// grid-wide barrier is safe. Each thread keeps its E elements of w in
+// registers for the whole step, so a pass moves only V_{j+1} from HBM (read
+// once, prefetched while the block waits at the previous barrier) instead of
+// w, V_j and V_{j+1} in and w out.
+//   pass p (sweep sw, index j):  w -= alpha_j V_j  (V_j in registers)
+//                                partial of <next, w>, next = V_{j+1}, V_0 of
+//                                the next sweep, or w itself after the last
+//   grid barrier; every block sums the G partials in the same fixed order
+//   -> alpha_{j+1}, identical bits in every block (no atomics on data).
+// Barrier: per-group arrival counters (group = blockIdx % 8, the XCD under
+// round-robin dispatch: speed only, the counts are exact for any placement),
+// the last arriver of a group bumps the top counter, one lane per block polls
+// it. Partials are stored write-through (agent-scope atomic stores) and read
+// back after an agent-scope acquire. Every spin is bounded: on timeout the
+// kernel raises ctrl->status = KRY_EDEVICE and every block leaves.
+constexpr int kMgsBlock = 512;
+constexpr int kBarWords = 16;  // [0, 8) group counters, 8 top counter, 9 abort
+constexpr unsigned kSpinLimit = 1u << 20;
+
+__device__ __forceinline__ void st_agent(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+  return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Grid barrier, split so the block can issue its next prefetch between
+// arriving and waiting. Arrive after this block's partials are stored
+// write-through and drained by every storing wave; the partials are read back
+// with write-through-coherent loads only (ld_agent), so no L1 invalidate is
+// needed. Counters: per-group arrivals (group = blockIdx % 8, the XCD under
+// round-robin dispatch: speed only, the counts are exact for any placement);
+// the last arriver of a group bumps the top counter.
+__device__ __forceinline__ void mgs_arrive(unsigned *bar, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int G = gridDim.x;
+    const int grp = blockIdx.x & 7;
+    const unsigned gsize = (unsigned)((G - grp + 7) / 8);
+    const unsigned old = __hip_atomic_fetch_add(bar + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == gsize * epoch) __hip_atomic_fetch_add(bar + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Wait for every block's arrival. Every spin is bounded: on timeout the block
+// raises ctrl->status = KRY_EDEVICE and the abort word, and every block
+// leaves. Returns false (in every thread) in that case.
+__device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag) {
+  if (threadIdx.x == 0) {
+    const int G = gridDim.x;
+    const unsigned ngroups = G < 8 ? (unsigned)G : 8u;
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ngroups * epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      ++spins;
+      if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        ok = 0;
+        break;
+      }
+      if (spins > kSpinLimit) {
+        __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the partial loads below the poll
+    *flag = ok;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Deterministic block sum for one column: each wave sums by a fixed xor
+// butterfly (lane 0's value is used), then thread 0 adds the wave sums in
+// order. Result in *out (LDS), valid after the trailing barrier.
+__device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wsum[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = wsum[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) s += wsum[i];
+    *out = s;
+  }
+  __syncthreads();
+}
+
+// Fixed-order sum of P partial rows (same order in every block of size B).
+template <int B, bool AGENT>
+__device__ __forceinline__ void reduce_rows(const double *part, int P, int k, double *red) {
+  const int tid = threadIdx.x;
+  if (k == 1) {
+    double s = 0.0;
+    for (int p = tid; p < P; p += B) s += AGENT ? ld_agent(part + p) : part[p];
+    block_sum1(s, red + B, red);
+    return;
+  }
+  const int c = tid & (k - 1);
+  const int step = B / k;
+  double s = 0.0;
+  int p = tid / k;
+  for (; p + 3 * step < P; p += 4 * step) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double *a = part + (int64_t)(p + u * step) * k + c;
+      v[u] = AGENT ? ld_agent(a) : *a;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u];
+  }
+  for (; p < P; p += step) {
+    const double *a = part + (int64_t)p * k + c;
+    s += AGENT ? ld_agent(a) : *a;
+  }
+  red[tid] = s;
+  block_tree_reduce(red, B, k);
+}
+
+template <typename V, int E>
+__global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V *__restrict__ w,
+                                                            const V *__restrict__ Vb, size_t stride, int col,
+                                                            int sweeps, const double *__restrict__ part0, int P0,
+                                                            double *__restrict__ pbuf, double *__restrict__ h,
+                                                            unsigned *bar, Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int NV = E / W;
+  __shared__ double red[kMgsBlock * W];
+  __shared__ double alpha[kMaxCols];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  const int64_t base = (int64_t)blockIdx.x * NV * kMgsBlock;
+  V wr[NV][W], vc[NV][W], vn[NV][W];
+  auto ld = [&](const V *src, V(&dst)[NV][W]) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) VIO<V>::load(src, (base + (int64_t)u * kMgsBlock + tid) * W, N, dst[u]);
+  };
+  const int np = sweeps * (col + 1);
+  auto next_of = [&](int p) -> const V * {  // the vector of pass p's inner product (null = w)
+    const int j = p % (col + 1), sw = p / (col + 1);
+    if (j < col) return Vb + stride * (size_t)(j + 1);
+    if (sw + 1 < sweeps) return Vb;
+    return nullptr;
+  };
+  ld(w, wr);
+  ld(Vb, vc);
+  if (const V *q = next_of(0)) ld(q, vn);
+  // alpha_0 = <V_0, w> from the SpMV's partials
+  reduce_rows<kMgsBlock, false>(part0, P0, k, red);
+  if (tid < k) alpha[tid] = red[tid];
+  __syncthreads();
+  for (int p = 0; p < np; ++p) {
+    const int j = p % (col + 1);
+    const bool first_sweep = p <= col;
+    if (blockIdx.x == 0 && tid < k) {  // h[j] += alpha_j (arnoldi.py:160-161)
+      const V a = (V)alpha[tid];
+      const V prev = first_sweep ? V(0) : (V)h[(int64_t)j * k + tid];
+      h[(int64_t)j * k + tid] = (double)(prev + a);
+    }
+    const V *q = next_of(p);
+    double acc[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc[v] = 0.0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int64_t e = (base + (int64_t)u * kMgsBlock + tid) * W;
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V t = (V)alpha[(e + v) & (k - 1)] * vc[u][v];
+        wr[u][v] = wr[u][v] - t;  // Av -= alpha * V[j] (arnoldi.py:162)
+        if (e + v < N) {
+          const double a = q ? (double)vn[u][v] : (double)wr[u][v];
+          const double b = (double)wr[u][v];
+          acc[v] += dterm(a, b);
+        }
+      }
+    }
+    if (q) {  // V_{j+1} becomes the next pass's subtrahend
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+#pragma unroll
+        for (int v = 0; v < W; ++v) vc[u][v] = vn[u][v];
+    }
+    if (k == 1) {
+      double t = acc[0];
+#pragma unroll
+      for (int v = 1; v < W; ++v) t += acc[v];
+      block_sum1(t, red + kMgsBlock, red);
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < W; ++v) red[tid * W + v] = acc[v];
+      block_tree_reduce(red, kMgsBlock * W, k);
+    }
+    double *slot = pbuf + (size_t)(p < np - 1 ? (p & 1) : 2) * G * k;
+    if (p == np - 1) {  // <w, w> partials for the QR kernel; w back to HBM
+      if (tid < k) slot[(int64_t)blockIdx.x * k + tid] = red[tid];
+#pragma unroll
+      for (int u = 0; u < NV; ++u) VIO<V>::store(w, (base + (int64_t)u * kMgsBlock + tid) * W, N, wr[u]);
+      return;
+    }
+    if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
+    mgs_arrive(bar, (unsigned)(p + 1));
+    // prefetch the vector after next only now: the drain in mgs_arrive must
+    // not wait for it (vmcnt is in order); it travels during the wait
+    if (const V *q2 = next_of(p + 1)) ld(q2, vn);
+    if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag)) return;
+    reduce_rows<kMgsBlock, true>(slot, G, k, red);
+    if (tid < k) alpha[tid] = red[tid];
+    __syncthreads();
+  }
 }
 
 // out = src / hsafe  (arnoldi.py:193-195, the guarded normalisation)
@@ -294,46 +532,61 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
 
 // yy = R[:m,:m]^-1 y[:m] per column (gmres.py:24-38; LAPACK ?trtrs semantics:
 // zero rhs -> 0, non-finite input -> error, zero diagonal -> singular).
+// One 64-lane block per column c (m <= 64): the column's R and y are read in
+// parallel, lane i owns x[i], and the back substitution walks j = m-1..0 with
+// x[j] broadcast through LDS, so every x[i] sees the same operations in the
+// same order as the serial column-oriented loop (reference BLAS xTRSV 'U','N',
+// 'N'): bitwise the same solution without m^2 dependent global loads.
 template <typename S>
-__global__ void gm_trsv_kernel(const double *R, const double *y, double *yy, int m, int k, int maxiter,
-                               Ctrl *ctrl) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= k) return;
+__global__ __launch_bounds__(64) void gm_trsv_kernel(const double *R, const double *y, double *yy, int m, int k,
+                                                     int maxiter, Ctrl *ctrl) {
+  __shared__ S Rs[64 * 64];
+  __shared__ S fin[64];
+  __shared__ int did[64];
+  const int c = blockIdx.x, i = threadIdx.x;
   const int64_t ld = (int64_t)maxiter * k;
-  bool allzero = true;
-  for (int i = 0; i < m; ++i) allzero = allzero && (y[(int64_t)i * k + c] == 0.0);
-  if (allzero) {
-    for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = 0.0;
+  bool nz = false, bad = false, sing = false;
+  S xi = S(0);
+  if (i < m) {
+    const double yv = y[(int64_t)i * k + c];
+    nz = yv != 0.0;
+    bad = !isfinite(yv);
+    xi = (S)yv;
+  }
+  for (int idx = i; idx < m * m; idx += 64) {
+    const int r = idx / m, q = idx - (idx / m) * m;
+    const double v = R[r * ld + (int64_t)q * k + c];
+    bad = bad || !isfinite(v);
+    sing = sing || (r == q && v == 0.0);
+    Rs[r * 64 + q] = (S)v;
+  }
+  // precedence of the reference: zero rhs -> 0, then non-finite, then singular
+  if (!__any(nz)) {
+    if (i < m) yy[(int64_t)i * k + c] = 0.0;
     return;
   }
-  bool finite = true;
-  for (int i = 0; i < m; ++i) {
-    finite = finite && isfinite(y[(int64_t)i * k + c]);
-    for (int j = 0; j < m; ++j) finite = finite && isfinite(R[i * ld + (int64_t)j * k + c]);
-  }
-  if (!finite) {
-    ctrl->status = KRY_ENONFINITE;
+  if (__any(bad)) {
+    if (i == 0) ctrl->status = KRY_ENONFINITE;
     return;
   }
-  for (int i = 0; i < m; ++i)
-    if (R[i * ld + (int64_t)i * k + c] == 0.0) {
-      ctrl->status = KRY_ESINGULAR;
-      return;
-    }
-  S x[64];
-  // column-oriented back substitution (reference BLAS xTRSV 'U','N','N')
-  for (int i = 0; i < m; ++i) x[i] = (S)y[(int64_t)i * k + c];
+  if (__any(sing)) {
+    if (i == 0) ctrl->status = KRY_ESINGULAR;
+    return;
+  }
+  __syncthreads();
   for (int j = m - 1; j >= 0; --j) {
-    if (x[j] != S(0)) {
-      x[j] = x[j] / (S)R[j * ld + (int64_t)j * k + c];
-      const S t = x[j];
-      for (int i = j - 1; i >= 0; --i) {
-        const S p = t * (S)R[i * ld + (int64_t)j * k + c];
-        x[i] = x[i] - p;
-      }
+    if (i == j) {
+      did[j] = xi != S(0);
+      if (xi != S(0)) xi = xi / Rs[j * 64 + j];
+      fin[j] = xi;
+    }
+    __syncthreads();
+    if (did[j] && i < j) {
+      const S p = fin[j] * Rs[i * 64 + j];
+      xi = xi - p;
     }
   }
-  for (int i = 0; i < m; ++i) yy[(int64_t)i * k + c] = (double)x[i];
+  if (i < m) yy[(int64_t)i * k + c] = (double)xi;
 }
 
 // Larger triangular systems: same algorithm, solution kept in global memory.
@@ -674,6 +927,54 @@ void hh_run_impl(kry_gmres *s, int max_steps) {
   }
 }
 
+// Launch the persistent MGS kernel for this Arnoldi step if w fits the
+// registers of one resident 512-thread block per CU; false = not eligible
+// (decided once per solver: s->mgsp_E = 0 no, else elements per thread).
+template <typename V>
+bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int step) {
+  const int64_t N = s->n * (int64_t)s->k;
+  if (s->mgsp_E < 0) {
+    s->mgsp_E = 0;
+    const char *e = getenv("KRY_MGS_PERSIST");
+    if (!(e && atoi(e) == 0)) {
+      int dev = 0, ncu = 0;
+      KRY_HIP(hipGetDevice(&dev));
+      KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      auto fits = [&](auto kern, int E) {
+        const int64_t G = (N + (int64_t)kMgsBlock * E - 1) / ((int64_t)kMgsBlock * E);
+        int per_cu = 0;
+        KRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kMgsBlock, 0));
+        // one block per CU: VGPR-bound residency (<= 256 VGPRs at 2 waves
+        // per SIMD), far from the SGPR band where the answer runs high
+        return G <= ncu && per_cu >= 1;
+      };
+      // (E = 32 doubles per thread would spill: float only)
+      if (fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
+      else if (fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
+      else if (sizeof(V) == 4 && fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
+    }
+  }
+  if (s->mgsp_E == 0) return false;
+  hipStream_t st = s->ctx->stream;
+  const int E = s->mgsp_E;
+  const int G = (int)((N + (int64_t)kMgsBlock * E - 1) / ((int64_t)kMgsBlock * E));
+  if (step == 0) KRY_HIP(hipMemsetAsync(s->bar, 0, (size_t)s->chunk_cap * kBarWords * 4, st));
+  unsigned *bar = s->bar + (size_t)step * kBarWords;
+  double *pbuf = s->part2;  // [pass parity 0 | parity 1 | last pass], G * k each
+  ProfScope ps(s->ctx, PROF_MGS);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
+                       pin, Pin, pbuf, s->h, bar, s->ctrl, step);
+  };
+  if (E == 8) go(gm_mgsp_kernel<V, 8>);
+  else if (E == 16) go(gm_mgsp_kernel<V, 16>);
+  else if constexpr (sizeof(V) == 4) go(gm_mgsp_kernel<V, 32>);
+  KRY_HIP(hipGetLastError());
+  s->mgsp_grid = G;
+  s->mgsp_out = pbuf + (size_t)2 * G * s->k;
+  return true;
+}
+
 template <typename V, typename MV, typename I>
 void gm_run_impl(kry_gmres *s, int max_steps) {
   if (s->householder) return hh_run_impl<V, MV, I>(s, max_steps);
@@ -702,6 +1003,19 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
         w = wb[s->wcur];
         gm_apply_op<V, MV, I>(s, Vk, EpiStoreDot<V>{w, V0, s->w, k}, s->part, &P, s->ctrl, step);
       }
+    }
+    if (fuse_norm && !s->w && mgsp_launch<V>(s, w, s->part, P, col, step)) {
+      // the QR kernel reads the persistent kernel's <w, w> partials
+      hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const double *)s->mgsp_out, s->mgsp_grid,
+                         k, s->scal, s->h, s->R, s->y, s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
+      KRY_HIP(hipGetLastError());
+      if (col + 1 < s->maxiter) {
+        s->vpending = true;  // V_{col+1} is formed by the next step's SpMV
+        continue;
+      }
+      launch_elementwise<V>(N, k, OpScaleDiv<V>{w, basis<V>(s->V, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
+                            nullptr, s->ctrl, step, st);
+      continue;
     }
     // the SpMV's partials of <V_0, w> -> one value per column, so every MGS
     // block reduces a single partial row for its first coefficient
@@ -767,7 +1081,7 @@ void gm_solution_impl(kry_gmres *s) {
   if (m > 0) {
     const int g = (k + kBlock - 1) / kBlock;
     if (m <= 64)
-      hipLaunchKernelGGL(gm_trsv_kernel<V>, dim3(g), dim3(kBlock), 0, st, s->R, s->y, s->yy, m, k, s->maxiter, s->ctrl);
+      hipLaunchKernelGGL(gm_trsv_kernel<V>, dim3(k), dim3(64), 0, st, s->R, s->y, s->yy, m, k, s->maxiter, s->ctrl);
     else
       hipLaunchKernelGGL(gm_trsv_big_kernel<V>, dim3(g), dim3(kBlock), 0, st, s->R, s->y, s->yy, m, k, s->maxiter,
                          s->ctrl);
@@ -804,7 +1118,7 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 void gm_free(kry_gmres *s) {
   void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
                   s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2,
-                  s->U, s->vnew, s->hh, s->wv2};
+                  s->U, s->vnew, s->hh, s->wv2, s->bar};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -873,6 +1187,7 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     s->yy = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
     s->chunk_cap = 64;
     s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * k * 8));
+    s->bar = static_cast<unsigned *>(dev_alloc((size_t)s->chunk_cap * kBarWords * 4));
     s->ctrl = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
     KRY_HIP(hipStreamSynchronize(ctx->stream));
   } catch (...) {
@@ -990,6 +1305,9 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
     dev_free(s->hist);
     s->hist = nullptr;
     s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
+    dev_free(s->bar);
+    s->bar = nullptr;
+    s->bar = static_cast<unsigned *>(dev_alloc((size_t)max_steps * kBarWords * 4));
     s->chunk_cap = max_steps;
   }
   reset_ctrl(s->ctrl, st);
@@ -997,6 +1315,7 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   Ctrl c;
   KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
+  if (c.status == KRY_EDEVICE) throw Error{KRY_EDEVICE, "persistent MGS kernel: grid barrier timed out"};
   const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
   if (done > 0) {
     KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * s->k * 8, hipMemcpyDeviceToHost, st));

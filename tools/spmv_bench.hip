@@ -239,6 +239,127 @@ static int random_study(int64_t n, int reps) {
   return 0;
 }
 
+// Variant kept for the record (measured 0.358 ms vs spmv_cbp_kernel 0.264 ms
+// on cfg3, grid 1024): software-pipelined spmv_cbp_kernel (same ownership,
+// same per-row order, bitwise the same result). The block's work is one sequence of
+// chunks (column block b, owned group o, entry offset c0); the segment table
+// of that sequence is staged in LDS once. Per chunk: gather x for the
+// chunk's columns, THEN issue the column/value/row-offset loads of the next
+// chunk (so a wait for the gathers never waits for the prefetch: vmcnt is in
+// order), stage the products in one of two LDS buffers, one barrier, and
+// every thread adds its row's products to its running sum. The HBM stream of
+// chunk i+1 is in flight while chunk i is gathered, staged and summed.
+constexpr int kCbMaxSteps = 512;  // nb * owned groups per block
+template <typename V, typename MV, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_cbq_kernel(int nb, int64_t n, int64_t ng,
+                                                          const int64_t *__restrict__ gptr,
+                                                          const uint16_t *__restrict__ roff,
+                                                          const int *__restrict__ col, const MV *__restrict__ val,
+                                                          Src src, Epi epi, double *__restrict__ part,
+                                                          const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  constexpr int U = kCbCap / kBlock;
+  __shared__ V prod[2][kCbCap];
+  __shared__ double red[kBlock];
+  __shared__ int64_t seg_s0[kCbMaxSteps];
+  __shared__ int seg_len[kCbMaxSteps];
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  const int own = (int)((ng - blockIdx.x + G - 1) / G);  // groups blk, blk + G, ... (host: own <= kCbMaxOwn)
+  const int T = nb * own;                                 // steps (b, o), b major (host: T <= kCbMaxSteps)
+  for (int t = tid; t < T; t += kBlock) {
+    const int b = t / own, o = t - (t / own) * own;
+    const int64_t q = (int64_t)b * ng + blockIdx.x + (int64_t)o * G;
+    const int64_t s0 = gptr[q];
+    seg_s0[t] = s0;
+    seg_len[t] = (int)(gptr[q + 1] - s0);
+  }
+  __syncthreads();
+  const auto bs = src.template bind<1>(0);
+  V acc[kCbMaxOwn];
+#pragma unroll
+  for (int o = 0; o < kCbMaxOwn; ++o) acc[o] = V(0);
+
+  struct Chunk {
+    int j[U];
+    MV a[U];
+    int r0, r1;
+  };
+  // loads of chunk (t, c0): its entries and this thread's row range in step t
+  auto load = [&](int t, int c0, Chunk &c) {
+    const int64_t s0 = seg_s0[t];
+    const int len = seg_len[t];
+    const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = c0 + tid + u * kBlock;
+      c.j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
+      c.a[u] = e < c1 ? __builtin_nontemporal_load(val + s0 + e) : MV(0);
+    }
+    const int b = t / own, o = t - (t / own) * own;
+    const int64_t row = ((int64_t)blockIdx.x + (int64_t)o * G) * kCbRows + tid;
+    c.r0 = 0;
+    c.r1 = 0;
+    if (row < n) {
+      c.r0 = roff[(int64_t)b * n + row];
+      c.r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
+    }
+  };
+  int t = 0, c0 = 0, par = 0;
+  // one chunk: gathers of `cur`, prefetch of the next chunk into `nxt`,
+  // products to LDS, barrier, row sums. Returns false after the last chunk.
+  auto body = [&](Chunk &cur, Chunk &nxt) -> bool {
+    int tn = t, cn = c0 + kCbCap;
+    if (cn >= seg_len[t]) {
+      tn = t + 1;
+      cn = 0;
+    }
+    V xj[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xj[u] = cur.j[u] >= 0 ? bs(cur.j[u], 0) : V(0);
+    if (tn < T) load(tn, cn, nxt);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (cur.j[u] >= 0) prod[par][tid + u * kBlock] = (V)cur.a[u] * xj[u];
+    __syncthreads();
+    const int len = seg_len[t];
+    const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
+    const int lo = cur.r0 > c0 ? cur.r0 : c0, hi = cur.r1 < c1 ? cur.r1 : c1;
+    const int o = t - (t / own) * own;
+    V s = acc[0];
+#pragma unroll
+    for (int oo = 1; oo < kCbMaxOwn; ++oo)
+      if (oo == o) s = acc[oo];
+    for (int e = lo; e < hi; ++e) s = s + prod[par][e - c0];
+#pragma unroll
+    for (int oo = 0; oo < kCbMaxOwn; ++oo)
+      if (oo == o) acc[oo] = s;
+    t = tn;
+    c0 = cn;
+    par ^= 1;
+    return t < T;
+  };
+  Chunk A, B;
+  if (T > 0) {
+    load(0, 0, A);
+    while (body(A, B) && body(B, A)) {
+    }
+  }
+  double dacc = 0.0;
+#pragma unroll
+  for (int o = 0; o < kCbMaxOwn; ++o) {
+    if (o >= own) break;
+    const int64_t row = ((int64_t)blockIdx.x + (int64_t)o * G) * kCbRows + tid;
+    if (row < n) dacc += epi(row, 0, acc[o], bs(row, 0));
+  }
+  if (part != nullptr) {
+    __syncthreads();
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[blockIdx.x] = red[0];
+  }
+}
+
 // Column-blocked image tuning on the cfg3 pattern: block width x launch grid.
 static int cb_tune(int64_t n, int reps) {
   kry_ctx *ctx;
@@ -336,6 +457,32 @@ static int cb_tune(int64_t n, int reps) {
       printf("cb persistent cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
              S / (tot / reps) / 1e6);
       verify("persistent");
+    }
+    for (int grid : {1024, 1536, 2048}) {
+      if (A->cb_ng > (int64_t)grid * kCbMaxOwn) continue;
+      if (A->cb_nb * ((A->cb_ng + grid - 1) / grid) > kCbMaxSteps) continue;
+      auto launch = [&] {
+        hipLaunchKernelGGL((spmv_cbq_kernel<double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
+                           dim3(kBlock), 0, 0, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr,
+                           (const uint16_t *)A->cb_roff, (const int *)A->cb_col, (const double *)A->cb_val,
+                           SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, (double *)nullptr, (const Ctrl *)nullptr, 0);
+      };
+      CK(hipMemset(d_y, 0, n * 8));
+      launch();
+      CK(hipDeviceSynchronize());
+      float tot = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+      }
+      printf("cb pipelined cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
+             S / (tot / reps) / 1e6);
+      verify("pipelined");
     }
     KC(kry_csr_destroy(A));
   }
