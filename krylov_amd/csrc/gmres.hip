@@ -288,12 +288,71 @@ __device__ __forceinline__ void reduce_rows(const double *part, int P, int k, do
   block_tree_reduce(red, B, k);
 }
 
+// One column (k = 1): the partials travel as self-validating granules
+// {tag, 32 data bits} (two per block: the double's low and high words), stored
+// write-through; no counters, no flag. Wave 0 of every block sweeps all G
+// blocks' granules until every tag matches, then sums the values in a fixed
+// order (lane l: blocks l, l + 64, ..., then a fixed xor butterfly; lane 0's
+// value). tag = (step + 1) << 12 | (pass + 1) is unique within a chunk, and
+// the granule words are zeroed once per chunk.
+constexpr int kGranWords = 2 * 2 * 256;  // two pass parities x two words x G <= 256 blocks
+// barrier words for `steps` chunk steps, then the (shared) granule words
+inline size_t bar_bytes(int steps) { return (size_t)steps * kBarWords * 4 + (size_t)kGranWords * 8; }
+__device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned tag, double v) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, t | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 only; returns the same value in every lane (false = timed out / aborted).
+__device__ bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out) {
+  const int lane = threadIdx.x;
+  unsigned long long g[4][2];
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = lane + 64 * i;
+      if (b < G) {
+        g[i][0] = __hip_atomic_load(gr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[i][1] = __hip_atomic_load(gr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && (unsigned)(g[i][0] >> 32) == tag && (unsigned)(g[i][1] >> 32) == tag;
+      }
+    }
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    ++spins;
+    if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      return false;
+    if (spins > kSpinLimit) {
+      if (lane == 0) {
+        __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = lane + 64 * i;
+    if (b < G) s += __longlong_as_double((long long)((g[i][1] << 32) | (g[i][0] & 0xffffffffull)));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) *out = s;
+  return true;
+}
+
 template <typename V, int E>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V *__restrict__ w,
                                                             const V *__restrict__ Vb, size_t stride, int col,
                                                             int sweeps, const double *__restrict__ part0, int P0,
                                                             double *__restrict__ pbuf, double *__restrict__ h,
-                                                            unsigned *bar, Ctrl *ctrl, int step) {
+                                                            unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
+                                                            int step) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int NV = E / W;
@@ -371,6 +430,19 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
 #pragma unroll
       for (int u = 0; u < NV; ++u) VIO<V>::store(w, (base + (int64_t)u * kMgsBlock + tid) * W, N, wr[u]);
       return;
+    }
+    if (k == 1) {  // granule all-gather of the block partials
+      unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
+      const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
+      if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, red[0]);
+      if (const V *q2 = next_of(p + 1)) ld(q2, vn);
+      if (tid < 64) {
+        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha);
+        if (tid == 0) flag = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!flag) return;
+      continue;
     }
     if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
     mgs_arrive(bar, (unsigned)(p + 1));
@@ -946,7 +1018,7 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
         KRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kMgsBlock, 0));
         // one block per CU: VGPR-bound residency (<= 256 VGPRs at 2 waves
         // per SIMD), far from the SGPR band where the answer runs high
-        return G <= ncu && per_cu >= 1;
+        return G <= ncu && G <= 256 && per_cu >= 1 && (int64_t)s->sweeps * (s->maxiter + 1) < 4095;
       };
       // (E = 32 doubles per thread would spill: float only)
       if (fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
@@ -958,13 +1030,14 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   hipStream_t st = s->ctx->stream;
   const int E = s->mgsp_E;
   const int G = (int)((N + (int64_t)kMgsBlock * E - 1) / ((int64_t)kMgsBlock * E));
-  if (step == 0) KRY_HIP(hipMemsetAsync(s->bar, 0, (size_t)s->chunk_cap * kBarWords * 4, st));
+  if (step == 0) KRY_HIP(hipMemsetAsync(s->bar, 0, bar_bytes(s->chunk_cap), st));
   unsigned *bar = s->bar + (size_t)step * kBarWords;
+  unsigned long long *gran = reinterpret_cast<unsigned long long *>(s->bar + (size_t)s->chunk_cap * kBarWords);
   double *pbuf = s->part2;  // [pass parity 0 | parity 1 | last pass], G * k each
   ProfScope ps(s->ctx, PROF_MGS);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
-                       pin, Pin, pbuf, s->h, bar, s->ctrl, step);
+                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step);
   };
   if (E == 8) go(gm_mgsp_kernel<V, 8>);
   else if (E == 16) go(gm_mgsp_kernel<V, 16>);
@@ -1187,7 +1260,7 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     s->yy = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
     s->chunk_cap = 64;
     s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * k * 8));
-    s->bar = static_cast<unsigned *>(dev_alloc((size_t)s->chunk_cap * kBarWords * 4));
+    s->bar = static_cast<unsigned *>(dev_alloc(bar_bytes(s->chunk_cap)));
     s->ctrl = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
     KRY_HIP(hipStreamSynchronize(ctx->stream));
   } catch (...) {
@@ -1307,7 +1380,7 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
     s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
     dev_free(s->bar);
     s->bar = nullptr;
-    s->bar = static_cast<unsigned *>(dev_alloc((size_t)max_steps * kBarWords * 4));
+    s->bar = static_cast<unsigned *>(dev_alloc(bar_bytes(max_steps)));
     s->chunk_cap = max_steps;
   }
   reset_ctrl(s->ctrl, st);
