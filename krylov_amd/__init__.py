@@ -15,7 +15,7 @@ from .extra import bicgstab, cgr, cgs, gcr
 from .givens import givens, lartg
 from .gmres import gmres, gmres_restarted
 from .minres import minres
-from .sparse import CsrOperator, as_device_operator
+from .sparse import CsrOperator, as_device_operator, clear_operator_cache
 
 __version__ = "0.1.0"
 
@@ -32,6 +32,7 @@ __all__ = [
     "lartg",
     "CsrOperator",
     "as_device_operator",
+    "clear_operator_cache",
     "WeightedInner",
     "Identity",
     "Info",

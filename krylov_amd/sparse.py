@@ -109,8 +109,62 @@ class CsrOperator:
         return f"CsrOperator(n={self.n}, nnz={self.nnz}, dtype={self.dtype}, device={self.device})"
 
 
+# --------------------------------------------------------------- upload cache
+# a scipy/dense matrix handed to krylov_amd.cg/gmres/...
+# again (the reference's tests and users call the solvers repeatedly on one A)
+# is not uploaded and re-imaged again. The cache is keyed by the object and
+# verified by a content fingerprint (xxh3 over indptr/indices/data, shape,
+# dtype), so an in-place change of the matrix is re-uploaded. It holds at most
+# _CACHE_MAX entries and drops an entry when its matrix is garbage-collected.
+_CACHE_MAX = 4
+_cache = {}  # (device, id(A)) -> (weakref(A), fingerprint, CsrOperator)
+
+
+def _fingerprint(A):
+    import xxhash
+
+    h = xxhash.xxh3_64()
+    if scipy.sparse.issparse(A):
+        csr = A if A.format == "csr" else None
+        if csr is None:
+            return None  # other formats are converted on every call
+        for arr in (csr.indptr, csr.indices, csr.data):
+            h.update(np.ascontiguousarray(arr).view(np.uint8).data)
+        return (csr.shape, str(csr.dtype), str(csr.indices.dtype), csr.nnz, h.intdigest())
+    if isinstance(A, np.ndarray):
+        h.update(np.ascontiguousarray(A).view(np.uint8).data)
+        return (A.shape, str(A.dtype), h.intdigest())
+    return None
+
+
+def clear_operator_cache():
+    """Release every cached device copy of a host matrix."""
+    _cache.clear()
+
+
 def as_device_operator(A, device=None):
     """Return ``A`` as a CsrOperator (uploading scipy/dense inputs once)."""
+    import os
+
     if isinstance(A, CsrOperator):
         return A
-    return CsrOperator(A, device=device)
+    if os.environ.get("KRYLOV_CSR_CACHE", "1") == "0":
+        return CsrOperator(A, device=device)
+    dev = get_context(device).device
+    fp = _fingerprint(A)
+    if fp is None:
+        return CsrOperator(A, device=device)
+    key = (dev, id(A))
+    hit = _cache.get(key)
+    if hit is not None and hit[0]() is A and hit[1] == fp:
+        return hit[2]
+    op = CsrOperator(A, device=dev)
+    try:
+        ref = weakref.ref(A, lambda _r, key=key: _cache.pop(key, None))
+    except TypeError:
+        return op
+    _cache.pop(key, None)
+    while len(_cache) >= _CACHE_MAX:
+        _cache.pop(next(iter(_cache)))
+    _cache[key] = (ref, fp, op)
+    return op

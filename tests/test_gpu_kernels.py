@@ -275,3 +275,27 @@ def test_spmv_metric_matrix_bitwise():
     x = np.random.default_rng(0).standard_normal(A.shape[0])
     got = krylov_amd.CsrOperator(A) @ x
     np.testing.assert_array_equal(got, A @ x)
+
+
+def test_operator_upload_cache():
+    """SURVEY §8(f) rank 3: a scipy matrix passed again is not re-uploaded;
+    an in-place change of its values is detected and re-uploaded."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    krylov_amd.clear_operator_cache()
+    A = problems.poisson2d(40)
+    b = np.ones(A.shape[0])
+    op1 = krylov_amd.as_device_operator(A)
+    assert krylov_amd.as_device_operator(A) is op1
+    _, i1 = krylov_amd.cg(A, b, tol=1e-10)
+    assert krylov_amd.as_device_operator(A) is op1
+    A.data *= 2.0  # in place: the fingerprint changes
+    op2 = krylov_amd.as_device_operator(A)
+    assert op2 is not op1
+    _, i2 = krylov_amd.cg(A, b, tol=1e-10)
+    assert i2.numsteps == i1.numsteps
+    np.testing.assert_allclose(np.asarray(i2.resnorms[:-1]), np.asarray(i1.resnorms[:-1]), rtol=1e-10)
+    B = A.copy()
+    assert krylov_amd.as_device_operator(B) is not op2  # another object: its own upload
+    krylov_amd.clear_operator_cache()
