@@ -240,19 +240,27 @@ __device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag) {
 }
 
 // Deterministic block sum for one column: each wave sums by a fixed xor
-// butterfly (lane 0's value is used), then thread 0 adds the wave sums in
-// order. Result in *out (LDS), valid after the trailing barrier.
-__device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
+// butterfly (lane 0's value is used), one barrier, then wave 0 adds the wave
+// sums by a fixed butterfly over lanes 0..7 (blockDim <= 512). The result is
+// returned in thread 0 (no trailing barrier); block_sum1 also stores it to
+// *out and makes it visible to the block.
+__device__ __forceinline__ double block_sum1_t0(double v, double *wsum) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) wsum[wv] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = wsum[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) s += wsum[i];
-    *out = s;
+  double s = 0.0;
+  if (wv == 0) {
+    s = lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0;
+#pragma unroll
+    for (int off = 1; off <= 4; off <<= 1) s += __shfl_xor(s, off);
   }
+  return s;
+}
+__device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
+  const double s = block_sum1_t0(v, wsum);
+  if (threadIdx.x == 0) *out = s;
   __syncthreads();
 }
 
@@ -413,11 +421,12 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
 #pragma unroll
         for (int v = 0; v < W; ++v) vc[u][v] = vn[u][v];
     }
+    double part1 = 0.0;  // k == 1: the block partial, in thread 0
     if (k == 1) {
       double t = acc[0];
 #pragma unroll
       for (int v = 1; v < W; ++v) t += acc[v];
-      block_sum1(t, red + kMgsBlock, red);
+      part1 = block_sum1_t0(t, red + kMgsBlock);
     } else {
       __syncthreads();
 #pragma unroll
@@ -426,7 +435,11 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
     }
     double *slot = pbuf + (size_t)(p < np - 1 ? (p & 1) : 2) * G * k;
     if (p == np - 1) {  // <w, w> partials for the QR kernel; w back to HBM
-      if (tid < k) slot[(int64_t)blockIdx.x * k + tid] = red[tid];
+      if (k == 1) {
+        if (tid == 0) slot[blockIdx.x] = part1;
+      } else if (tid < k) {
+        slot[(int64_t)blockIdx.x * k + tid] = red[tid];
+      }
 #pragma unroll
       for (int u = 0; u < NV; ++u) VIO<V>::store(w, (base + (int64_t)u * kMgsBlock + tid) * W, N, wr[u]);
       return;
@@ -434,7 +447,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
     if (k == 1) {  // granule all-gather of the block partials
       unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
       const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
-      if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, red[0]);
+      if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
       if (const V *q2 = next_of(p + 1)) ld(q2, vn);
       if (tid < 64) {
         const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha);
