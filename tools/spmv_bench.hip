@@ -491,7 +491,197 @@ static int cb_tune(int64_t n, int reps) {
   return 0;
 }
 
+// Variant kept for the record (cfg4 k = 8: 0.749 ms at UNR 4 vs the
+// lane-group kernel 0.795 ms; UNR 8 and k = 16 slower): lane-group SpMV with
+// broadcast matrix entries (K in {4, 8, 16}). The
+// lane-group kernel above re-loads every slot's index and value once per row
+// pass (K passes of 64 / K rows), so a wave issues 2K narrow matrix loads per
+// slot column. Here the 64 lanes load a slot column once (lane = row, one
+// coalesced access as in the k = 1 kernel) and each pass takes its row's entry
+// by a cross-lane shuffle; lane (row r, column c) keeps one accumulator per
+// pass. The gathers are unchanged (K contiguous values of x per row), and
+// every (row, column) is still summed over the slots in stored order from 0:
+// bitwise the lane-group and csr_matvecs results.
+template <typename V, typename MV, typename I, int K, int UNR, bool D16, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_sell_lgb_kernel(
+    const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
+    const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
+    int64_t nslices, int64_t n, int k, const I *__restrict__ indptr, const I *__restrict__ indices,
+    const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part, const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  constexpr int RPP = 64 / K;  // rows per pass
+  constexpr int NP = K;        // passes per slice
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / K, c = lane & (K - 1);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const auto bs = src.template bind<1>(c);
+  double dacc = 0.0;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    V acc[NP];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) acc[t] = V(0);
+    if (w >= 0) {
+      const I *ci = sidx + base + lane;
+      const uint16_t *cd = sdelta + base + lane;
+      const int *cb = scbase + (base >> 6);
+      const MV *cv = sval + base + lane;
+      for (int j0 = 0; j0 < w; j0 += UNR) {
+        I col[UNR];
+        V a[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const bool in = j0 + u < w;
+          if constexpr (D16) {
+            const unsigned d = in ? (unsigned)__builtin_nontemporal_load(cd + (int64_t)(j0 + u) * 64) : 0xFFFFu;
+            const int b = in ? cb[j0 + u] : 0;
+            col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
+          } else {
+            col[u] = in ? __builtin_nontemporal_load(ci + (int64_t)(j0 + u) * 64) : I(-1);
+          }
+          a[u] = in ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
+        }
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+          const int src_lane = t * RPP + rl0;
+          I cx[UNR];
+          V ax[UNR], xv[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            cx[u] = __shfl(col[u], src_lane);
+            ax[u] = __shfl(a[u], src_lane);
+          }
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) xv[u] = cx[u] >= 0 ? bs(cx[u], 0) : V(0);
+#pragma unroll
+          for (int u = 0; u < UNR; ++u)
+            if (cx[u] >= 0) {
+              const V p = ax[u] * xv[u];
+              acc[t] = acc[t] + p;
+            }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NP; ++t) {
+        const int64_t row = s * 64 + t * RPP + rl0;
+        if (row < n)
+          for (I e = indptr[row]; e < indptr[row + 1]; ++e) {
+            const V p = (V)data[e] * bs(indices[e], 0);
+            acc[t] = acc[t] + p;
+          }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const int64_t row = s * 64 + t * RPP + rl0;
+      if (row < n) dacc += epi(row, c, acc[t], bs(row, 0));
+    }
+  }
+  if (part != nullptr) {
+    red[tid] = dacc;  // slot tid holds column tid % k
+    block_tree_reduce(red, kBlock, k);
+    if (tid < k) part[(int64_t)g * k + tid] = red[tid];
+  }
+}
+
+// cfg4 block SpMV (5-pt Poisson m^2, k = 8 row-major RHS): lane-group kernel
+// vs the broadcast lane-group kernel, both checked bitwise against csr_matvecs.
+static int block_study(int m, int k, int reps) {
+  const int64_t n = (int64_t)m * m;
+  std::vector<int> ip(n + 1, 0), ix;
+  std::vector<double> dv;
+  ix.reserve(n * 5);
+  dv.reserve(n * 5);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t i = r % m, j = r / m;
+    if (j > 0) { ix.push_back((int)(r - m)); dv.push_back(-1.0); }
+    if (i > 0) { ix.push_back((int)(r - 1)); dv.push_back(-1.0); }
+    ix.push_back((int)r); dv.push_back(4.0);
+    if (i + 1 < m) { ix.push_back((int)(r + 1)); dv.push_back(-1.0); }
+    if (j + 1 < m) { ix.push_back((int)(r + m)); dv.push_back(-1.0); }
+    ip[r + 1] = (int)ix.size();
+  }
+  const int64_t nnz = ix.size();
+  const double S = nnz * 12.0 + (n + 1) * 4.0 + 2.0 * n * k * 8.0;
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  kry_csr *A;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+  printf("block study: poisson %d^2 n=%ld nnz=%ld k=%d compact=%d S=%.3f GB\n", m, n, nnz, k, (int)A->compact, S / 1e9);
+  double *d_x, *d_y;
+  CK(hipMalloc(&d_x, n * k * 8));
+  CK(hipMalloc(&d_y, n * k * 8));
+  std::vector<double> xh(n * k);
+  for (int64_t i = 0; i < n * k; ++i) xh[i] = 1.0 + 1e-3 * (double)((i * 2654435761u) % 1000);
+  CK(hipMemcpy(d_x, xh.data(), n * k * 8, hipMemcpyHostToDevice));
+  std::vector<double> yref(n * k);
+  for (int64_t r = 0; r < n; ++r)
+    for (int c = 0; c < k; ++c) {
+      double sum = 0;
+      for (int e = ip[r]; e < ip[r + 1]; ++e) {
+        const double p = dv[e] * xh[(int64_t)ix[e] * k + c];
+        sum = sum + p;
+      }
+      yref[r * k + c] = sum;
+    }
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->nslices + 3) / 4));
+  auto run = [&](const char *name, auto kern) {
+    CK(hipMemset(d_y, 0, n * k * 8));
+    auto launch = [&] {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                         (const int *)A->sidx, (const uint16_t *)A->sdelta, (const int *)A->scbase,
+                         (const double *)A->sval, A->nslices, A->n, k, (const int *)A->indptr,
+                         (const int *)A->indices, (const double *)A->data, SrcPlain<double>{d_x, k},
+                         EpiStore<double>{d_y, k}, (double *)nullptr, (const Ctrl *)nullptr, 0);
+    };
+    launch();
+    CK(hipDeviceSynchronize());
+    float tot = 0;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      tot += ms;
+    }
+    std::vector<double> h(n * k);
+    CK(hipMemcpy(h.data(), d_y, n * k * 8, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n * k; ++i) bad += memcmp(&h[i], &yref[i], 8) != 0;
+    printf("  %s: %.4f ms  %.0f GB/s (S)  bitwise mismatches %ld\n", name, tot / reps, S / (tot / reps) / 1e6, bad);
+  };
+  if (k == 8) {
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 8, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("broadcast lane-group UNR4", spmv_sell_lgb_kernel<double, double, int, 8, 4, true, SrcPlain<double>, EpiStore<double>>);
+  } else if (k == 4) {
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 4, 8, true, SrcPlain<double>, EpiStore<double>>);
+  } else if (k == 16) {
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 16, 8, true, SrcPlain<double>, EpiStore<double>>);
+  }
+  KC(kry_csr_destroy(A));
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "block") == 0)
+    return block_study(argc > 2 ? atoi(argv[2]) : 3163, argc > 3 ? atoi(argv[3]) : 8, 10);
   if (argc > 1 && strcmp(argv[1], "random") == 0) return random_study(argc > 2 ? atol(argv[2]) : 2000000, 10);
   if (argc > 1 && strcmp(argv[1], "cbtune") == 0) return cb_tune(argc > 2 ? atol(argv[2]) : 2000000, 10);
   const int m = argc > 1 ? atoi(argv[1]) : 216;
