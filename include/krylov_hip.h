@@ -200,6 +200,14 @@ int kry_comm_destroy(kry_comm *c);
 /* in-place sum over ranks of `count` host doubles (setup-time exchanges) */
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);
 int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k);
+/* GMRES / MINRES: the same sharding (gmres.py:193 and minres.py:162 stop rules,
+ * arnoldi.py:187 / 270-272 invariance over all columns): one
+ * ncclAllReduce(sum, f64, count = total_k + 1) per step of the zero-padded
+ * residual norms plus a count of ranks with a non-invariant column. After
+ * attaching, set_criterion takes total_k values and each run history row
+ * holds total_k values. */
+int kry_gmres_attach_comm(kry_gmres *s, kry_comm *c, int32_t col_offset, int32_t total_k);
+int kry_minres_attach_comm(kry_minres *s, kry_comm *c, int32_t col_offset, int32_t total_k);
 
 /* ---- timing: HIP events on the context stream --------------------------- */
 int kry_timer_start(kry_ctx *ctx);

@@ -95,6 +95,8 @@ _SIGNATURES = {
     "kry_comm_destroy": [_vp],
     "kry_comm_allreduce": [_vp, _dp, _i32],
     "kry_cg_attach_comm": [_vp, _vp, _i32, _i32],
+    "kry_gmres_attach_comm": [_vp, _vp, _i32, _i32],
+    "kry_minres_attach_comm": [_vp, _vp, _i32, _i32],
     "kry_timer_start": [_vp],
     "kry_timer_stop": [_vp, _dp],
     "kry_profile_enable": [_vp, _int],

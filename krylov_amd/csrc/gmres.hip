@@ -58,6 +58,12 @@ struct kry_gmres {
   // grid-barrier words of the persistent MGS kernel: 16 per chunk step,
   // zeroed once per chunk (kry_gmres_run)
   unsigned *bar = nullptr;
+  // RHS sharding (kry_gmres_attach_comm): one allreduce per step of the
+  // zero-padded residual-norm vector + a non-invariant count, global stop
+  kry_comm *comm = nullptr;
+  double *gbuf = nullptr;   // total_k + 1
+  double *gcrit = nullptr;  // total_k
+  int col_offset = 0, total_k = 0;
   int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
   int mgsp_grid = 0;
   double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
@@ -556,7 +562,7 @@ __global__ void gm_coef_kernel(const double *part, int P, int k, double *scal, d
 template <typename S>
 __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, double *h, double *R, double *y,
                              double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step,
-                             int hgiven = 0) {
+                             int hgiven = 0, double *gbuf = nullptr, int col_offset = 0, int total_k = 0) {
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock];
   __shared__ double rn[kMaxCols];
@@ -605,10 +611,34 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
     y[(int64_t)col * k + c] = (double)(a0 + a1);
     y[(int64_t)(col + 1) * k + c] = (double)ny1;
     rn[c] = (double)fabs(ny1);
-    hist[(int64_t)step * k + c] = rn[c];
+    if (!gbuf) hist[(int64_t)step * k + c] = rn[c];
   }
   __syncthreads();
+  if (gbuf) {  // sharded: this rank's share of the global vector; gm_global_check decides
+    for (int t = threadIdx.x; t < total_k; t += blockDim.x) {
+      const int lc = t - col_offset;
+      gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
+    }
+    if (threadIdx.x == 0) gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+    return;
+  }
   const bool conv = all_le(rn, scal + G_CRIT * k, k, &flag);
+  if (threadIdx.x == 0) {
+    if (inv) ctrl->invariant = 1;
+    if (inv || conv) ctrl->stop_at = step + 1;
+  }
+}
+
+// Sharded global step decision on the allreduced vector: the history row,
+// np.all(h[k+1] <= 1e-14) over ALL columns of all ranks (arnoldi.py:187) and
+// the stop rule over all columns (gmres.py:193).
+__global__ void gm_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
+                                int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ int flag;
+  for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
+  const bool inv = gbuf[total_k] == 0.0;
+  const bool conv = all_le(gbuf, gcrit, total_k, &flag);
   if (threadIdx.x == 0) {
     if (inv) ctrl->invariant = 1;
     if (inv || conv) ctrl->stop_at = step + 1;
@@ -1061,6 +1091,25 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   return true;
 }
 
+// h[k+1], Givens QR, resnorm and the step decision; sharded: one RCCL
+// allreduce of the residual-norm vector (+ non-invariant count) per step and
+// the global decision.
+template <typename V>
+void gm_qr_step(kry_gmres *s, const double *pin, int P, int col, int step) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, pin, P, k, s->scal, s->h, s->R, s->y, s->Gc,
+                     s->Gs, col, s->maxiter, s->hist, s->ctrl, step, 0, s->comm ? s->gbuf : nullptr, s->col_offset,
+                     s->total_k);
+  KRY_HIP(hipGetLastError());
+  if (!s->comm) return;
+  ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+  KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  hipLaunchKernelGGL(gm_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
+                     (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
+  KRY_HIP(hipGetLastError());
+}
+
 template <typename V, typename MV, typename I>
 void gm_run_impl(kry_gmres *s, int max_steps) {
   if (s->householder) return hh_run_impl<V, MV, I>(s, max_steps);
@@ -1092,9 +1141,7 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     }
     if (fuse_norm && !s->w && mgsp_launch<V>(s, w, s->part, P, col, step)) {
       // the QR kernel reads the persistent kernel's <w, w> partials
-      hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const double *)s->mgsp_out, s->mgsp_grid,
-                         k, s->scal, s->h, s->R, s->y, s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
-      KRY_HIP(hipGetLastError());
+      gm_qr_step<V>(s, s->mgsp_out, s->mgsp_grid, col, step);
       if (col + 1 < s->maxiter) {
         s->vpending = true;  // V_{col+1} is formed by the next step's SpMV
         continue;
@@ -1139,9 +1186,7 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
                          &P, s->ctrl, step, st);
       pin = s->part;
     }
-    hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, pin, P, k, s->scal, s->h, s->R, s->y,
-                       s->Gc, s->Gs, col, s->maxiter, s->hist, s->ctrl, step);
-    KRY_HIP(hipGetLastError());
+    gm_qr_step<V>(s, pin, P, col, step);
     // P_{col+1} = w / guard(h[col+1]), V_{col+1} = M w / guard(h[col+1]) unless
     // invariant; these run for this step even when the QR kernel just raised
     // stop_at to step + 1 (arnoldi.py:191-196).
@@ -1204,7 +1249,7 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 void gm_free(kry_gmres *s) {
   void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
                   s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2,
-                  s->U, s->vnew, s->hh, s->wv2, s->bar};
+                  s->U, s->vnew, s->hh, s->wv2, s->bar, s->gbuf, s->gcrit};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -1373,7 +1418,10 @@ int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r
 int kry_gmres_set_criterion(kry_gmres *s, const double *criterion) {
   KRY_API_BEGIN
   KRY_REQUIRE(s && criterion, KRY_EINVAL, "null argument");
-  KRY_HIP(hipMemcpyAsync(s->scal + G_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  if (s->comm)  // all total_k columns, in rank order
+    KRY_HIP(hipMemcpyAsync(s->gcrit, criterion, s->total_k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  else
+    KRY_HIP(hipMemcpyAsync(s->scal + G_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
   KRY_HIP(hipStreamSynchronize(s->ctx->stream));
   KRY_API_END
 }
@@ -1390,7 +1438,7 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   if (max_steps > s->chunk_cap) {
     dev_free(s->hist);
     s->hist = nullptr;
-    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
+    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * (s->comm ? s->total_k : s->k) * 8));
     dev_free(s->bar);
     s->bar = nullptr;
     s->bar = static_cast<unsigned *>(dev_alloc(bar_bytes(max_steps)));
@@ -1404,7 +1452,8 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   if (c.status == KRY_EDEVICE) throw Error{KRY_EDEVICE, "persistent MGS kernel: grid barrier timed out"};
   const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
   if (done > 0) {
-    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * s->k * 8, hipMemcpyDeviceToHost, st));
+    const int hk = s->comm ? s->total_k : s->k;
+    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));
     KRY_HIP(hipStreamSynchronize(st));
   }
   s->steps += done;
@@ -1447,6 +1496,33 @@ int kry_gmres_get(kry_gmres *s, int which, void *host) {
   KRY_HIP(hipSetDevice(s->ctx->device));
   KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)s->n * s->k * dsize(s->dtype), hipMemcpyDeviceToHost, s->ctx->stream));
   KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  KRY_API_END
+}
+
+// RHS sharding: this solver's k columns are global columns
+// [col_offset, col_offset + k) of total_k; every step allreduces the residual
+// norms (and a non-invariant count) over the communicator and applies the
+// reference's stop and invariance rules to all columns. The history rows
+// returned by kry_gmres_run then hold total_k values.
+int kry_gmres_attach_comm(kry_gmres *s, kry_comm *c, int32_t col_offset, int32_t total_k) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && c, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(col_offset >= 0 && total_k >= col_offset + s->k && total_k <= 4096, KRY_EINVAL,
+              "bad column range");
+  KRY_REQUIRE(!s->householder, KRY_EUNSUPPORTED, "Householder Arnoldi is single right-hand side");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dev_free(s->gbuf);
+  dev_free(s->gcrit);
+  s->gbuf = nullptr;
+  s->gcrit = nullptr;
+  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 1) * 8));
+  s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
+  dev_free(s->hist);
+  s->hist = nullptr;
+  s->hist = static_cast<double *>(dev_alloc((size_t)s->chunk_cap * total_k * 8));
+  s->comm = c;
+  s->col_offset = col_offset;
+  s->total_k = total_k;
   KRY_API_END
 }
 

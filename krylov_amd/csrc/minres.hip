@@ -40,6 +40,11 @@ struct kry_minres {
   double *scal = nullptr;
   double *hist = nullptr;
   Ctrl *ctrl = nullptr;
+  // RHS sharding (kry_minres_attach_comm), as in GMRES
+  kry_comm *comm = nullptr;
+  double *gbuf = nullptr;   // total_k + 1
+  double *gcrit = nullptr;  // total_k
+  int col_offset = 0, total_k = 0;
   int chunk_cap = 0;
   int64_t it = 0;
   int wflip = 0;
@@ -164,7 +169,7 @@ __global__ void mr_alpha_kernel(const double *part, int P, int k, double *scal, 
 
 template <typename V, typename S>
 __global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int have_g0, int have_g1, double *hist,
-                             Ctrl *ctrl, int step) {
+                             Ctrl *ctrl, int step, double *gbuf = nullptr, int col_offset = 0, int total_k = 0) {
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock];
   __shared__ double rn[kMaxCols];
@@ -220,10 +225,33 @@ __global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int
     // next step's h[0] = this step's h[2] (arnoldi.py:246-247)
     scal[M_H0 * k + c] = (double)h2;
     rn[c] = fabs(ny1);
-    hist[(int64_t)step * k + c] = rn[c];
+    if (!gbuf) hist[(int64_t)step * k + c] = rn[c];
   }
   __syncthreads();
+  if (gbuf) {  // sharded: this rank's share of the global vector; mr_global_check decides
+    for (int t = threadIdx.x; t < total_k; t += blockDim.x) {
+      const int lc = t - col_offset;
+      gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
+    }
+    if (threadIdx.x == 0) gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+    return;
+  }
   const bool conv = all_le(rn, scal + M_CRIT * k, k, &flag);
+  if (threadIdx.x == 0) {
+    if (inv) ctrl->invariant = 1;
+    if (inv || conv) ctrl->stop_at = step + 1;
+  }
+}
+
+// Sharded global step decision (Lanczos invariance over all columns,
+// arnoldi.py:270-272; stop rule over all columns, minres.py:162).
+__global__ void mr_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
+                                int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ int flag;
+  for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
+  const bool inv = gbuf[total_k] == 0.0;
+  const bool conv = all_le(gbuf, gcrit, total_k, &flag);
   if (threadIdx.x == 0) {
     if (inv) ctrl->invariant = 1;
     if (inv || conv) ctrl->stop_at = step + 1;
@@ -334,8 +362,16 @@ void mr_run_typed(kry_minres *s, int max_steps) {
       launch_spmv_any<V>(s->M, k, SrcPlain<V>{w, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), w, s->w, k}, partB, &PB,
                          s->ctrl, step, st);
     hipLaunchKernelGGL((mr_qr_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, i >= 1 ? 1 : 0,
-                       i >= 2 ? 1 : 0, s->hist, s->ctrl, step);
+                       i >= 2 ? 1 : 0, s->hist, s->ctrl, step, s->comm ? s->gbuf : nullptr, s->col_offset,
+                       s->total_k);
     KRY_HIP(hipGetLastError());
+    if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
+      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
+                         (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
+      KRY_HIP(hipGetLastError());
+    }
     const int f = (s->wflip + step) & 1;
     {
       ProfScope ps(s->ctx, PROF_UPDATE);
@@ -375,7 +411,8 @@ void mr_residual_impl(kry_minres *s, double *norm2) {
 
 void mr_free(kry_minres *s) {
   void *bufs[] = {s->b,  s->x0,   s->yk,   s->wv,   s->xk,    s->rt,  s->P[0], s->P[1], s->P[2], s->W[0],
-                  s->W[1], s->w, s->part, s->scal, s->hist, s->ctrl, s->Vr[0], s->Vr[1], s->mw, s->t1, s->t2};
+                  s->W[1], s->w, s->part, s->scal, s->hist, s->ctrl, s->Vr[0], s->Vr[1], s->mw, s->t1, s->t2,
+                  s->gbuf, s->gcrit};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -520,7 +557,10 @@ int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double 
 int kry_minres_set_criterion(kry_minres *s, const double *criterion) {
   KRY_API_BEGIN
   KRY_REQUIRE(s && criterion, KRY_EINVAL, "null argument");
-  KRY_HIP(hipMemcpyAsync(s->scal + M_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  if (s->comm)  // all total_k columns, in rank order
+    KRY_HIP(hipMemcpyAsync(s->gcrit, criterion, s->total_k * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  else
+    KRY_HIP(hipMemcpyAsync(s->scal + M_CRIT * s->k, criterion, s->k * 8, hipMemcpyHostToDevice, s->ctx->stream));
   KRY_HIP(hipStreamSynchronize(s->ctx->stream));
   KRY_API_END
 }
@@ -536,7 +576,7 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   if (max_steps > s->chunk_cap) {
     dev_free(s->hist);
     s->hist = nullptr;
-    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * s->k * 8));
+    s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * (s->comm ? s->total_k : s->k) * 8));
     s->chunk_cap = max_steps;
   }
   reset_ctrl(s->ctrl, st);
@@ -546,7 +586,8 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   KRY_HIP(hipStreamSynchronize(st));
   const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
   if (done > 0) {
-    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * s->k * 8, hipMemcpyDeviceToHost, st));
+    const int hk = s->comm ? s->total_k : s->k;
+    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));
     KRY_HIP(hipStreamSynchronize(st));
   }
   s->it += done;
@@ -578,6 +619,28 @@ int kry_minres_get(kry_minres *s, int which, void *host) {
     mr_compute_xk<float>(s);
   KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
+  KRY_API_END
+}
+
+// RHS sharding: see kry_gmres_attach_comm.
+int kry_minres_attach_comm(kry_minres *s, kry_comm *c, int32_t col_offset, int32_t total_k) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && c, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(col_offset >= 0 && total_k >= col_offset + s->k && total_k <= 4096, KRY_EINVAL,
+              "bad column range");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  dev_free(s->gbuf);
+  dev_free(s->gcrit);
+  s->gbuf = nullptr;
+  s->gcrit = nullptr;
+  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 1) * 8));
+  s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
+  dev_free(s->hist);
+  s->hist = nullptr;
+  s->hist = static_cast<double *>(dev_alloc((size_t)(s->chunk_cap > 0 ? s->chunk_cap : 1) * total_k * 8));
+  s->comm = c;
+  s->col_offset = col_offset;
+  s->total_k = total_k;
   KRY_API_END
 }
 

@@ -125,3 +125,124 @@ def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None)
     xk = prob.unpad_vec(st.get(0), prob.r0_dtype)
     ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 2 + 2 * k}
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)
+
+
+def _shard_layout(prob, comm):
+    kp, world = prob.kpad, comm.world
+    total = kp * world
+    off = kp * comm.rank
+    real = np.concatenate([np.arange(r * kp, r * kp + prob.kc) for r in range(world)])
+    return total, off, real
+
+
+def _run_global(lib_run, h, steps, total):
+    out = np.zeros((max(steps, 1), total))
+    done = ctypes.c_int32()
+    inv = ctypes.c_int32()
+    check(lib_run(h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
+    return out[: done.value], bool(inv.value)
+
+
+def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"):
+    """GMRES (MGS) on this rank's RHS columns ``B`` (n, k_local), k_local
+    equal on every rank. Every Arnoldi step performs one RCCL allreduce of the
+    residual norms and a non-invariant count, so all ranks apply the
+    reference's stop rule (gmres.py:193) and invariance test (arnoldi.py:187)
+    to ALL columns and stop at the same step as the unsharded block solve.
+    Returns ``(xk_local or None, Info)`` with the global history."""
+    from .gmres import _GmresState
+
+    if not ortho.startswith("mgs"):
+        raise NotImplementedError("the sharded path runs MGS Arnoldi (Householder is single right-hand side)")
+    sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    B = np.asarray(B)
+    if B.ndim == 1:
+        B = B[:, None]
+    prob = Problem(A, B, x0, None, device=comm.ctx.device)
+    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+    total, off, real = _shard_layout(prob, comm)
+
+    def glob(local_vals):
+        v = np.zeros(total)
+        v[off:off + prob.kpad] = local_vals
+        return comm.allreduce(v)
+
+    st = _GmresState(prob, maxiter, sweeps)
+    check(lib.kry_gmres_attach_comm(st.h, comm.handle, off, total))
+    rn0 = glob(st.start())
+    resnorms = [rn0[real].astype(prob.inner_dtype).astype(np.float64)]
+    criterion = np.maximum(tol * resnorms[0], atol)
+    crit_full = np.full(total, np.inf)
+    crit_full[real] = criterion
+    st.set_criterion(crit_full)
+    k = 0
+    success = False
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            st.solution()
+            sq = glob(st.residual_norm2())
+            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        hist, _ = _run_global(lib.kry_gmres_run, st.h, min(_helpers.CHUNK, maxiter - k), total)
+        for row in hist:
+            resnorms.append(np.asarray(row)[real].astype(prob.inner_dtype).astype(np.float64))
+            k += 1
+    if k == 0:
+        xk = prob.zeros_like_b() if prob.x0 is None else prob.x0
+    else:
+        st.solution()
+        xk = st.xk()
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + k + k * (k + 1) / 2,
+           "axpy": 4 + 2 * k + k * (k + 1) / 2}
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)
+
+
+def minres(A, B, comm, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None):
+    """MINRES on this rank's RHS columns ``B`` (n, k_local), k_local equal on
+    every rank; one RCCL allreduce per iteration for the global stop rule
+    (minres.py:162) and the Lanczos invariance test over all columns.
+    Returns ``(xk_local or None, Info)`` with the global history."""
+    from .minres import _MinresState
+
+    B = np.asarray(B)
+    if B.ndim == 1:
+        B = B[:, None]
+    prob = Problem(A, B, x0, inner, device=comm.ctx.device)
+    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+    total, off, real = _shard_layout(prob, comm)
+
+    def glob(local_vals):
+        v = np.zeros(total)
+        v[off:off + prob.kpad] = local_vals
+        return comm.allreduce(v)
+
+    st = _MinresState(prob)
+    check(lib.kry_minres_attach_comm(st.h, comm.handle, off, total))
+    rn0 = glob(st.start())
+    resnorms = [rn0[real].astype(prob.inner_dtype).astype(np.float64)]
+    criterion = np.maximum(tol * resnorms[0], atol)
+    crit_full = np.full(total, np.inf)
+    crit_full[real] = criterion
+    st.set_criterion(crit_full)
+    k = 0
+    success = False
+    while True:
+        if np.all(resnorms[-1] <= criterion):
+            sq = glob(st.residual_norm2())
+            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
+            if np.all(resnorms[-1] <= criterion):
+                success = True
+                break
+        if k == maxiter:
+            break
+        hist, _ = _run_global(lib.kry_minres_run, st.h, min(_helpers.CHUNK, maxiter - k), total)
+        for row in hist:
+            resnorms.append(np.asarray(row)[real].astype(prob.inner_dtype).astype(np.float64))
+            k += 1
+    xk = st.xk()
+    ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 4 + 8 * k}
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)

@@ -241,10 +241,20 @@ class _ArnoldiHouseholder:
         return v, h
 
 
+def _ident(v):
+    return v
+
+
 def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None,
-          Ml=None, Mr=None):
+          Ml=None, Mr=None, shard=None):
     """Restates gmres.py:41-251 with Arnoldi MGS (arnoldi.py:107-200) or
-    Householder (arnoldi.py:33-104)."""
+    Householder (arnoldi.py:33-104).
+
+    ``shard`` (test hook for the RHS-sharded path): a callable
+    mapping this rank's per-column values to the global column vector (all
+    ranks, in rank order). The history, the stop rule and the invariance test
+    then act on all columns, as krylov_amd.distributed.gmres does."""
+    glob = _ident if shard is None else shard
     b = np.asarray(b)
     assert A.shape[0] == A.shape[1] == b.shape[0]
     house = ortho == "householder"
@@ -260,11 +270,11 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
         return M_Ml_r, Ml_r, np.sqrt(_real_norm2(inner(Ml_r, M_Ml_r)))
 
     def resnorm_of(z):
-        return resid(z)[2]
+        return glob(resid(z)[2])
 
     M_Ml_r0, Ml_r0, r0norm = resid(x0)
     r0 = M_Ml_r0
-    resnorms = [r0norm]
+    resnorms = [glob(r0norm)]
     if callback is not None:
         callback(x0, Ml_r0)
 
@@ -341,7 +351,7 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
                 w -= a * P[j]
         Mw = _apply(M, w)
         h[steps + 1] = np.sqrt(inner(w, Mw))
-        if np.all(h[steps + 1] <= 1.0e-14):
+        if np.all(glob(h[steps + 1]) <= 1.0e-14):
             invariant = True
         else:
             hk = np.where(h[steps + 1] != 0.0, h[steps + 1], 1.0)
@@ -363,7 +373,7 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
         if callback is not None:
             xk = solution(yk)
             callback(xk, rn)
-        resnorms.append(rn[()])
+        resnorms.append(glob(rn[()]))
         k += 1
     if xk is None:
         xk = solution(y[:steps])
@@ -372,8 +382,10 @@ def gmres(A, b, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1e-15, maxiter=
     return (xk if success else None), Info(success, xk, k, resnorms, num_operations=ops)
 
 
-def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None, Ml=None, Mr=None):
+def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callback=None, M=None, Ml=None, Mr=None,
+           shard=None):
     """Restates minres.py:28-253 with Lanczos (arnoldi.py:203-281).
+    ``shard``: the RHS-sharding test hook, as in ``gmres``.
 
     Precision follows the reference under NumPy-2 promotion: the Lanczos
     scalars ``h`` are kept in the vector dtype, while ``R``, the rotations, ``y``
@@ -385,9 +397,11 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
     maxiter = A.shape[0] if maxiter is None else maxiter
     x0 = np.zeros_like(b) if x0 is None else x0
 
+    glob = _ident if shard is None else shard
+
     def resnorm_of(z):  # minres.py:105-118
         Ml_r = _apply(Ml, b - A @ z)
-        return np.sqrt(_real_norm2(inner(Ml_r, _apply(M, Ml_r))))
+        return glob(np.sqrt(_real_norm2(inner(Ml_r, _apply(M, Ml_r)))))
 
     r = b - A @ x0
     Ml_r = _apply(Ml, r)
@@ -412,7 +426,7 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
     rn = np.array(rnorm)
     if callback is not None:
         callback(x0, rn)
-    resnorms = [rn[()]]
+    resnorms = [glob(rn[()])]
     k = 0
     success = False
     criterion = np.maximum(tol * resnorms[0], atol)
@@ -438,7 +452,7 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
         w -= a * lz_p
         Mw = _apply(M, w)
         lz_h[2] = np.sqrt(inner(w, Mw))
-        if np.all(lz_h[2] <= 1.0e-14):
+        if np.all(glob(lz_h[2]) <= 1.0e-14):
             invariant = True
             lz_v = lz_p = None
         else:
@@ -471,7 +485,7 @@ def minres(A, b, inner=None, x0=None, tol=1e-5, atol=1e-15, maxiter=None, callba
         if callback is not None:
             xk = x0 + _apply(Mr, yk)
             callback(xk, rn)
-        resnorms.append(rn[()])
+        resnorms.append(glob(rn[()]))
         k += 1
     if xk is None:
         xk = x0 + _apply(Mr, yk)
