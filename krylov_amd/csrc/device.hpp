@@ -26,6 +26,46 @@ __device__ __forceinline__ double dterm(double x, double y) { return x * y; }
 __device__ __forceinline__ double dterm_w(double x, double w, double y) { return x * (w * y); }
 
 // ------------------------------------------------------------- x sources
+// C consecutive values starting at p (16-B aligned: p's element offset is a
+// multiple of C, C in {2, 4}, and allocations are 256-B aligned) as 16-B
+// vector loads.
+template <typename V, int C>
+__device__ __forceinline__ void vload_row(const V *p, V (&o)[C]) {
+  if constexpr (sizeof(V) == 8) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < C / 2; ++q) {
+      const d2 t = reinterpret_cast<const d2 *>(p)[q];
+      o[2 * q] = t.x;
+      o[2 * q + 1] = t.y;
+    }
+  } else {
+    typedef float fC __attribute__((ext_vector_type(C)));
+    const fC t = *reinterpret_cast<const fC *>(p);
+#pragma unroll
+    for (int q = 0; q < C; ++q) o[q] = t[q];
+  }
+}
+template <typename V, int C, bool NT = false>
+__device__ __forceinline__ void vstore_row(V *p, const V (&o)[C]) {
+  if constexpr (sizeof(V) == 8) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < C / 2; ++q) {
+      const d2 t = d2{o[2 * q], o[2 * q + 1]};
+      if (NT) __builtin_nontemporal_store(t, reinterpret_cast<d2 *>(p) + q);
+      else reinterpret_cast<d2 *>(p)[q] = t;
+    }
+  } else {
+    typedef float fC __attribute__((ext_vector_type(C)));
+    fC t;
+#pragma unroll
+    for (int q = 0; q < C; ++q) t[q] = o[q];
+    if (NT) __builtin_nontemporal_store(t, reinterpret_cast<fC *>(p));
+    else *reinterpret_cast<fC *>(p) = t;
+  }
+}
+
 // The SpMV input x[j, c] may be materialised on the fly from other vectors
 // (the p-update of CG, the normalisation of GMRES), so the gather never
 // needs a separate pass over HBM. The owner row writes the same value out.
@@ -42,6 +82,8 @@ struct SrcPlain {
     const V *x;
     int k, c0;
     __device__ __forceinline__ V operator()(int64_t j, int c) const { return x[j * k + c0 + c]; }
+    // the KT values of row j (lane-group kernel, KT in {2, 4})
+    __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const { vload_row<V, KT>(x + j * k + c0, o); }
   };
   template <int KT>
   __device__ __forceinline__ Bound<KT> bind(int c0) const {
@@ -75,6 +117,17 @@ struct SrcCgP {
       const V t = om[c] * pold[j * k + c0 + c];
       return rj + t;
     }
+    __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const {
+      vload_row<V, KT>(r + j * k + c0, o);
+      if (first) return;
+      V q[KT];
+      vload_row<V, KT>(pold + j * k + c0, q);
+#pragma unroll
+      for (int c = 0; c < KT; ++c) {
+        const V t = om[c] * q[c];
+        o[c] = o[c] + t;
+      }
+    }
   };
   template <int KT>
   __device__ __forceinline__ Bound<KT> bind(int c0) const {
@@ -104,6 +157,11 @@ struct SrcScaled {
     V h[KT];
     int k, c0;
     __device__ __forceinline__ V operator()(int64_t j, int c) const { return w[j * k + c0 + c] / h[c]; }
+    __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const {
+      vload_row<V, KT>(w + j * k + c0, o);
+#pragma unroll
+      for (int c = 0; c < KT; ++c) o[c] = o[c] / h[c];
+    }
   };
   template <int KT>
   __device__ __forceinline__ Bound<KT> bind(int c0) const {
@@ -128,6 +186,12 @@ struct EpiStore {
     y[i * k + c] = s;
     return 0.0;
   }
+  // C consecutive columns c0.. of row i at once (lane-group kernel): 16-B
+  // stores, dot contributions added to d[]
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C>(y + i * k + c0, s);
+  }
 };
 
 // y = A v and the first MGS inner product <q, y> (arnoldi.py:176,159).
@@ -142,6 +206,14 @@ struct EpiStoreDot {
     const double qv = (double)q[i * k + c];
     return w ? dterm_w(qv, w[i], (double)s) : dterm(qv, (double)s);
   }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C>(y + i * k + c0, s);
+    V qv[C];
+    vload_row<V, C>(q + i * k + c0, qv);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)qv[c], w[i], (double)s[c]) : dterm((double)qv[c], (double)s[c]);
+  }
 };
 
 // y = A x and <y, y> (weighted): a preconditioned residual M_l r and its norm.
@@ -155,6 +227,12 @@ struct EpiStoreNorm {
     const double sv = (double)s;
     return w ? dterm_w(sv, w[i], sv) : dterm(sv, sv);
   }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C>(y + i * k + c0, s);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)s[c], w[i], (double)s[c]) : dterm((double)s[c], (double)s[c]);
+  }
 };
 
 // out = x0 + A y (gmres.py:97-99 / minres.py: x0 + Mr @ yk).
@@ -166,6 +244,19 @@ struct EpiAddStore {
   __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
     out[i * k + c] = x0 ? x0[i * k + c] + s : s;
     return 0.0;
+  }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    V o[C];
+    if (x0) {
+      vload_row<V, C>(x0 + i * k + c0, o);
+#pragma unroll
+      for (int c = 0; c < C; ++c) o[c] = o[c] + s[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) o[c] = s[c];
+    }
+    vstore_row<V, C>(out + i * k + c0, o);
   }
 };
 
@@ -184,6 +275,15 @@ struct EpiStoreDotV {
     const double qv = (double)q[i * k + c];
     return w ? dterm_w(qv, w[i], (double)s) : dterm(qv, (double)s);
   }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C>(vout + i * k + c0, xi);
+    vstore_row<V, C>(y + i * k + c0, s);
+    V qv[C];
+    vload_row<V, C>(q + i * k + c0, qv);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)qv[c], w[i], (double)s[c]) : dterm((double)qv[c], (double)s[c]);
+  }
 };
 
 // r = b - A z and <r, r> (cg.py:86-90, gmres.py:106-108).
@@ -198,6 +298,16 @@ struct EpiResidual {
     r[i * k + c] = ri;
     const double rv = (double)ri;
     return w ? dterm_w(rv, w[i], rv) : dterm(rv, rv);
+  }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    V ri[C];
+    vload_row<V, C>(b + i * k + c0, ri);
+#pragma unroll
+    for (int c = 0; c < C; ++c) ri[c] = ri[c] - s[c];
+    vstore_row<V, C>(r + i * k + c0, ri);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)ri[c], w[i], (double)ri[c]) : dterm((double)ri[c], (double)ri[c]);
   }
 };
 
@@ -216,6 +326,13 @@ struct EpiCgAp {
     const double pv = (double)pi;
     return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
   }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C>(pnew + i * k + c0, xi);
+    vstore_row<V, C, true>(Ap + i * k + c0, s);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
+  }
 };
 
 // CG: Ap = A p (nontemporal: read once, by the update pass) and <p, Ap>
@@ -229,6 +346,12 @@ struct EpiApDot {
     __builtin_nontemporal_store(s, Ap + i * k + c);
     const double pv = (double)xi;
     return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
+  }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    vstore_row<V, C, true>(Ap + i * k + c0, s);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
   }
 };
 
@@ -250,6 +373,26 @@ struct EpiLanczos {
     out[i * k + c] = o;
     const double vv = (double)v[i * k + c];
     return w ? dterm_w(vv, w[i], (double)o) : dterm(vv, (double)o);
+  }
+  template <int C>
+  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
+    V o[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) o[c] = s[c];
+    if (pold) {
+      V po[C];
+      vload_row<V, C>(pold + i * k + c0, po);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const V t = (V)h0[c0 + c] * po[c];
+        o[c] = o[c] - t;
+      }
+    }
+    vstore_row<V, C>(out + i * k + c0, o);
+    V vv[C];
+    vload_row<V, C>(v + i * k + c0, vv);
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)vv[c], w[i], (double)o[c]) : dterm((double)vv[c], (double)o[c]);
   }
 };
 
@@ -544,36 +687,43 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
 
 // ---------------------------------------------- lane-group SELL SpMV (4 <= k <= 64)
 // For a block of k right-hand sides stored row-major (row i's k values are
-// contiguous), k lanes share a row and lane c owns column c: a wave covers
-// 64 / k rows of a slice per pass, and each gather instruction reads whole
-// contiguous rows of x (k * 8 bytes each) instead of one column-strided value
-// per lane. Same slot order, same per-(row, column) sequential sum, so the
-// result is bitwise the lane-per-row kernel's (and csr_matvecs').
-template <typename V, typename MV, typename I, int UNR, bool D16, class Src, class Epi>
+// contiguous), LPR = k / CPL lanes share a row and each owns CPL consecutive
+// columns: a wave covers 64 / LPR rows of a slice per pass (LPR passes), and
+// each lane gathers its CPL values of an x row with 16-B vector loads, so one
+// pass's gathers read whole contiguous rows (k * 8 bytes each). Same slot
+// order, same per-(row, column) sequential sum, so the result is bitwise the
+// lane-per-row kernel's (and csr_matvecs'). CPL = 4 measured 0.53 ms against
+// 0.80 ms for one column per lane on cfg4 (k = 8, tools/spmv_bench block).
+template <typename V, typename MV, typename I, int CPL, int UNR, bool D16, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
     const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
     int64_t nslices, int64_t n, int k, const I *__restrict__ indptr, const I *__restrict__ indices,
     const MV *__restrict__ data, Src src, Epi epi, double *__restrict__ part, const Ctrl *ctrl, int step) {
   if (halted(ctrl, step)) return;
-  __shared__ double red[kBlock];
+  __shared__ double red[kBlock * CPL];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int rows_per_pass = 64 / k;
-  const int rl0 = lane / k, c = lane & (k - 1);
+  const int lpr = k / CPL;          // lanes per row
+  const int rows_per_pass = 64 / lpr;
+  const int rl0 = lane / lpr, c0 = (lane % lpr) * CPL;
   const int64_t W = (int64_t)gridDim.x * 4;
   const int64_t m = (int64_t)g * 4 + wid;
   const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
-  const auto bs = src.template bind<1>(c);
-  double dacc = 0.0;
+  const auto bs = src.template bind<CPL>(c0);
+  double dacc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
   for (int64_t s = s_begin; s < s_end; ++s) {
     const int w = swidth[s];
     const int64_t base = sptr[s];
     for (int rl = rl0; rl < 64; rl += rows_per_pass) {
       const int64_t row = s * 64 + rl;
-      V acc = V(0);
+      V acc[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[c] = V(0);
       if (w >= 0) {
         const I *ci = sidx + base + rl;
         const uint16_t *cd = sdelta + base + rl;
@@ -594,28 +744,41 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
             }
             a[u] = in ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
           }
-          V xv[UNR];
-#pragma unroll
-          for (int u = 0; u < UNR; ++u) xv[u] = col[u] >= 0 ? bs(col[u], 0) : V(0);
 #pragma unroll
           for (int u = 0; u < UNR; ++u)
             if (col[u] >= 0) {
-              const V p = a[u] * xv[u];
-              acc = acc + p;
+              V xv[CPL];
+              bs.row(col[u], xv);
+#pragma unroll
+              for (int c = 0; c < CPL; ++c) {
+                const V p = a[u] * xv[c];
+                acc[c] = acc[c] + p;
+              }
             }
         }
       } else if (row < n) {
         for (I e = indptr[row]; e < indptr[row + 1]; ++e) {
-          const V p = (V)data[e] * bs(indices[e], 0);
-          acc = acc + p;
+          const V a = (V)data[e];
+          V xv[CPL];
+          bs.row(indices[e], xv);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const V p = a * xv[c];
+            acc[c] = acc[c] + p;
+          }
         }
       }
-      if (row < n) dacc += epi(row, c, acc, bs(row, 0));
+      if (row < n) {
+        V xi[CPL];
+        bs.row(row, xi);
+        epi.template row<CPL>(row, c0, acc, xi, dacc);
+      }
     }
   }
   if (part != nullptr) {
-    red[tid] = dacc;  // slot tid holds column tid % k
-    block_tree_reduce(red, kBlock, k);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];  // slot tid * CPL + c holds column (c0 + c)
+    block_tree_reduce(red, kBlock * CPL, k);
     if (tid < k) part[(int64_t)g * k + tid] = red[tid];
   }
 }
@@ -842,8 +1005,8 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                          static_cast<const I *>(A->indices), static_cast<const MV *>(A->data), src, epi, part, ctrl,
                          step);
     };
-    if (d16) go(spmv_sell_lg_kernel<V, MV, I, 8, true, Src, Epi>);
-    else go(spmv_sell_lg_kernel<V, MV, I, 8, false, Src, Epi>);
+    if (d16) go(spmv_sell_lg_kernel<V, MV, I, 4, 8, true, Src, Epi>);
+    else go(spmv_sell_lg_kernel<V, MV, I, 4, 8, false, Src, Epi>);
     KRY_HIP(hipGetLastError());
     if (grid_out) *grid_out = grid;
     return;

@@ -155,6 +155,70 @@ __global__ __launch_bounds__(256, MINW) void spmv_pf(const int64_t *__restrict__
   }
 }
 
+
+// ---- prototype: packed compact SELL. Lane l loads 4 slots' uint16 deltas as
+// one 8-B access and 2 slots' values as one 16-B access (slot pairs, odd tail
+// slot alone), so a slot costs 1/4 + 1/2 + 1 (gather) vector memory
+// instructions instead of 3. Same per-row order: bitwise.
+template <int UNR>
+__global__ __launch_bounds__(256) void spmv_packed(const int64_t *__restrict__ sptr, const int64_t *__restrict__ dptr,
+                                                   const int *__restrict__ swidth, const uint16_t *__restrict__ dpk,
+                                                   const int *__restrict__ scbase, const double *__restrict__ vpk,
+                                                   int64_t nslices, int64_t n, const double *__restrict__ x,
+                                                   double *__restrict__ y) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s], doff = dptr[s];
+    unsigned d[UNR];
+    double a[UNR];
+    int b[UNR];
+#pragma unroll
+    for (int q = 0; q < UNR / 4; ++q) {
+      if (4 * q < w) {
+        typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+        const us4 v = __builtin_nontemporal_load(reinterpret_cast<const us4 *>(dpk + doff + (int64_t)q * 256 + lane * 4));
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+      } else {
+        d[4 * q] = d[4 * q + 1] = d[4 * q + 2] = d[4 * q + 3] = 0xFFFFu;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < UNR / 2; ++p) {
+      if (2 * p + 1 < w) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(vpk + base + (int64_t)p * 128 + lane * 2));
+        a[2 * p] = v.x;
+        a[2 * p + 1] = v.y;
+      } else if (2 * p < w) {
+        a[2 * p] = __builtin_nontemporal_load(vpk + base + (int64_t)p * 128 + lane);
+        a[2 * p + 1] = 0.0;
+      } else {
+        a[2 * p] = a[2 * p + 1] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) b[u] = u < w ? scbase[(base >> 6) + u] : 0;
+    double xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) xv[u] = (u < w && d[u] != 0xFFFFu) ? x[b[u] + (int)d[u]] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (u < w && d[u] != 0xFFFFu) {
+        const double pr = a[u] * xv[u];
+        acc = acc + pr;
+      }
+    const int64_t row = s * 64 + lane;
+    if (row < n) y[row] = acc;
+  }
+}
 __global__ __launch_bounds__(256) void pupdate_kernel(const double *__restrict__ r, const double *__restrict__ pold,
                                                       const double *__restrict__ om, double *__restrict__ p,
                                                       int64_t n) {
@@ -592,6 +656,130 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_lgb_kernel(
   }
 }
 
+
+// ---- prototype: one lane per row for a k = KB row-major block, the row's KB
+// x values gathered as KB/2 16-B loads, KB accumulators per lane (matrix
+// entries loaded once per slot, coalesced). Same per-(row, column) order.
+template <int KB, int UNR>
+__global__ __launch_bounds__(256) void spmv_rowblk(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                   const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                   const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                   const double *__restrict__ x, double *__restrict__ y) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    double acc[KB];
+#pragma unroll
+    for (int c = 0; c < KB; ++c) acc[c] = 0.0;
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      int col[UNR];
+      double a[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const bool in = j0 + u < w;
+        const unsigned d = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)(j0 + u) * 64 + lane) : 0xFFFFu;
+        const int b = in ? scbase[(base >> 6) + j0 + u] : 0;
+        col[u] = d != 0xFFFFu ? b + (int)d : -1;
+        a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)(j0 + u) * 64 + lane) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (col[u] >= 0) {
+          const d2 *xr = reinterpret_cast<const d2 *>(x + (int64_t)col[u] * KB);
+          d2 xv[KB / 2];
+#pragma unroll
+          for (int q = 0; q < KB / 2; ++q) xv[q] = xr[q];
+#pragma unroll
+          for (int q = 0; q < KB / 2; ++q) {
+            const double p0 = a[u] * xv[q].x, p1 = a[u] * xv[q].y;
+            acc[2 * q] = acc[2 * q] + p0;
+            acc[2 * q + 1] = acc[2 * q + 1] + p1;
+          }
+        }
+      }
+    }
+    const int64_t row = s * 64 + lane;
+    if (row < n) {
+      d2 *yr = reinterpret_cast<d2 *>(y + row * KB);
+#pragma unroll
+      for (int q = 0; q < KB / 2; ++q) yr[q] = d2{acc[2 * q], acc[2 * q + 1]};
+    }
+  }
+}
+
+// ---- prototype: LPR = KB / CPL lanes per row, CPL columns per lane
+// (CPL * 8-B vector gathers and stores), 64 / LPR rows per pass, LPR passes.
+template <int KB, int CPL, int UNR, bool NTS>
+__global__ __launch_bounds__(256) void spmv_lgv(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                const double *__restrict__ x, double *__restrict__ y) {
+  constexpr int LPR = KB / CPL, RPP = 64 / LPR;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const int rl0 = lane / LPR, cq = lane % LPR;
+  typedef double dv __attribute__((ext_vector_type(2)));
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+#pragma unroll
+    for (int t = 0; t < LPR; ++t) {
+      const int rl = t * RPP + rl0;
+      double acc[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[c] = 0.0;
+      for (int j0 = 0; j0 < w; j0 += UNR) {
+        int col[UNR];
+        double a[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const bool in = j0 + u < w;
+          const unsigned d = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)(j0 + u) * 64 + rl) : 0xFFFFu;
+          const int b = in ? scbase[(base >> 6) + j0 + u] : 0;
+          col[u] = d != 0xFFFFu ? b + (int)d : -1;
+          a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)(j0 + u) * 64 + rl) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (col[u] >= 0) {
+            const dv *xr = reinterpret_cast<const dv *>(x + (int64_t)col[u] * KB + cq * CPL);
+            dv xv[CPL / 2];
+#pragma unroll
+            for (int q = 0; q < CPL / 2; ++q) xv[q] = xr[q];
+#pragma unroll
+            for (int q = 0; q < CPL / 2; ++q) {
+              const double p0 = a[u] * xv[q].x, p1 = a[u] * xv[q].y;
+              acc[2 * q] = acc[2 * q] + p0;
+              acc[2 * q + 1] = acc[2 * q + 1] + p1;
+            }
+          }
+        }
+      }
+      const int64_t row = s * 64 + rl;
+      if (row < n) {
+        dv *yr = reinterpret_cast<dv *>(y + row * KB + cq * CPL);
+#pragma unroll
+        for (int q = 0; q < CPL / 2; ++q) {
+          if (NTS) __builtin_nontemporal_store(dv{acc[2 * q], acc[2 * q + 1]}, yr + q);
+          else yr[q] = dv{acc[2 * q], acc[2 * q + 1]};
+        }
+      }
+    }
+  }
+}
 // cfg4 block SpMV (5-pt Poisson m^2, k = 8 row-major RHS): lane-group kernel
 // vs the broadcast lane-group kernel, both checked bitwise against csr_matvecs.
 static int block_study(int m, int k, int reps) {
@@ -664,14 +852,51 @@ static int block_study(int m, int k, int reps) {
     printf("  %s: %.4f ms  %.0f GB/s (S)  bitwise mismatches %ld\n", name, tot / reps, S / (tot / reps) / 1e6, bad);
   };
   if (k == 8) {
-    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 4, 8, true, SrcPlain<double>, EpiStore<double>>);
     run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 8, 8, true, SrcPlain<double>, EpiStore<double>>);
     run("broadcast lane-group UNR4", spmv_sell_lgb_kernel<double, double, int, 8, 4, true, SrcPlain<double>, EpiStore<double>>);
+    auto rowblk = [&](const char *name, auto kern, int gsz) {
+      CK(hipMemset(d_y, 0, n * k * 8));
+      auto launch = [&] {
+        hipLaunchKernelGGL(kern, dim3(gsz), dim3(kBlock), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                           (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices,
+                           A->n, (const double *)d_x, d_y);
+      };
+      launch();
+      CK(hipDeviceSynchronize());
+      float tot = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+      }
+      std::vector<double> h(n * k);
+      CK(hipMemcpy(h.data(), d_y, n * k * 8, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (int64_t i = 0; i < n * k; ++i) bad += memcmp(&h[i], &yref[i], 8) != 0;
+      printf("  %s grid %d: %.4f ms  %.0f GB/s (S)  bitwise mismatches %ld\n", name, gsz, tot / reps,
+             S / (tot / reps) / 1e6, bad);
+    };
+    for (int gsz : {8192}) {
+      rowblk("row-per-lane k=8 UNR4", spmv_rowblk<8, 4>, gsz);
+      rowblk("lgv CPL2 UNR4", spmv_lgv<8, 2, 4, false>, gsz);
+      rowblk("lgv CPL2 UNR8", spmv_lgv<8, 2, 8, false>, gsz);
+      rowblk("lgv CPL4 UNR4", spmv_lgv<8, 4, 4, false>, gsz);
+      rowblk("lgv CPL4 UNR8", spmv_lgv<8, 4, 8, false>, gsz);
+      rowblk("lgv CPL8 UNR4", spmv_lgv<8, 8, 4, false>, gsz);
+      rowblk("lgv CPL2 UNR4 nt-store", spmv_lgv<8, 2, 4, true>, gsz);
+      rowblk("lgv CPL4 UNR4 nt-store", spmv_lgv<8, 4, 4, true>, gsz);
+      rowblk("lgv CPL8 UNR4 nt-store", spmv_lgv<8, 8, 4, true>, gsz);
+    }
   } else if (k == 4) {
-    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 4, 8, true, SrcPlain<double>, EpiStore<double>>);
     run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 4, 8, true, SrcPlain<double>, EpiStore<double>>);
   } else if (k == 16) {
-    run("lane-group", spmv_sell_lg_kernel<double, double, int, 8, true, SrcPlain<double>, EpiStore<double>>);
+    run("lane-group", spmv_sell_lg_kernel<double, double, int, 4, 8, true, SrcPlain<double>, EpiStore<double>>);
     run("broadcast lane-group UNR8", spmv_sell_lgb_kernel<double, double, int, 16, 8, true, SrcPlain<double>, EpiStore<double>>);
   }
   KC(kry_csr_destroy(A));
@@ -836,6 +1061,61 @@ int main(int argc, char **argv) {
                            (double *)nullptr, (const Ctrl *)nullptr, 0);
       });
       check(nm, d_y, yref);
+    }
+  }
+  {
+    // packed image from the library's compact image (host repack)
+    const int64_t ns = A->nslices;
+    std::vector<int64_t> sp(ns + 1);
+    std::vector<int> sw(ns);
+    CK(hipMemcpy(sp.data(), A->sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sw.data(), A->swidth, ns * 4, hipMemcpyDeviceToHost));
+    std::vector<uint16_t> dl(A->nslots);
+    std::vector<double> vl(A->nslots);
+    CK(hipMemcpy(dl.data(), A->sdelta, A->nslots * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(vl.data(), A->sval, A->nslots * 8, hipMemcpyDeviceToHost));
+    std::vector<int64_t> dp(ns + 1, 0);
+    int maxw = 0;
+    for (int64_t s = 0; s < ns; ++s) {
+      maxw = std::max(maxw, sw[s]);
+      dp[s + 1] = dp[s] + 256 * ((std::max(sw[s], 0) + 3) / 4);
+    }
+    if (maxw <= 16) {
+      std::vector<uint16_t> dpk(dp[ns] + 256, 0xFFFF);
+      std::vector<double> vpk(A->nslots + 128, 0.0);
+      for (int64_t s = 0; s < ns; ++s) {
+        const int w = sw[s];
+        const int64_t base = sp[s];
+        for (int j = 0; j < w; ++j)
+          for (int l = 0; l < 64; ++l) {
+            dpk[dp[s] + (j / 4) * 256 + l * 4 + (j & 3)] = dl[base + 64 * j + l];
+            const double v = vl[base + 64 * j + l];
+            if (j < 2 * (w / 2)) vpk[base + (j / 2) * 128 + l * 2 + (j & 1)] = v;
+            else vpk[base + (w / 2) * 128 + l] = v;
+          }
+      }
+      int64_t *d_dp;
+      uint16_t *d_dpk;
+      double *d_vpk;
+      CK(hipMalloc(&d_dp, (ns + 1) * 8));
+      CK(hipMalloc(&d_dpk, dpk.size() * 2));
+      CK(hipMalloc(&d_vpk, vpk.size() * 8));
+      CK(hipMemcpy(d_dp, dp.data(), (ns + 1) * 8, hipMemcpyHostToDevice));
+      CK(hipMemcpy(d_dpk, dpk.data(), dpk.size() * 2, hipMemcpyHostToDevice));
+      CK(hipMemcpy(d_vpk, vpk.data(), vpk.size() * 8, hipMemcpyHostToDevice));
+      for (int gsz : {2048, 4096, 8192}) {
+        char nm[96];
+        snprintf(nm, 96, "proto packed d16 (8B deltas, 16B vals) grid=%d", gsz);
+        report(nm, S, [&] {
+          hipLaunchKernelGGL((spmv_packed<16>), dim3(gsz), dim3(256), 0, 0, (const int64_t *)A->sptr,
+                             (const int64_t *)d_dp, (const int *)A->swidth, (const uint16_t *)d_dpk,
+                             (const int *)A->scbase, (const double *)d_vpk, ns, n, d_x, d_y);
+        });
+        check(nm, d_y, yref);
+      }
+      CK(hipFree(d_dp));
+      CK(hipFree(d_dpk));
+      CK(hipFree(d_vpk));
     }
   }
   report("CG p pass p = r + om p_old (3 vectors)", 24.0 * n, [&] {
