@@ -219,6 +219,161 @@ __global__ __launch_bounds__(256) void spmv_packed(const int64_t *__restrict__ s
     if (row < n) y[row] = acc;
   }
 }
+
+// ---- probe: the d16 SpMV with the gathers replaced by x[base_j + lane]
+// (contiguous, independent of the per-lane delta load). Wrong result by
+// design; isolates what the data-dependent gather costs.
+template <int UNR, int MODE>
+__global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                  const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                  const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                  const double *__restrict__ x, double *__restrict__ y) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    unsigned d[UNR];
+    double a[UNR];
+    int b[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool in = u < w;
+      d[u] = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)u * 64 + lane) : 0xFFFFu;
+      a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)u * 64 + lane) : 0.0;
+      b[u] = in ? scbase[(base >> 6) + u] : 0;
+    }
+    double xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (MODE == 0) xv[u] = u < w ? x[b[u] + lane] : 0.0;           // contiguous, delta-independent
+      else if (MODE == 1) xv[u] = 1.0;                               // no gather at all
+      else if (MODE == 2) xv[u] = (u < w && d[u] != 0xFFFFu) ? x[s * 64 + lane] : 0.0;  // delta-dependent
+      else xv[u] = 1.0;  // 3: no gather, no y store; 4: no gather, nontemporal y store
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (d[u] != 0xFFFFu) {
+        const double pr = a[u] * xv[u];
+        acc = acc + pr;
+      }
+    const int64_t row = s * 64 + lane;
+    if (MODE == 3) {
+      if (row < n && acc == 12345.678) y[row] = acc;
+    } else if (MODE == 4) {
+      if (row < n) __builtin_nontemporal_store(acc, y + row);
+    } else if (MODE == 5) {
+      if (row < n) y[(blockIdx.x * 4 + wid) * 64 + lane] = acc;  // same store count, a small L2-resident target
+    } else if (row < n) {
+      y[row] = acc;
+    }
+  }
+}
+
+// ---- prototype: the d16 SpMV with XCD-interleaved slice order. XCD x owns a
+// contiguous 1/8 of the slices (x gathers stay in its L2); inside it the
+// waves take slices round-robin (wave j: start + j, start + j + Wx, ...), so
+// the waves resident at one time stream one compact region of the matrix
+// instead of one region each.
+template <int UNR>
+__global__ __launch_bounds__(256) void spmv_ilv(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                const double *__restrict__ x, double *__restrict__ y) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int nbx = (gridDim.x - xcd + 7) / 8;  // blocks on this XCD group
+  const int64_t s0 = nslices * xcd / 8, s1 = nslices * (xcd + 1) / 8;
+  const int64_t Wx = (int64_t)nbx * 4;
+  for (int64_t s = s0 + (int64_t)idx * 4 + wid; s < s1; s += Wx) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    unsigned d[UNR];
+    double a[UNR];
+    int b[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool in = u < w;
+      d[u] = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)u * 64 + lane) : 0xFFFFu;
+      a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)u * 64 + lane) : 0.0;
+      b[u] = in ? scbase[(base >> 6) + u] : 0;
+    }
+    double xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) xv[u] = (u < w && d[u] != 0xFFFFu) ? x[b[u] + (int)d[u]] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (u < w && d[u] != 0xFFFFu) {
+        const double pr = a[u] * xv[u];
+        acc = acc + pr;
+      }
+    const int64_t row = s * 64 + lane;
+    if (row < n) y[row] = acc;
+  }
+}
+
+// ---- probe: the d16 SpMV with every y store deferred to the end of the
+// wave's slice range (staged in LDS; MODE 0 per-slice 8-B stores at the end,
+// MODE 1 the whole range as 16-B vector stores).
+template <int UNR, int MODE>
+__global__ __launch_bounds__(256) void spmv_defer(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                  const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                  const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                  const double *__restrict__ x, double *__restrict__ y) {
+  __shared__ double ys[4][8 * 64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  int t = 0;
+  for (int64_t s = s_begin; s < s_end; ++s, ++t) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    unsigned d[UNR];
+    double a[UNR];
+    int b[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool in = u < w;
+      d[u] = in ? (unsigned)__builtin_nontemporal_load(sdelta + base + (int64_t)u * 64 + lane) : 0xFFFFu;
+      a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)u * 64 + lane) : 0.0;
+      b[u] = in ? scbase[(base >> 6) + u] : 0;
+    }
+    double xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) xv[u] = (u < w && d[u] != 0xFFFFu) ? x[b[u] + (int)d[u]] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (u < w && d[u] != 0xFFFFu) {
+        const double pr = a[u] * xv[u];
+        acc = acc + pr;
+      }
+    ys[wid][t * 64 + lane] = acc;
+  }
+  const int64_t r0 = s_begin * 64, r1 = s_end * 64 < n ? s_end * 64 : n;
+  if (MODE == 0) {
+    for (int64_t r = r0 + lane; r < r1; r += 64) y[r] = ys[wid][r - r0];
+  } else {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    for (int64_t r = r0 + 2 * lane; r < r1; r += 128) {
+      if (r + 1 < r1) *reinterpret_cast<d2 *>(y + r) = d2{ys[wid][r - r0], ys[wid][r - r0 + 1]};
+      else y[r] = ys[wid][r - r0];
+    }
+  }
+}
 __global__ __launch_bounds__(256) void pupdate_kernel(const double *__restrict__ r, const double *__restrict__ pold,
                                                       const double *__restrict__ om, double *__restrict__ p,
                                                       int64_t n) {
@@ -1117,6 +1272,46 @@ int main(int argc, char **argv) {
       CK(hipFree(d_dpk));
       CK(hipFree(d_vpk));
     }
+  }
+  for (int gsz : {1024, 1280, 2048, 4096, 8192}) {
+    char nm[96];
+    snprintf(nm, 96, "proto XCD-interleaved d16 grid=%d", gsz);
+    report(nm, S, [&] {
+      hipLaunchKernelGGL((spmv_ilv<16>), dim3(gsz), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                         (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices, n,
+                         d_x, d_y);
+    });
+    check(nm, d_y, yref);
+  }
+  for (int mode = 0; mode < 2; ++mode) {
+    char nm[96];
+    snprintf(nm, 96, "proto deferred y stores mode %d", mode);
+    if ((A->nslices + 32767) / 32768 > 8) break;
+    report(nm, S, [&] {
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(8192), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                           (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices, n,
+                           d_x, d_y);
+      };
+      if (mode == 0) go(spmv_defer<16, 0>);
+      else go(spmv_defer<16, 1>);
+    });
+    check(nm, d_y, yref);
+  }
+  for (int mode = 1; mode < 6; mode += (mode == 1 ? 2 : 1)) {
+    char nm[96];
+    snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather" : mode == 3 ? "no gather, no store" : mode == 4 ? "no gather, nt store" : "no gather, store to 8 MB");
+    report(nm, S, [&] {
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(8192), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                           (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices, n,
+                           d_x, d_y);
+      };
+      if (mode == 1) go(spmv_probe<16, 1>);
+      else if (mode == 3) go(spmv_probe<16, 3>);
+      else if (mode == 4) go(spmv_probe<16, 4>);
+      else go(spmv_probe<16, 5>);
+    });
   }
   report("CG p pass p = r + om p_old (3 vectors)", 24.0 * n, [&] {
     hipLaunchKernelGGL(pupdate_kernel, dim3(4096), dim3(256), 0, 0, d_x, d_x, d_om, d_y, n);
