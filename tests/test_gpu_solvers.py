@@ -295,3 +295,31 @@ def test_return_arnoldi(name):
     Hg, Hr = np.asarray(H), d[p + "_H"]
     assert Hg.shape == Hr.shape
     np.testing.assert_allclose(Hg, Hr, rtol=1e-8, atol=1e-8 * np.abs(Hr).max())
+
+
+@pytest.mark.parametrize("k", [1, 4])
+@pytest.mark.parametrize("ortho", ["mgs", "mgs2"])
+def test_gmres_persistent_mgs_matches_pass_kernels(monkeypatch, k, ortho):
+    """The persistent MGS kernel (w in registers, one launch per Arnoldi step,
+    granule all-gather for k = 1, counter barrier for k > 1) against the
+    one-launch-per-pass MGS kernels (KRY_MGS_PERSIST=0): the same step count
+    and histories to round-off (the two reduce the inner products in
+    different fixed orders), and the oracle."""
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref
+
+    R = problems.random_nonsym(200_000)
+    A = krylov_amd.CsrOperator(R)
+    b = np.ones(R.shape[0]) if k == 1 else np.random.default_rng(7).standard_normal((R.shape[0], k))
+    _, fast = krylov_amd.gmres(A, b, ortho=ortho, maxiter=30, tol=1e-9)
+    monkeypatch.setenv("KRY_MGS_PERSIST", "0")
+    _, slow = krylov_amd.gmres(A, b, ortho=ortho, maxiter=30, tol=1e-9)
+    assert fast.numsteps == slow.numsteps
+    f, s = np.asarray(fast.resnorms), np.asarray(slow.resnorms)
+    np.testing.assert_allclose(f[:-1], s[:-1], rtol=1e-11)
+    np.testing.assert_allclose(fast.xk, slow.xk, rtol=1e-9, atol=1e-12)
+    if k == 1 and ortho == "mgs":
+        _, ref = krylov_ref.gmres(R, b, maxiter=30, tol=1e-9)
+        assert ref.numsteps == fast.numsteps
+        np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
