@@ -60,6 +60,9 @@ enum {
   M_Z0, M_Z1, M_Z2, M_ZY, M_CRIT, M_TMP, M_COUNT
 };
 
+// store = 0 (no preconditioner M, so p is the v the update pass reads
+// anyway): only the <Av, Av> partials; the update pass recomputes
+// Av - alpha p with the same operations instead of re-reading a stored copy.
 template <typename V, typename S>
 struct OpLanczosOrtho {
   V *w;
@@ -67,6 +70,7 @@ struct OpLanczosOrtho {
   const double *alpha;
   const double *wt;
   int k;
+  int store;
   __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&acc)[Vec16<V>::W]) const {
     constexpr int W = Vec16<V>::W;
     V wv[W], pv[W];
@@ -82,21 +86,22 @@ struct OpLanczosOrtho {
         acc[v] += wt ? dterm_w(d, wt[(e + v) / k], d) : dterm(d, d);
       }
     }
-    VIO<V>::store(w, e, N, wv);
+    if (store) VIO<V>::store(w, e, N, wv);
   }
 };
 
-template <typename V>
+template <typename V, typename S>
 struct OpMinresUpdate {
   const V *vold;   // the v this step multiplied (minres.py:187)
   const double *W0;
   double *W1z;     // holds W[0] on entry; receives z (becomes the new W[1])
   const double *W1;
   V *yk;
-  const V *wv;
+  const V *wv;     // Av, or Av - alpha p when ortho_here == 0
   V *pnew;         // null when the space is invariant
   const double *scal;
   int k;
+  int ortho_here;  // apply Av -= alpha p here (p = vold; arnoldi.py:264)
   __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
     constexpr int W = Vec16<V>::W;
     V va[W], ya[W], wa[W];
@@ -115,7 +120,14 @@ struct OpMinresUpdate {
       W1z[e + v] = z;
       const double dy = y0 * z;
       ya[v] = (V)((double)ya[v] + dy);                     // minres.py:221
-      if (pnew) wa[v] = wa[v] / (V)scal[M_HSAFE * k + c]; // arnoldi.py:276-277
+      if (pnew) {
+        if (ortho_here) {  // the same operations as OpLanczosOrtho
+          const S a = (S)scal[M_ALPHA * k + c];
+          const S t = a * (S)va[v];
+          wa[v] = (V)((S)wa[v] - t);
+        }
+        wa[v] = wa[v] / (V)scal[M_HSAFE * k + c];  // arnoldi.py:276-277
+      }
     }
     VIO<V>::store(yk, e, N, ya);
     if (pnew) VIO<V>::store(pnew, e, N, wa);
@@ -356,7 +368,7 @@ void mr_run_typed(kry_minres *s, int max_steps) {
       mr_apply_op<V, MV, I>(s, v, EpiLanczos<V>{w, v, pold, s->scal + M_H0 * k, s->w, k}, partA, &PA, s->ctrl, step);
     }
     hipLaunchKernelGGL((mr_alpha_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
-    PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, p, s->scal + M_ALPHA * k, s->w, k},
+    PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, p, s->scal + M_ALPHA * k, s->w, k, s->M ? 1 : 0},
                                s->M ? nullptr : partB, s->ctrl, step, st);
     if (s->M)  // MAv = M Av, h[2] = sqrt(<Av, MAv>) (arnoldi.py:268-269)
       launch_spmv_any<V>(s->M, k, SrcPlain<V>{w, k}, EpiStoreDot<V>{static_cast<V *>(s->mw), w, s->w, k}, partB, &PB,
@@ -376,8 +388,8 @@ void mr_run_typed(kry_minres *s, int max_steps) {
     {
       ProfScope ps(s->ctx, PROF_UPDATE);
       launch_elementwise<V>(N, k,
-                            OpMinresUpdate<V>{v, s->W[f], s->W[f], s->W[f ^ 1], static_cast<V *>(s->yk), w, pnew,
-                                              s->scal, k},
+                            OpMinresUpdate<V, S>{v, s->W[f], s->W[f], s->W[f ^ 1], static_cast<V *>(s->yk), w,
+                                                 pnew, s->scal, k, s->M ? 0 : 1},
                             nullptr, s->ctrl, step, st);
     }
     if (s->M)  // v = MAv / guard(h[2]) (arnoldi.py:277)
