@@ -172,6 +172,12 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done,
 int kry_gmres_solution(kry_gmres *s);
 int kry_gmres_residual(kry_gmres *s, double *resnorm);
 int kry_gmres_get(kry_gmres *s, int which, void *host);
+/* multi_solve_triangular (gmres.py:24-38) as a standalone call: per column c
+ * of k, out[:, c] = R[:, :, c]^-1 y[:, c] for upper-triangular R (m x m x k,
+ * C order) and y (m x k), host float64 arrays; arithmetic in `dtype`
+ * (dtrtrs / strtrs). Zero rhs -> 0; KRY_ENONFINITE, KRY_ESINGULAR as LAPACK. */
+int kry_trsv_upper(kry_ctx *ctx, int32_t m, int32_t k, int dtype, const double *R, const double *y,
+                   double *out);
 
 /* ---- MINRES (minres.py:28-253, ArnoldiLanczos arnoldi.py:203-281) --------
  * set_preconditioners: M, Ml, Mr as device operators (NULL = identity);

@@ -1526,4 +1526,59 @@ int kry_gmres_attach_comm(kry_gmres *s, kry_comm *c, int32_t col_offset, int32_t
   KRY_API_END
 }
 
+// multi_solve_triangular (gmres.py:24-38) as a standalone device call: per
+// column c of k, yy = R[:, :, c]^-1 y[:, c] for upper-triangular R (m x m x k,
+// C order) and y (m x k), with the reference's semantics (zero rhs -> 0,
+// non-finite input -> KRY_ENONFINITE, zero diagonal -> KRY_ESINGULAR). The
+// arithmetic runs in `dtype` (float64 / float32, as scipy's dtrtrs / strtrs);
+// host arrays are float64.
+int kry_trsv_upper(kry_ctx *ctx, int32_t m, int32_t k, int dtype, const double *R, const double *y, double *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && R && y && out && m >= 1 && k >= 1, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(dtype == KRY_F64 || dtype == KRY_F32, KRY_EINVAL, "dtype must be float64 or float32");
+  KRY_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const size_t rb = (size_t)m * m * k * 8, yb = (size_t)m * k * 8;
+  double *dR = static_cast<double *>(dev_alloc(rb));
+  double *dy = nullptr, *dout = nullptr;
+  Ctrl *c = nullptr;
+  try {
+    dy = static_cast<double *>(dev_alloc(yb));
+    dout = static_cast<double *>(dev_alloc(yb));
+    c = static_cast<Ctrl *>(dev_alloc(sizeof(Ctrl)));
+    reset_ctrl(c, st);
+    KRY_HIP(hipMemcpyAsync(dR, R, rb, hipMemcpyHostToDevice, st));
+    KRY_HIP(hipMemcpyAsync(dy, y, yb, hipMemcpyHostToDevice, st));
+    auto go = [&](auto s0) {
+      using S = decltype(s0);
+      if (m <= 64)
+        hipLaunchKernelGGL(gm_trsv_kernel<S>, dim3(k), dim3(64), 0, st, (const double *)dR, (const double *)dy, dout,
+                           m, k, m, c);
+      else
+        hipLaunchKernelGGL(gm_trsv_big_kernel<S>, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                           (const double *)dR, (const double *)dy, dout, m, k, m, c);
+    };
+    if (dtype == KRY_F64) go(0.0);
+    else go(0.0f);
+    KRY_HIP(hipGetLastError());
+    Ctrl hc;
+    KRY_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipMemcpyAsync(out, dout, yb, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+    if (hc.status == KRY_ESINGULAR) throw Error{KRY_ESINGULAR, "singular matrix: resolution failed at a zero diagonal"};
+    if (hc.status == KRY_ENONFINITE) throw Error{KRY_ENONFINITE, "array must not contain infs or NaNs"};
+  } catch (...) {
+    dev_free(dR);
+    dev_free(dy);
+    dev_free(dout);
+    dev_free(c);
+    throw;
+  }
+  dev_free(dR);
+  dev_free(dy);
+  dev_free(dout);
+  dev_free(c);
+  KRY_API_END
+}
+
 }  // extern "C"

@@ -17,6 +17,39 @@ from ._helpers import Info, Problem
 from ._lib import check, lib
 
 
+def multi_solve_triangular(A, B, device=None):
+    """``multi_solve_triangular`` (reference ``gmres.py:24-38``) on the GPU:
+    for every trailing column c, solve the upper-triangular ``A[:, :, c] y =
+    B[:, c]`` (``kry_trsv_upper``). All-zero right-hand sides give zeros;
+    non-finite input raises ``ValueError`` and a zero diagonal
+    ``numpy.linalg.LinAlgError``, as ``scipy.linalg.solve_triangular`` does."""
+    from .device import get_context
+
+    A = np.asarray(A)
+    B = np.asarray(B)
+    m = A.shape[0]
+    a = A.reshape(A.shape[0], A.shape[1], -1)
+    b = B.reshape(B.shape[0], -1)
+    if a.shape[0] != a.shape[1] or b.shape[0] != m or b.shape[1] != a.shape[2]:
+        raise ValueError(f"shapes {A.shape} and {B.shape} do not match")
+    if np.iscomplexobj(a) or np.iscomplexobj(b):
+        raise TypeError("complex systems are outside the MI355X path")
+    k = a.shape[2]
+    dt = np.result_type(a.dtype, b.dtype, np.float32)
+    work = np.float32 if dt == np.float32 else np.float64
+    out = np.empty((m, k))
+    if m > 0 and k > 0:
+        ctx = get_context(device)
+        check(lib.kry_trsv_upper(ctx.handle, m, k, _lib.dtype_code(work),
+                                 _lib.dptr(np.ascontiguousarray(a, dtype=np.float64)),
+                                 _lib.dptr(np.ascontiguousarray(b, dtype=np.float64)), _lib.dptr(out)))
+    # the reference stacks per-column results: float32 solves next to float64
+    # zero columns promote to float64
+    zero_cols = np.all(b == 0.0, axis=0)
+    res_dt = work if (work == np.float64 or not zero_cols.any()) else np.float64
+    return out.astype(res_dt).reshape([A.shape[0]] + list(A.shape[2:]))
+
+
 class _GmresState:
     def __init__(self, prob, maxiter, sweeps):
         self.prob = prob

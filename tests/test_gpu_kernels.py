@@ -299,3 +299,45 @@ def test_operator_upload_cache():
     B = A.copy()
     assert krylov_amd.as_device_operator(B) is not op2  # another object: its own upload
     krylov_amd.clear_operator_cache()
+
+
+@pytest.mark.parametrize("m,k", [(1, 1), (5, 3), (30, 1), (64, 4), (90, 2)])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_multi_solve_triangular(m, k, dtype):
+    """gmres.py:24-38 on the device against scipy.linalg.solve_triangular per
+    column (the reference's own loop); zero right-hand sides give zeros."""
+    import scipy.linalg
+
+    import krylov_amd
+
+    rng = np.random.default_rng(m * 10 + k)
+    R = np.triu(rng.standard_normal((m, m, k)).transpose(2, 0, 1)).transpose(1, 2, 0).astype(dtype)
+    for c in range(k):
+        R[np.arange(m), np.arange(m), c] += np.sign(R[np.arange(m), np.arange(m), c]) * 3.0
+    y = rng.standard_normal((m, k)).astype(dtype)
+    if k > 1:
+        y[:, 1] = 0.0
+    got = krylov_amd.multi_solve_triangular(R, y)
+    ref = np.array([np.zeros(m) if np.all(y[:, c] == 0) else scipy.linalg.solve_triangular(R[:, :, c], y[:, c])
+                    for c in range(k)]).T
+    assert got.shape == ref.shape and got.dtype == ref.dtype
+    tol = 1e-12 if dtype == np.float64 else 1e-4
+    np.testing.assert_allclose(got, ref, rtol=tol, atol=tol * np.abs(ref).max())
+    if k > 1:
+        assert np.all(got[:, 1] == 0.0)
+
+
+def test_multi_solve_triangular_errors():
+    import krylov_amd
+
+    R = np.triu(np.ones((4, 4, 1)).transpose(2, 0, 1)).transpose(1, 2, 0)
+    y = np.ones((4, 1))
+    bad = R.copy()
+    bad[2, 2, 0] = 0.0
+    with pytest.raises(np.linalg.LinAlgError):
+        krylov_amd.multi_solve_triangular(bad, y)
+    nan = R.copy()
+    nan[0, 3, 0] = np.nan
+    with pytest.raises(ValueError):
+        krylov_amd.multi_solve_triangular(nan, y)
+    np.testing.assert_array_equal(krylov_amd.multi_solve_triangular(bad, np.zeros((4, 1))), np.zeros((4, 1)))
