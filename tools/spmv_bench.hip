@@ -579,6 +579,171 @@ __global__ __launch_bounds__(kBlock) void spmv_cbq_kernel(int nb, int64_t n, int
   }
 }
 
+
+// ---- calibration: random 8-B gathers from an L2-sized window. Each lane
+// performs G gathers per round at hashed indices in [0, span); returns the
+// chip-wide gather rate (gathers / s) — the ceiling a random-column SpMV's x
+// gathers run against.
+template <int G>
+__global__ __launch_bounds__(256) void gather_calib(const double *__restrict__ x, int64_t span, int rounds,
+                                                    double *out) {
+  uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u + 12345u;
+  double s = 0.0;
+  for (int r = 0; r < rounds; ++r) {
+    double v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+      v[g] = x[h % (uint32_t)span];
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) s += v[g];
+  }
+  if (s == 12345.678) out[0] = s;
+}
+
+// ---- prototype: column-blocked SpMV with owner-contiguous segments. Block b
+// owns rows [b * RB, (b + 1) * RB) (RB = 256 * RPT); for column block c its
+// entries are one contiguous segment, processed in chunks of 256 * GPT
+// entries (GPT gathers per thread in flight), products staged in LDS; thread
+// t owns rows b * RB + t + 256 i (i < RPT) and adds each row's products to
+// its running sum in stored order (bitwise csr_matvec).
+template <int RPT, int GPT>
+__global__ __launch_bounds__(256) void spmv_cbo(int nb, int64_t n, const int64_t *__restrict__ seg,
+                                                const uint16_t *__restrict__ roff, const int *__restrict__ col,
+                                                const double *__restrict__ val, const double *__restrict__ x,
+                                                double *__restrict__ y) {
+  constexpr int RB = 256 * RPT, CH = 256 * GPT;
+  __shared__ double prod[CH];
+  const int tid = threadIdx.x;
+  const int64_t rbase = (int64_t)blockIdx.x * RB;
+  double acc[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) acc[i] = 0.0;
+  for (int c = 0; c < nb; ++c) {
+    const int64_t s0 = seg[(int64_t)c * gridDim.x + blockIdx.x];
+    const int len = (int)(seg[(int64_t)c * gridDim.x + blockIdx.x + 1] - s0);
+    int r0[RPT], r1[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int lr = tid + 256 * i;  // local row
+      const int64_t row = rbase + lr;
+      r0[i] = r1[i] = 0;
+      if (row < n) {
+        r0[i] = roff[(int64_t)c * gridDim.x * (RB + 1) + (int64_t)blockIdx.x * (RB + 1) + lr];
+        r1[i] = roff[(int64_t)c * gridDim.x * (RB + 1) + (int64_t)blockIdx.x * (RB + 1) + lr + 1];
+      }
+    }
+    for (int c0 = 0; c0 < len; c0 += CH) {
+      const int c1 = len < c0 + CH ? len : c0 + CH;
+      int j[GPT];
+      double a[GPT];
+#pragma unroll
+      for (int u = 0; u < GPT; ++u) {
+        const int e = c0 + tid + u * 256;
+        j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
+        a[u] = e < c1 ? __builtin_nontemporal_load(val + s0 + e) : 0.0;
+      }
+      double xj[GPT];
+#pragma unroll
+      for (int u = 0; u < GPT; ++u) xj[u] = j[u] >= 0 ? x[j[u]] : 0.0;
+      __syncthreads();  // the previous chunk's products are consumed
+#pragma unroll
+      for (int u = 0; u < GPT; ++u)
+        if (j[u] >= 0) prod[tid + u * 256] = a[u] * xj[u];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int lo = r0[i] > c0 ? r0[i] : c0, hi = r1[i] < c1 ? r1[i] : c1;
+        for (int e = lo; e < hi; ++e) acc[i] = acc[i] + prod[e - c0];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int64_t row = rbase + tid + 256 * i;
+    if (row < n) y[row] = acc[i];
+  }
+}
+
+template <int RPT, int GPT>
+static void cbo_study(int64_t n, const std::vector<int> &ip, const std::vector<int> &ix,
+                      const std::vector<double> &dv, const std::vector<double> &yref, const double *d_x, double *d_y,
+                      int reps, hipEvent_t a, hipEvent_t b, int64_t cols) {
+  constexpr int RB = 256 * RPT;
+  const int G = (int)((n + RB - 1) / RB);
+  const int nb = (int)((n + cols - 1) / cols);
+  // segments: (c, block) -> contiguous entries; roff per (c, block, local row)
+  std::vector<int64_t> seg((size_t)nb * G + 1, 0);
+  std::vector<uint16_t> roff((size_t)nb * G * (RB + 1), 0);
+  std::vector<int64_t> cnt((size_t)nb * G, 0);
+  for (int64_t r = 0; r < n; ++r)
+    for (int e = ip[r]; e < ip[r + 1]; ++e) cnt[(size_t)(ix[e] / cols) * G + r / RB]++;
+  for (size_t i = 0; i < cnt.size(); ++i) seg[i + 1] = seg[i] + cnt[i];
+  std::vector<int> col(ip[n]);
+  std::vector<double> val(ip[n]);
+  std::vector<int64_t> pos(seg.begin(), seg.end() - 1);
+  bool fits = true;
+  for (int64_t r = 0; r < n; ++r) {
+    const int blk = (int)(r / RB), lr = (int)(r % RB);
+    for (int c = 0; c < nb; ++c) {
+      const int64_t off = pos[(size_t)c * G + blk] - seg[(size_t)c * G + blk];
+      if (off > 65535) fits = false;
+      roff[((size_t)c * G + blk) * (RB + 1) + lr] = (uint16_t)off;
+    }
+    for (int e = ip[r]; e < ip[r + 1]; ++e) {
+      const int c = ix[e] / cols;
+      const int64_t p = pos[(size_t)c * G + blk]++;
+      col[p] = ix[e];
+      val[p] = dv[e];
+    }
+  }
+  for (int blk = 0; blk < G; ++blk)
+    for (int c = 0; c < nb; ++c) {
+      const int64_t rows = std::min<int64_t>(RB, n - (int64_t)blk * RB);
+      for (int64_t lr = rows; lr <= RB; ++lr)
+        roff[((size_t)c * G + blk) * (RB + 1) + lr] = (uint16_t)(seg[(size_t)c * G + blk + 1] - seg[(size_t)c * G + blk]);
+    }
+  if (!fits) { printf("cbo RPT=%d: segment too long\n", RPT); return; }
+  int64_t *d_seg; uint16_t *d_roff; int *d_col; double *d_val;
+  CK(hipMalloc(&d_seg, seg.size() * 8));
+  CK(hipMalloc(&d_roff, roff.size() * 2));
+  CK(hipMalloc(&d_col, col.size() * 4 + 4096));
+  CK(hipMalloc(&d_val, val.size() * 8 + 8192));
+  CK(hipMemcpy(d_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_roff, roff.data(), roff.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_col, col.data(), col.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_val, val.data(), val.size() * 8, hipMemcpyHostToDevice));
+  auto launch = [&] {
+    hipLaunchKernelGGL((spmv_cbo<RPT, GPT>), dim3(G), dim3(256), 0, 0, nb, n, (const int64_t *)d_seg,
+                       (const uint16_t *)d_roff, (const int *)d_col, (const double *)d_val, d_x, d_y);
+  };
+  CK(hipMemset(d_y, 0, n * 8));
+  launch();
+  CK(hipDeviceSynchronize());
+  float tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(a, 0));
+    launch();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    tot += ms;
+  }
+  std::vector<double> h(n);
+  CK(hipMemcpy(h.data(), d_y, n * 8, hipMemcpyDeviceToHost));
+  int64_t bad = 0;
+  for (int64_t i = 0; i < n; ++i) bad += memcmp(&h[i], &yref[i], 8) != 0;
+  printf("cbo cols=%ld RPT=%d GPT=%d grid=%d nb=%d: %.4f ms  bitwise mismatches %ld\n", cols, RPT, GPT, G, nb,
+         tot / reps, bad);
+  CK(hipFree(d_seg)); CK(hipFree(d_roff)); CK(hipFree(d_col)); CK(hipFree(d_val));
+}
+// probe epilogue: no store, the value only feeds a dot partial
+struct EpiNoStore {
+  __device__ __forceinline__ double operator()(int64_t i, int c, double s, double xi) const { return s * s; }
+};
+
 // Column-blocked image tuning on the cfg3 pattern: block width x launch grid.
 static int cb_tune(int64_t n, int reps) {
   kry_ctx *ctx;
@@ -625,6 +790,79 @@ static int cb_tune(int64_t n, int reps) {
     for (int64_t i = 0; i < n; ++i) bad += memcmp(&h[i], &yref[i], 8) != 0;
     printf("  %s: bitwise mismatches %ld\n", what, bad);
   };
+  {
+    // epilogue cost on the single-launch kernel (default image): y store,
+    // y + V store + dot (the GMRES form), and no store at all
+    kry_csr *A;
+    KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+    double *d_v, *d_part, *d_hs;
+    CK(hipMalloc(&d_v, n * 8));
+    CK(hipMalloc(&d_part, kMaxGrid * 8));
+    CK(hipMalloc(&d_hs, 64));
+    const double one = 1.0;
+    CK(hipMemcpy(d_hs, &one, 8, hipMemcpyHostToDevice));
+    const int grid = (int)std::min<int64_t>(A->cb_ng, kCbPersistGrid);
+    auto timeit = [&](const char *name, auto &&launch) {
+      launch();
+      CK(hipDeviceSynchronize());
+      float tot = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+      }
+      printf("cb epilogue %-40s %.4f ms\n", name, tot / reps);
+    };
+    auto cbp = [&](auto src, auto epi, double *part) {
+      hipLaunchKernelGGL((spmv_cbp_kernel<double, double, decltype(src), decltype(epi)>), dim3(grid), dim3(kBlock), 0,
+                         0, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr, (const uint16_t *)A->cb_roff,
+                         (const int *)A->cb_col, (const double *)A->cb_val, src, epi, part, (const Ctrl *)nullptr, 0);
+    };
+    timeit("store y", [&] { cbp(SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr); });
+    timeit("store y + V, <q, y> (GMRES)", [&] {
+      cbp(SrcScaled<double>{d_x, d_hs, 1}, EpiStoreDotV<double>{d_y, d_x, d_v, nullptr, 1}, d_part);
+    });
+    timeit("store y, <q, y>", [&] { cbp(SrcPlain<double>{d_x, 1}, EpiStoreDot<double>{d_y, d_x, nullptr, 1}, d_part); });
+    timeit("no store, <y, y>", [&] { cbp(SrcPlain<double>{d_x, 1}, EpiNoStore{}, d_part); });
+    KC(kry_csr_destroy(A));
+    CK(hipFree(d_v));
+    CK(hipFree(d_part));
+    CK(hipFree(d_hs));
+  }
+  cbo_study<8, 8>(n, ip, ix, dv, yref, d_x, d_y, reps, a, b, 262144);
+  cbo_study<8, 4>(n, ip, ix, dv, yref, d_x, d_y, reps, a, b, 262144);
+  cbo_study<4, 8>(n, ip, ix, dv, yref, d_x, d_y, reps, a, b, 262144);
+  cbo_study<8, 16>(n, ip, ix, dv, yref, d_x, d_y, reps, a, b, 262144);
+  cbo_study<8, 8>(n, ip, ix, dv, yref, d_x, d_y, reps, a, b, 131072);
+  {
+    double *d_out;
+    CK(hipMalloc(&d_out, 64));
+    for (int64_t span : {(int64_t)4096, (int64_t)262144, (int64_t)2000000}) {
+      for (int grid : {2048, 8192}) {
+        const int rounds = 64;
+        hipLaunchKernelGGL((gather_calib<8>), dim3(grid), dim3(256), 0, 0, d_x, span, rounds, d_out);
+        CK(hipDeviceSynchronize());
+        float tot = 0;
+        for (int r = 0; r < reps; ++r) {
+          CK(hipEventRecord(a, 0));
+          hipLaunchKernelGGL((gather_calib<8>), dim3(grid), dim3(256), 0, 0, d_x, span, rounds, d_out);
+          CK(hipEventRecord(b, 0));
+          CK(hipEventSynchronize(b));
+          float ms;
+          CK(hipEventElapsedTime(&ms, a, b));
+          tot += ms;
+        }
+        const double ng = (double)grid * 256 * rounds * 8;
+        printf("gather calib span %ld doubles (%.1f MB) grid %d: %.4f ms, %.1f G gathers/s (40M gathers -> %.1f us)\n",
+               span, span * 8 / 1e6, grid, tot / reps, ng / (tot / reps) / 1e6, 40e6 / (ng / (tot / reps) / 1e3) * 1e3);
+      }
+    }
+    CK(hipFree(d_out));
+  }
   for (const char *cols : {"131072", "262144", "524288"}) {
     setenv("KRY_CB_COLS", cols, 1);
     kry_csr *A;
