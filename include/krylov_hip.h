@@ -160,7 +160,11 @@ int kry_cg_scalars(kry_cg *s, double *out);
  *         invariant (*invariant = 1). Returns KRY_EINVARIANT if called after
  *         an invariant step (arnoldi.py:168-171).
  * solution: xk = x0 + sum_i yy_i V_i with yy = R^-1 y (gmres.py:89-99),
- *         left on device; residual: explicit ||b - A xk||. */
+ *         left on device; residual: explicit ||b - A xk||.
+ * get:    which = 0: xk (after solution); 1: the basis V_0..V_m and 2: P_0..P_m
+ *         (m = steps, or steps - 1 after an invariant step; n x k each, packed);
+ *         3: the Hessenberg matrix H, (maxiter + 1) x maxiter x k (ArnoldiMGS /
+ *         ArnoldiHouseholder state, arnoldi.py:33-200). */
 int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t maxiter,
                      int32_t sweeps, kry_gmres **out);
 int kry_gmres_destroy(kry_gmres *s);

@@ -13,7 +13,7 @@ from .cg import cg
 from .errors import ArgumentError
 from .extra import bicgstab, cgr, cgs, gcr
 from .givens import givens, lartg
-from .gmres import gmres, gmres_restarted, multi_solve_triangular
+from .gmres import arnoldi, gmres, gmres_restarted, multi_solve_triangular
 from .minres import minres
 from .sparse import CsrOperator, as_device_operator, clear_operator_cache
 
@@ -24,6 +24,7 @@ __all__ = [
     "gmres",
     "gmres_restarted",
     "multi_solve_triangular",
+    "arnoldi",
     "minres",
     "bicgstab",
     "cgs",

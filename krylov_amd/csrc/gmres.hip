@@ -50,6 +50,7 @@ struct kry_gmres {
   double *scal = nullptr;  // alpha[k], hsafe[k], crit[k], tmp[k]
   double *h = nullptr;     // (maxiter + 2) x k, current Arnoldi column
   double *R = nullptr;     // (maxiter + 1) x maxiter x k
+  double *Hs = nullptr;    // (maxiter + 1) x maxiter x k: the Hessenberg columns before rotation
   double *y = nullptr;     // (maxiter + 1) x k
   double *Gc = nullptr, *Gs = nullptr;  // maxiter x k rotations
   double *yy = nullptr;    // maxiter x k triangular-solve result
@@ -562,7 +563,8 @@ __global__ void gm_coef_kernel(const double *part, int P, int k, double *scal, d
 template <typename S>
 __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, double *h, double *R, double *y,
                              double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step,
-                             int hgiven = 0, double *gbuf = nullptr, int col_offset = 0, int total_k = 0) {
+                             int hgiven = 0, double *gbuf = nullptr, int col_offset = 0, int total_k = 0,
+                             double *Hs = nullptr) {
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock];
   __shared__ double rn[kMaxCols];
@@ -574,6 +576,8 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
     const S hk1 = hgiven ? (S)h[(int64_t)(col + 1) * k + c] : sqrt((S)red[c]);
     h[(int64_t)(col + 1) * k + c] = (double)hk1;
     red[c] = (double)hk1;
+    if (Hs)  // the Arnoldi relation's H[:col+2, col] (the reference's h column)
+      for (int i = 0; i <= col + 1; ++i) Hs[i * ld + (int64_t)col * k + c] = h[(int64_t)i * k + c];
   }
   __syncthreads();
   // np.all(h[k+1] <= 1e-14) over the columns (arnoldi.py:187)
@@ -1017,7 +1021,8 @@ void hh_run_impl(kry_gmres *s, int max_steps) {
                        more ? (const V *)U(k + 1) : (const V *)nullptr, k, N, (const double *)hh(more ? k + 1 : 0),
                        (const double *)pout, G, s->h, s->ctrl, step);
     hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, (const double *)nullptr, 0, 1, s->scal, s->h,
-                       s->R, s->y, s->Gc, s->Gs, (int)k, s->maxiter, s->hist, s->ctrl, step, 1);
+                       s->R, s->y, s->Gc, s->Gs, (int)k, s->maxiter, s->hist, s->ctrl, step, 1, (double *)nullptr, 0,
+                       0, s->Hs);
     KRY_HIP(hipGetLastError());
     if (!more) continue;  // invariant: no new basis vector
     // vnew = e_{k+1}; vnew[j:] = H_j vnew[j:] for j = k+1..0; V_{k+1} = vnew alpha_{k+1}
@@ -1100,7 +1105,7 @@ void gm_qr_step(kry_gmres *s, const double *pin, int P, int col, int step) {
   const int k = s->k;
   hipLaunchKernelGGL(gm_qr_kernel<V>, dim3(1), dim3(kBlock), 0, st, pin, P, k, s->scal, s->h, s->R, s->y, s->Gc,
                      s->Gs, col, s->maxiter, s->hist, s->ctrl, step, 0, s->comm ? s->gbuf : nullptr, s->col_offset,
-                     s->total_k);
+                     s->total_k, s->Hs);
   KRY_HIP(hipGetLastError());
   if (!s->comm) return;
   ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
@@ -1249,7 +1254,7 @@ void gm_residual_impl(kry_gmres *s, double *norm2) {
 void gm_free(kry_gmres *s) {
   void *bufs[] = {s->b,  s->x0,   s->V,     s->wv,   s->xk,   s->rt, s->w,  s->part, s->part1, s->part2,
                   s->scal, s->h, s->R, s->y, s->Gc, s->Gs, s->yy, s->hist, s->ctrl, s->P, s->mw, s->t1, s->t2,
-                  s->U, s->vnew, s->hh, s->wv2, s->bar, s->gbuf, s->gcrit};
+                  s->U, s->vnew, s->hh, s->wv2, s->bar, s->gbuf, s->gcrit, s->Hs};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -1312,6 +1317,8 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     s->scal = static_cast<double *>(dev_alloc(G_COUNT * (size_t)k * 8));
     s->h = static_cast<double *>(dev_alloc(((size_t)maxiter + 2) * k * 8));
     s->R = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8));
+    s->Hs = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8));
+    KRY_HIP(hipMemsetAsync(s->Hs, 0, ((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8, ctx->stream));
     s->y = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
     s->Gc = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
     s->Gs = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * k * 8));
@@ -1489,13 +1496,46 @@ int kry_gmres_residual(kry_gmres *s, double *norm2) {
   KRY_API_END
 }
 
+// which = 0: xk (after kry_gmres_solution); 1: the basis V_0..V_m, 2: P_0..P_m
+// (= V without M), m = steps (steps - 1 after an invariant step), each n x k;
+// 3: the Hessenberg matrix H, (maxiter + 1) x maxiter x k, column j filled
+// for j < steps (arnoldi.py:158-196, the relation A V_m = V_{m+1} H).
 int kry_gmres_get(kry_gmres *s, int which, void *host) {
   KRY_API_BEGIN
-  KRY_REQUIRE(s && host && which == 0, KRY_EINVAL, "bad argument");
-  KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
+  KRY_REQUIRE(s && host && which >= 0 && which <= 3, KRY_EINVAL, "bad argument");
   KRY_HIP(hipSetDevice(s->ctx->device));
-  KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)s->n * s->k * dsize(s->dtype), hipMemcpyDeviceToHost, s->ctx->stream));
-  KRY_HIP(hipStreamSynchronize(s->ctx->stream));
+  hipStream_t st = s->ctx->stream;
+  const size_t vb = (size_t)s->n * s->k * dsize(s->dtype);
+  if (which == 0) {
+    KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
+    KRY_HIP(hipMemcpyAsync(host, s->xk, vb, hipMemcpyDeviceToHost, st));
+  } else if (which == 3) {
+    const int mi = s->maxiter > 0 ? s->maxiter : 1;
+    KRY_HIP(hipMemcpyAsync(host, s->Hs, ((size_t)s->maxiter + 1) * mi * s->k * 8, hipMemcpyDeviceToHost, st));
+  } else {
+    KRY_REQUIRE(s->started, KRY_EINVAL, "solver not started");
+    KRY_REQUIRE(!s->householder || which == 1, KRY_EINVAL, "Householder Arnoldi has no P basis");
+    const int nv = s->steps + (s->invariant ? 0 : 1);
+    if (s->vpending && !s->invariant) {  // V_steps is still w / guard(h[steps]): form it now
+      const int64_t N = s->n * (int64_t)s->k;
+      const int k = s->k;
+      auto go = [&](auto v0) {
+        using V = decltype(v0);
+        V *wb[2] = {static_cast<V *>(s->wv), static_cast<V *>(s->wv2)};
+        launch_elementwise<V>(N, k,
+                              OpScaleDiv<V>{wb[s->wcur], basis<V>(s->V, s->vstride, s->steps), s->scal + G_HSAFE * k, k},
+                              nullptr, nullptr, 0, st);
+      };
+      if (s->dtype == KRY_F64) go(0.0);
+      else go(0.0f);
+    }
+    const void *base = (which == 2 && s->M) ? s->P : s->V;
+    const size_t stride = s->vstride * dsize(s->dtype);
+    for (int i = 0; i < nv; ++i)
+      KRY_HIP(hipMemcpyAsync(static_cast<char *>(host) + (size_t)i * vb, static_cast<const char *>(base) + i * stride,
+                             vb, hipMemcpyDeviceToHost, st));
+  }
+  KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END
 }
 

@@ -94,6 +94,57 @@ class _GmresState:
         return p.unpad_vec(out, p.r0_dtype)
 
 
+def arnoldi(A, v, maxiter, ortho="mgs", M=None, inner=None):
+    """The device Arnoldi process of ``gmres`` run on its own: ``ArnoldiMGS``
+    (``arnoldi.py:107-200``, ``ortho="mgs"`` / ``"mgsK"``) or
+    ``ArnoldiHouseholder`` (``arnoldi.py:33-104``) from the start vector ``v``
+    for up to ``maxiter`` steps, stopping early at an invariant subspace like
+    the reference's ``while arnoldi.iter < maxiter and not
+    arnoldi.is_invariant`` loop (tests/test_arnoldi.py).
+
+    Returns ``(V, H, P, is_invariant)``: the basis as a list of vectors
+    (``V = M P``), the (steps + 1) x steps Hessenberg matrix (steps x steps
+    after an invariant step), and the ``P`` basis (``P is V`` without M)."""
+    if ortho.startswith("mgs"):
+        sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
+    elif ortho == "householder":
+        assert inner is None and _helpers._is_identity(M)
+        sweeps = 0
+    else:
+        raise ValueError(f"unknown ortho {ortho!r}")
+    v = np.asarray(v)
+    if v.ndim != 1:
+        raise ValueError("arnoldi takes one start vector")
+    prob = Problem(A, v, None, inner, M=M)
+    st = _GmresState(prob, maxiter, sweeps)
+    st.start()
+    st.set_criterion(prob.pad_cols(np.full(prob.kc, -1.0), np.inf))  # never "converged"
+    steps = 0
+    invariant = False
+    while steps < maxiter and not invariant:
+        hist, invariant = st.run(min(_helpers.CHUNK, maxiter - steps))
+        steps += len(hist)
+        if len(hist) == 0:
+            break
+    nv = steps + (0 if invariant else 1)
+    n, kp = prob.n, prob.kpad
+
+    def basis(which):
+        out = np.empty((max(nv, 1), n, kp), dtype=prob.dtype)
+        check(lib.kry_gmres_get(st.h, which, _lib.ptr(out)))
+        return [out[i, :, 0].copy() for i in range(nv)]
+
+    V = basis(1)
+    P = basis(2) if (not _helpers._is_identity(M) and sweeps > 0) else V
+    mi = max(maxiter, 1)
+    Hs = np.empty((maxiter + 1, mi, kp))
+    check(lib.kry_gmres_get(st.h, 3, _lib.ptr(Hs)))
+    H = Hs[: steps + 1, :steps, 0].astype(prob.dtype)
+    if invariant:
+        H = H[:steps]
+    return V, H, P, invariant
+
+
 def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1.0e-15,
           maxiter=None, callback=None):
     """Preconditioned GMRES, reference signature (``gmres.py:41-54``).
