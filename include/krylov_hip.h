@@ -196,6 +196,8 @@ int kry_minres_set_criterion(kry_minres *s, const double *criterion);
 int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done,
                    double *resnorms, int32_t *invariant);
 int kry_minres_residual(kry_minres *s, double *resnorm);
+/* get: which = 0: xk; 1: the current Lanczos vector p; 2: v = M p; 3: the last
+ * step's [h0, h1, h2] (3 x k; ArnoldiLanczos state, arnoldi.py:203-281). */
 int kry_minres_get(kry_minres *s, int which, void *host);
 
 /* ---- multi-GPU: RHS columns sharded one block per GPU ----

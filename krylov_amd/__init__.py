@@ -14,7 +14,7 @@ from .errors import ArgumentError
 from .extra import bicgstab, cgr, cgs, gcr
 from .givens import givens, lartg
 from .gmres import arnoldi, gmres, gmres_restarted, multi_solve_triangular
-from .minres import minres
+from .minres import lanczos, minres
 from .sparse import CsrOperator, as_device_operator, clear_operator_cache
 
 __version__ = "0.1.0"
@@ -25,6 +25,7 @@ __all__ = [
     "gmres_restarted",
     "multi_solve_triangular",
     "arnoldi",
+    "lanczos",
     "minres",
     "bicgstab",
     "cgs",

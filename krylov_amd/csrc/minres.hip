@@ -619,12 +619,27 @@ int kry_minres_residual(kry_minres *s, double *norm2) {
   KRY_API_END
 }
 
+// which = 0: xk = x0 + Mr yk; 1: the current Lanczos vector p (the next step
+// multiplies it); 2: v = M p; 3: the scalars [h0, h1, h2] of the last step
+// (3 x k; h0 already holds the next step's h[0] = this step's h[2]).
 int kry_minres_get(kry_minres *s, int which, void *host) {
   KRY_API_BEGIN
-  KRY_REQUIRE(s && host && which == 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(s && host && which >= 0 && which <= 3, KRY_EINVAL, "bad argument");
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   const int64_t N = s->n * (int64_t)s->k;
+  if (which != 0) {
+    KRY_REQUIRE(s->started, KRY_EINVAL, "kry_minres_start has not been called");
+    if (which == 3) {
+      KRY_HIP(hipMemcpyAsync(host, s->scal + M_H0 * s->k, 3 * (size_t)s->k * 8, hipMemcpyDeviceToHost, st));
+    } else {
+      const void *src = s->P[s->it % 3];
+      if (which == 2 && s->M) src = s->Vr[s->it % 2];
+      KRY_HIP(hipMemcpyAsync(host, src, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
+    }
+    KRY_HIP(hipStreamSynchronize(st));
+    return KRY_OK;
+  }
   if (s->dtype == KRY_F64)
     mr_compute_xk<double>(s);
   else

@@ -54,6 +54,52 @@ class _MinresState:
         return p.unpad_vec(out, p.r0_dtype)
 
 
+def lanczos(A, v, maxiter, M=None, inner=None):
+    """The device Lanczos process of ``minres`` on its own (``ArnoldiLanczos``,
+    ``arnoldi.py:203-281``): up to ``maxiter`` steps from ``v``, stopping at an
+    invariant subspace. Returns ``(V, H, P, is_invariant)`` with the bases as
+    lists of vectors and the (steps + 1) x steps tridiagonal H (steps x steps
+    after an invariant step), as tests/test_arnoldi.py assembles them."""
+    v = np.asarray(v)
+    if v.ndim != 1:
+        raise ValueError("lanczos takes one start vector")
+    prob = Problem(A, v, None, inner, M=M)
+    st = _MinresState(prob)
+    st.start()
+    st.set_criterion(prob.pad_cols(np.full(prob.kc, -1.0), np.inf))  # never "converged"
+
+    def vec(which):
+        out = np.empty((prob.n, prob.kpad), dtype=prob.dtype)
+        check(lib.kry_minres_get(st.h, which, _lib.ptr(out)))
+        return out[:, 0].copy()
+
+    V, P, cols = [vec(2)], [vec(1)], []
+    prev_h2 = 0.0
+    invariant = False
+    for _ in range(maxiter):
+        hist, invariant = st.run(1)
+        if len(hist) == 0:
+            break
+        h = np.empty((3, prob.kpad))
+        check(lib.kry_minres_get(st.h, 3, _lib.dptr(h)))
+        cols.append(np.array([prev_h2, h[1, 0], h[2, 0]]))
+        prev_h2 = h[2, 0]
+        if invariant:
+            break
+        V.append(vec(2))
+        P.append(vec(1))
+    k = len(cols)
+    H = np.zeros((k + 1, k))
+    for i, hv in enumerate(cols):
+        if i == 0:
+            H[:2, 0] = hv[1:]
+        else:
+            H[i - 1:i + 2, i] = hv
+    if invariant:
+        H = H[:k]
+    return V, H.astype(prob.dtype), P, invariant
+
+
 def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None,
            callback=None):
     """Preconditioned MINRES, reference signature (``minres.py:28-40``)."""

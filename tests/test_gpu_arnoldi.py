@@ -73,7 +73,8 @@ def _check(A, v, V, H, P, maxiter, ortho, Bm, weighted):
     else:
         sv = scipy.linalg.svd(np.column_stack([Vm[:, [0]], MAV[:, :-1] if invariant else MAV]), compute_uv=False)
         ortho_tol = np.inf if sv[-1] == 0 else k**2 * N * eps * sv[0] / sv[-1]
-    if ortho != "mgs" or N != k:  # MGS cannot detect an invariant space reliably
+    # MGS (at k = N) and Lanczos cannot detect an invariant space reliably
+    if (ortho != "mgs" or N != k) and ortho != "lanczos":
         assert ortho_res <= ortho_tol
     proj = np.linalg.norm(ip(Pm, MAV) - H, 2)
     assert proj <= max(10 * (ortho_res * An + arnoldi_res * np.sqrt(np.linalg.norm(ip(Vm, Vm), 2))), eps)
@@ -120,3 +121,18 @@ def test_arnoldi_matches_oracle_relation():
     Vm = np.column_stack(V)
     res = R @ Vm[:, :-1] - Vm @ H
     assert np.linalg.norm(res) <= 20 * 5000**1.5 * np.finfo(float).eps * scipy.sparse.linalg.norm(R, 1)
+
+
+@pytest.mark.parametrize("A", [_spd(), _symm_indef()], ids=["spd", "symm_indef"])
+@pytest.mark.parametrize("v", [np.ones(N), _e0()], ids=["ones", "e0"])
+@pytest.mark.parametrize("maxiter", [1, 5, 9, 10])
+@pytest.mark.parametrize("use_m", [False, True])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_arnoldi_lanczos(A, v, maxiter, use_m, weighted):
+    """tests/test_arnoldi.py:125-163 on the MINRES device Lanczos process."""
+    import krylov_amd
+
+    Bm = np.diag(_BDIAG) if use_m else None
+    inner = krylov_amd.WeightedInner(_BDIAG) if weighted else None
+    V, H, P, _ = krylov_amd.lanczos(A, v, maxiter, M=Bm, inner=inner)
+    _check(A, v, V, H, P, maxiter, "lanczos", Bm, weighted)
