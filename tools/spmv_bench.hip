@@ -251,10 +251,9 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
     double xv[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      if (MODE == 0) xv[u] = u < w ? x[b[u] + lane] : 0.0;           // contiguous, delta-independent
-      else if (MODE == 1) xv[u] = 1.0;                               // no gather at all
-      else if (MODE == 2) xv[u] = (u < w && d[u] != 0xFFFFu) ? x[s * 64 + lane] : 0.0;  // delta-dependent
-      else xv[u] = 1.0;  // 3: no gather, no y store; 4: no gather, nontemporal y store
+      // 1: no gather, y stored; 3: no gather, no y store; 4: no gather,
+      // nontemporal y store; 5: no gather, y stored to a small target
+      xv[u] = 1.0;
     }
     double acc = 0.0;
 #pragma unroll
@@ -269,7 +268,9 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
     } else if (MODE == 4) {
       if (row < n) __builtin_nontemporal_store(acc, y + row);
     } else if (MODE == 5) {
-      if (row < n) y[(blockIdx.x * 4 + wid) * 64 + lane] = acc;  // same store count, a small L2-resident target
+      // same store count into a small L2-resident target (bounded by n)
+      const int64_t idx = ((int64_t)blockIdx.x * 4 + wid) * 64 + lane;
+      if (row < n && idx < n) y[idx] = acc;
     } else if (row < n) {
       y[row] = acc;
     }
@@ -1297,7 +1298,50 @@ static int block_study(int m, int k, int reps) {
   return 0;
 }
 
+// The library's CG SpMV (compact image, Ap stored + <p, Ap> partials) alone on
+// the m^3 15-point stencil: `spmv_bench cgonly m reps`.
+static int cg_only(int m, int reps) {
+  std::vector<int> ip, ix;
+  std::vector<double> dv;
+  build_stencil(m, ip, ix, dv);
+  const int64_t n = ip.size() - 1, nnz = ix.size();
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  kry_csr *A;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+  double *d_p, *d_ap, *part;
+  CK(hipMalloc(&d_p, n * 8));
+  CK(hipMalloc(&d_ap, n * 8));
+  CK(hipMalloc(&part, kMaxGrid * 8));
+  CK(hipMemset(d_p, 0, n * 8));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto launch = [&] {
+    launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_p, 1}, EpiApDot<double>{d_ap, nullptr, 1}, part, nullptr,
+                                     nullptr, 0, 0);
+  };
+  launch();
+  CK(hipDeviceSynchronize());
+  float tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(a, 0));
+    launch();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    tot += ms;
+  }
+  printf("cgonly m=%d n=%ld nnz=%ld: CG SpMV %.4f ms\n", m, n, nnz, tot / reps);
+  KC(kry_csr_destroy(A));
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "cgonly") == 0)
+    return cg_only(argc > 2 ? atoi(argv[2]) : 216, argc > 3 ? atoi(argv[3]) : 20);
   if (argc > 1 && strcmp(argv[1], "block") == 0)
     return block_study(argc > 2 ? atoi(argv[2]) : 3163, argc > 3 ? atoi(argv[3]) : 8, 10);
   if (argc > 1 && strcmp(argv[1], "random") == 0) return random_study(argc > 2 ? atol(argv[2]) : 2000000, 10);
