@@ -182,6 +182,10 @@ int kry_gmres_get(kry_gmres *s, int which, void *host);
  * (dtrtrs / strtrs). Zero rhs -> 0; KRY_ENONFINITE, KRY_ESINGULAR as LAPACK. */
 int kry_trsv_upper(kry_ctx *ctx, int32_t m, int32_t k, int dtype, const double *R, const double *y,
                    double *out);
+/* Householder(x) (householder.py:6-53) for one vector (k = 1): v_out = the
+ * normalised reflector vector, out3 = [beta, alpha, xnorm] (H x = alpha xnorm
+ * e_1); the kernels of Householder Arnoldi, arithmetic in x's dtype. */
+int kry_householder(kry_ctx *ctx, kry_vec *x, kry_vec *v_out, double *out3);
 
 /* ---- MINRES (minres.py:28-253, ArnoldiLanczos arnoldi.py:203-281) --------
  * set_preconditioners: M, Ml, Mr as device operators (NULL = identity);

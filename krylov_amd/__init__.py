@@ -13,6 +13,7 @@ from .cg import cg
 from .errors import ArgumentError
 from .extra import bicgstab, cgr, cgs, gcr
 from .givens import givens, lartg
+from .householder import Householder
 from .gmres import arnoldi, gmres, gmres_restarted, multi_solve_triangular
 from .minres import lanczos, minres
 from .sparse import CsrOperator, as_device_operator, clear_operator_cache
@@ -32,6 +33,7 @@ __all__ = [
     "cgr",
     "gcr",
     "givens",
+    "Householder",
     "lartg",
     "CsrOperator",
     "as_device_operator",

@@ -81,6 +81,7 @@ _SIGNATURES = {
     "kry_gmres_set_criterion": [_vp, _dp],
     "kry_gmres_run": [_vp, _i32, _ip32, _dp, _ip32],
     "kry_trsv_upper": [_vp, _i32, _i32, ctypes.c_int, _dp, _dp, _dp],
+    "kry_householder": [_vp, _vp, _vp, _dp],
     "kry_gmres_solution": [_vp],
     "kry_gmres_residual": [_vp, _dp],
     "kry_gmres_get": [_vp, _int, _vp],

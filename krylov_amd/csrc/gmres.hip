@@ -756,7 +756,7 @@ __global__ void gm_trsv_big_kernel(const double *R, const double *y, double *yy,
 // values it was built from. Applying it to x[j:] is x - (beta * u) * <u, x>,
 // each a streaming pass whose <u, x> arrives as block partials from the pass
 // before (fixed-order reduction in every block, as in the MGS passes).
-enum { HH_BETA = 0, HH_ALPHA = 1, HH_V0 = 2, HH_NRM = 3, HH_COUNT = 4 };
+enum { HH_BETA = 0, HH_ALPHA = 1, HH_V0 = 2, HH_NRM = 3, HH_XNORM = 4, HH_COUNT = 5 };
 
 // Householder(x[j:]): gamma = x[j], sigma2 = <x[j+1:], x[j+1:]> from the partials
 // (arithmetic in the vector dtype, as the reference's arrays)
@@ -793,6 +793,7 @@ __global__ void hh_make_kernel(const S *x, int64_t j, const double *part, int P,
   hh[HH_ALPHA] = (double)alpha;
   hh[HH_V0] = (double)v0;
   hh[HH_NRM] = (double)nrm;
+  hh[HH_XNORM] = (double)xnorm;
 }
 
 // U_j = (v0 at j, x[i] beyond) / nrm, zero below j; partials of <U_j, x>.
@@ -1618,6 +1619,40 @@ int kry_trsv_upper(kry_ctx *ctx, int32_t m, int32_t k, int dtype, const double *
   dev_free(dy);
   dev_free(dout);
   dev_free(c);
+  KRY_API_END
+}
+
+// Householder(x) (householder.py:6-53) on its own, for a single vector x
+// (n x 1): v_out = v / sqrt(|v0|^2 + sigma2), out3 = [beta, alpha, xnorm],
+// with the same kernels (and arithmetic in x's dtype) as Householder Arnoldi.
+int kry_householder(kry_ctx *ctx, kry_vec *x, kry_vec *v_out, double *out3) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && x && v_out && out3, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(x->k == 1 && v_out->k == 1 && x->n == v_out->n && x->dtype == v_out->dtype && x->n >= 1, KRY_EINVAL,
+              "x and v_out must be matching single vectors");
+  KRY_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int64_t N = x->n;
+  double *part = ctx_scratch(ctx, ((size_t)kMaxGrid + HH_COUNT) * 8);
+  double *hh = part + kMaxGrid;
+  auto go = [&](auto v0) {
+    using V = decltype(v0);
+    const int P = launch_elementwise<V>(N, 1, OpSuffixSq<V>{static_cast<const V *>(x->d), 1}, part, nullptr, 0, st);
+    hipLaunchKernelGGL(hh_make_kernel<V>, dim3(1), dim3(kBlock), 0, st, static_cast<const V *>(x->d), (int64_t)0,
+                       (const double *)part, P, hh, (const Ctrl *)nullptr, 0);
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (N + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(hh_vec_kernel<V>, dim3(G), dim3(kBlock), 0, st, N, static_cast<const V *>(x->d),
+                       static_cast<V *>(v_out->d), (int64_t)0, (const double *)hh, part, (const Ctrl *)nullptr, 0);
+  };
+  if (x->dtype == KRY_F64) go(0.0);
+  else go(0.0f);
+  KRY_HIP(hipGetLastError());
+  double h[HH_COUNT];
+  KRY_HIP(hipMemcpyAsync(h, hh, sizeof(h), hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  out3[0] = h[HH_BETA];
+  out3[1] = h[HH_ALPHA];
+  out3[2] = h[HH_XNORM];
   KRY_API_END
 }
 
