@@ -49,6 +49,11 @@ struct kry_cg {
   int col_offset = 0, total_k = 0;
   double *gbuf = nullptr;  // total_k (allreduced residual norms)
   double *gcrit = nullptr; // total_k
+  // persistent small-n loop (cg_persist_kernel): second p buffer, barrier
+  // and granule words; cgp_spw = -1 undecided, 0 not used, else slices/wave
+  void *pb = nullptr;
+  unsigned *cgp_words = nullptr;
+  int cgp_spw = -1;
 };
 
 namespace {
@@ -282,6 +287,216 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
   }
 }
 
+// ------------------------------------- persistent CG for launch-bound sizes
+// One launch runs a whole chunk of iterations of the fused path (no M / Ml,
+// one RHS, default inner) on at most one 1024-thread block per CU, all
+// resident. Wave gw owns SPW consecutive SELL slices; each lane keeps y, r and
+// p of its rows in registers across iterations. Per iteration:
+//   SpMV of the own rows, <p, Ap> block partial   -> all-gather #1 -> alpha
+//   r -= alpha Ap (stored), <r, r> block partial  -> release, all-gather #2,
+//                                                    acquire -> rho, omega
+//   y += alpha p, p = r + omega p (p stored to the ping-pong buffer)
+// The SpMV gathers p_t(j) of other rows as r_t(j) + omega_{t-1} p_{t-1}(j)
+// (the owner's exact operations): r_t was stored before all-gather #2 of the
+// previous iteration and p_{t-1} one iteration earlier, so both are visible
+// after its acquire, and the loop needs two grid-wide exchanges, not three.
+// Scalar arithmetic is that of cg_alpha_kernel / cg_yp_kernel and every
+// block derives the same bits (fixed-order sums); the dot products are summed
+// in another order than the launch-per-pass path's, so the two agree to
+// rounding, not bitwise. The state left behind (y, r, p in s->p, the scalar
+// slots, the history, the stop word) has the fused path's layout.
+constexpr int kCgpBlock = 1024;
+constexpr int kCgpWaves = kCgpBlock / 64;
+constexpr int kCgpGran = 4 * 2 * 256;                 // (exchange, parity) regions x 2 words x G <= 256
+constexpr size_t kCgpBytes = 64 + (size_t)kCgpGran * 8;  // 16 barrier words, then the granules
+
+// write-through store (sc1): visible at agent scope once the wave's vmcnt
+// drains, so the exchange needs no L2 writeback (buffer_wbl2) on its release
+// side; the readers' acquire (buffer_inv) drops their stale lines
+template <typename V>
+__device__ __forceinline__ void st_wt(V *p, V v) {
+  if constexpr (sizeof(V) == 8)
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong((double)v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(reinterpret_cast<unsigned *>(p), __float_as_uint((float)v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename V, typename S, typename MV, typename I, bool D16, int SPW>
+__global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
+    const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
+    const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
+    int64_t nslices, int64_t n, V *__restrict__ Y, V *R, V *P0, V *P1, double *scal, double *hist,
+    unsigned *words, Ctrl *ctrl, int max_steps, int dbg) {
+  if (halted(ctrl, 0)) return;
+  constexpr int UNR = 4;     // 8 spills at 128 VGPRs (two gathers per slot)
+  constexpr int ROWS = SPW * kCgpBlock;  // rows of this block: [row0, row0 + ROWS)
+  __shared__ double wsum[kCgpWaves];
+  __shared__ double shv[2];
+  __shared__ int flag;
+  // LDS: y and Ap of the block's rows (r and p stay in registers) and p_t of
+  // the block's rows by local row, so that in-block columns (most of a
+  // banded matrix's) are gathered from LDS; SPW = 4 doubles is 96 KB of 160
+  __shared__ V ys[ROWS], aps[ROWS], ps[ROWS];
+  unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = gridDim.x;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  const int64_t s0 = ((int64_t)blockIdx.x * kCgpWaves + wid) * SPW;
+  const int lr0 = wid * SPW * 64 + lane;  // local row of slice i: lr0 + 64 i
+  V r[SPW], p[SPW];
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int64_t row = (s0 + i) * 64 + lane;
+    const bool own = s0 + i < nslices && row < n;
+    ys[i * kCgpBlock + tid] = own ? Y[row] : V(0);
+    r[i] = own ? R[row] : V(0);
+    p[i] = own ? P0[row] : V(0);
+  }
+  S rho = (S)scal[S_RHO];
+  const double crit = scal[S_CRIT];
+  V om_prev = V(0);
+  // all-gather of one double per block (fixed-order sum, same in every block);
+  // `data`: R / P stores precede it (write-through: drained, then acquire)
+  auto exchange = [&](double part, int t, int xid, bool data) -> bool {
+    const double bp = block_sum1_t0(part, wsum);
+    unsigned long long *gr = gran + (size_t)(xid * 2 + (t & 1)) * 2 * 256;
+    const unsigned tag = ((unsigned)(t + 1) << 2) | (unsigned)(xid + 1);
+    if (data) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, bp);
+    if (tid < 64) {
+      const bool ok = sweep_partials(gr, G, tag, words, ctrl, &shv[0]);
+      if (tid == 0) {
+        flag = ok ? 1 : 0;
+        if (data) {  // the other blocks' R / P stores are visible to this block's loads
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+    }
+    __syncthreads();
+    return flag != 0;
+  };
+  int t = 0;
+  for (; t < max_steps; ++t) {
+    // p_t of the block's rows into LDS
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) ps[lr0 + 64 * i] = p[i];
+    __syncthreads();
+    // p_t(j) of other blocks' rows: at t = 0 from P0 (kernel boundary); after
+    // that r_t(j) + omega p_{t-1}(j), the owner's operations
+    const V *Pprev = (t & 1) ? P0 : P1;  // holds p_{t-1} (t >= 1)
+    double pap = 0.0;
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      const int64_t sl = s0 + i;
+      V acc = V(0);
+      if (sl < nslices) {
+        const int w = swidth[sl];
+        const int64_t base = sptr[sl];
+        for (int j0 = 0; j0 < w; j0 += UNR) {
+          I col[UNR];
+          V a[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const bool in = j0 + u < w;
+            if constexpr (D16) {
+              const unsigned d = in ? (unsigned)sdelta[base + (int64_t)(j0 + u) * 64 + lane] : 0xFFFFu;
+              const int b = in ? scbase[(base >> 6) + j0 + u] : 0;
+              col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
+            } else {
+              col[u] = in ? sidx[base + (int64_t)(j0 + u) * 64 + lane] : I(-1);
+            }
+            a[u] = in ? (V)sval[base + (int64_t)(j0 + u) * 64 + lane] : V(0);
+          }
+          V xv[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const int64_t lc = (int64_t)col[u] - row0;
+            if ((uint64_t)lc < (uint64_t)ROWS && !(dbg & 1)) {
+              xv[u] = ps[lc];
+            } else if (col[u] < 0) {
+              xv[u] = V(0);
+            } else if (t == 0) {
+              xv[u] = P0[col[u]];
+            } else {
+              const V rj = R[col[u]], pj = Pprev[col[u]];
+              const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
+              xv[u] = rj + tt;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < UNR; ++u)
+            if (col[u] >= 0) {
+              const V pr = a[u] * xv[u];
+              acc = acc + pr;
+            }
+        }
+        if (sl * 64 + lane < n) pap += dterm((double)p[i], (double)acc);
+      }
+      aps[i * kCgpBlock + tid] = acc;
+    }
+    if (!exchange(pap, t, 0, false)) return;
+    const S pAp = (S)shv[0];
+    const S alpha = rho / safe<S>(pAp);  // cg.py:183-185
+    const V a = (V)(double)alpha;
+    double rr = 0.0;
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      const int64_t row = (s0 + i) * 64 + lane;
+      const V t2 = a * aps[i * kCgpBlock + tid];
+      r[i] = r[i] - t2;  // cg.py:200
+      if (s0 + i < nslices && row < n) {
+        st_wt(R + row, r[i]);
+        rr += dterm((double)r[i], (double)r[i]);
+      }
+    }
+    if (!exchange(rr, t, 1, true)) return;
+    const S rrS = (S)shv[0];
+    const S om = rrS / safe<S>(rho);
+    const V omV = (V)(double)om;
+    V *Pnext = (t & 1) ? P0 : P1;  // p_{t+1}
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      const int64_t row = (s0 + i) * 64 + lane;
+      const V t1 = a * p[i];
+      ys[i * kCgpBlock + tid] = ys[i * kCgpBlock + tid] + t1;  // cg.py:196
+      const V tt = omV * p[i];
+      p[i] = r[i] + tt;  // cg.py:178
+      if (s0 + i < nslices && row < n) st_wt(Pnext + row, p[i]);
+    }
+    const S nrm = sqrt(rrS);
+    if (blockIdx.x == 0 && tid == 0) {
+      scal[S_ALPHA] = (double)alpha;
+      scal[S_RHO_OLD] = (double)rho;
+      scal[S_RHO_PREV] = (double)rho;
+      scal[S_RHO] = (double)rrS;
+      scal[S_OMEGA] = (double)om;
+      hist[t] = (double)nrm;
+    }
+    rho = rrS;
+    om_prev = omV;
+    if ((double)nrm <= crit) {  // cg.py:156 (uniform: every block has the same bits)
+      if (blockIdx.x == 0 && tid == 0) ctrl->stop_at = t + 1;
+      ++t;
+      break;
+    }
+  }
+  // leave the fused path's state: y, r (already stored), the current p in P0
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int64_t row = (s0 + i) * 64 + lane;
+    if (s0 + i < nslices && row < n) {
+      Y[row] = ys[i * kCgpBlock + tid];
+      P0[row] = p[i];
+    }
+  }
+}
+
 template <typename V, typename MV, typename I>
 int cg_residual_chain(kry_cg *s, const V *src, V *raw, V *mlr) {
   hipStream_t st = s->ctx->stream;
@@ -322,11 +537,83 @@ void cg_start_impl(kry_cg *s) {
   KRY_HIP(hipGetLastError());
 }
 
+// The persistent loop when the whole problem fits one resident block per CU
+// (SPW slices per wave, SPW in 1..4: n <= 1 M at 256 CUs; 8 spills); false = use the
+// launch-per-pass path. Decided once per solver (s->cgp_spw); the words are
+// zeroed per launch so the granule tags restart at step 0.
+template <typename V, typename S, typename MV, typename I, bool D16>
+bool cgp_launch_t(kry_cg *s, int max_steps) {
+  const kry_csr *A = s->A;
+  auto kern_for = [](int spw) {
+    switch (spw) {
+      case 1: return cg_persist_kernel<V, S, MV, I, D16, 1>;
+      case 2: return cg_persist_kernel<V, S, MV, I, D16, 2>;
+      default: return cg_persist_kernel<V, S, MV, I, D16, 4>;
+    }
+  };
+  if (s->cgp_spw < 0) {
+    s->cgp_spw = 0;
+    const char *e = getenv("KRY_CG_PERSIST");
+    if (!(e && atoi(e) == 0)) {
+      int dev = 0, ncu = 0;
+      KRY_HIP(hipGetDevice(&dev));
+      KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      const int gmax = ncu < 256 ? ncu : 256;
+      for (int spw = 1; spw <= 4; spw *= 2) {
+        const int64_t G = (A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw);
+        if (G > gmax) continue;
+        int per_cu = 0;
+        KRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern_for(spw), kCgpBlock, 0));
+        if (per_cu >= 1) s->cgp_spw = spw;
+        break;
+      }
+      if (s->cgp_spw > 0) {
+        s->pb = dev_alloc(((size_t)s->n + 15) / 16 * 16 * sizeof(V));
+        s->cgp_words = static_cast<unsigned *>(dev_alloc(kCgpBytes));
+      }
+    }
+  }
+  if (s->cgp_spw == 0) return false;
+  const int spw = s->cgp_spw;
+  const int G = (int)((A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw));
+  hipStream_t st = s->ctx->stream;
+  KRY_HIP(hipMemsetAsync(s->cgp_words, 0, kCgpBytes, st));
+  ProfScope ps(s->ctx, PROF_OTHER);
+  hipLaunchKernelGGL(kern_for(spw), dim3(G), dim3(kCgpBlock), 0, st, static_cast<const int64_t *>(A->sptr),
+                     static_cast<const int *>(A->swidth), static_cast<const I *>(A->sidx),
+                     static_cast<const uint16_t *>(A->sdelta), static_cast<const int *>(A->scbase),
+                     static_cast<const MV *>(A->sval), A->nslices, A->n, static_cast<V *>(s->y),
+                     static_cast<V *>(s->r), static_cast<V *>(s->p), static_cast<V *>(s->pb), s->scal, s->hist,
+                     s->cgp_words, s->ctrl, max_steps, getenv("KRY_CGP_DBG") ? atoi(getenv("KRY_CGP_DBG")) : 0);
+  KRY_HIP(hipGetLastError());
+  return true;
+}
+
+// KRY_CG_PERSIST=0 disables the persistent loop; =2 requires it (tests).
+template <typename V, typename MV, typename I>
+bool cgp_launch(kry_cg *s, int max_steps) {
+  const kry_csr *A = s->A;
+  bool taken = false;
+  if (s->cgp_spw != 0 && s->k == 1 && !s->M && !s->Ml && !s->w && !s->comm && A->nirregular == 0 && A->cb_nb == 0 &&
+      A->sptr && max_steps > 0) {
+    const bool f32 = s->scalar_f32;
+    if (A->compact)
+      taken = f32 ? cgp_launch_t<V, float, MV, I, true>(s, max_steps) : cgp_launch_t<V, double, MV, I, true>(s, max_steps);
+    else
+      taken = f32 ? cgp_launch_t<V, float, MV, I, false>(s, max_steps) : cgp_launch_t<V, double, MV, I, false>(s, max_steps);
+  }
+  const char *e = getenv("KRY_CG_PERSIST");
+  KRY_REQUIRE(taken || max_steps <= 0 || !(e && atoi(e) == 2), KRY_EUNSUPPORTED,
+              "KRY_CG_PERSIST=2: this solve is not eligible for the persistent CG loop");
+  return taken;
+}
+
 template <typename V, typename MV, typename I>
 void cg_run_impl(kry_cg *s, int max_steps) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
+  if (cgp_launch<V, MV, I>(s, max_steps)) return;
   double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
   for (int step = 0; step < max_steps; ++step) {
     V *p = static_cast<V *>(s->p);
@@ -439,7 +726,7 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
 
 static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b, s->x0, s->y, s->r, s->p, s->Ap, s->z, s->t, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
-                  s->ctrl, s->gbuf, s->gcrit};
+                  s->ctrl, s->gbuf, s->gcrit, s->pb, s->cgp_words};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -560,6 +847,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   Ctrl c;
   KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
+  KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: an in-launch exchange timed out");
   const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
   if (done > 0) {
     KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));

@@ -186,7 +186,6 @@ __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t N, int k, V *__r
 // kernel raises ctrl->status = KRY_EDEVICE and every block leaves.
 constexpr int kMgsBlock = 512;
 constexpr int kBarWords = 16;  // [0, 8) group counters, 8 top counter, 9 abort
-constexpr unsigned kSpinLimit = 1u << 20;
 
 __device__ __forceinline__ void st_agent(double *p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
@@ -246,31 +245,6 @@ __device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag) {
   return *flag != 0;
 }
 
-// Deterministic block sum for one column: each wave sums by a fixed xor
-// butterfly (lane 0's value is used), one barrier, then wave 0 adds the wave
-// sums by a fixed butterfly over lanes 0..7 (blockDim <= 512). The result is
-// returned in thread 0 (no trailing barrier); block_sum1 also stores it to
-// *out and makes it visible to the block.
-__device__ __forceinline__ double block_sum1_t0(double v, double *wsum) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) wsum[wv] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (wv == 0) {
-    s = lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0;
-#pragma unroll
-    for (int off = 1; off <= 4; off <<= 1) s += __shfl_xor(s, off);
-  }
-  return s;
-}
-__device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
-  const double s = block_sum1_t0(v, wsum);
-  if (threadIdx.x == 0) *out = s;
-  __syncthreads();
-}
-
 // Fixed-order sum of P partial rows (same order in every block of size B).
 template <int B, bool AGENT>
 __device__ __forceinline__ void reduce_rows(const double *part, int P, int k, double *red) {
@@ -313,54 +287,6 @@ __device__ __forceinline__ void reduce_rows(const double *part, int P, int k, do
 constexpr int kGranWords = 2 * 2 * 256;  // two pass parities x two words x G <= 256 blocks
 // barrier words for `steps` chunk steps, then the (shared) granule words
 inline size_t bar_bytes(int steps) { return (size_t)steps * kBarWords * 4 + (size_t)kGranWords * 8; }
-__device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned tag, double v) {
-  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
-  const unsigned long long t = (unsigned long long)tag << 32;
-  __hip_atomic_store(g, t | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, t | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wave 0 only; returns the same value in every lane (false = timed out / aborted).
-__device__ bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out) {
-  const int lane = threadIdx.x;
-  unsigned long long g[4][2];
-  unsigned spins = 0;
-  for (;;) {
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int b = lane + 64 * i;
-      if (b < G) {
-        g[i][0] = __hip_atomic_load(gr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        g[i][1] = __hip_atomic_load(gr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = ok && (unsigned)(g[i][0] >> 32) == tag && (unsigned)(g[i][1] >> 32) == tag;
-      }
-    }
-    if (__all(ok)) break;
-    __builtin_amdgcn_s_sleep(1);
-    ++spins;
-    if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-      return false;
-    if (spins > kSpinLimit) {
-      if (lane == 0) {
-        __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return false;
-    }
-  }
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int b = lane + 64 * i;
-    if (b < G) s += __longlong_as_double((long long)((g[i][1] << 32) | (g[i][0] & 0xffffffffull)));
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-  if (lane == 0) *out = s;
-  return true;
-}
-
 template <typename V, int E>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V *__restrict__ w,
                                                             const V *__restrict__ Vb, size_t stride, int col,

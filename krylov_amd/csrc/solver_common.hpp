@@ -17,6 +17,91 @@ struct kry_comm {
 
 namespace kry {
 
+// ------------------------------------------------ in-launch all-gathers
+// Persistent kernels (GMRES MGS, small-n CG) exchange one double per block
+// per phase as self-validating granules {tag, 32 data bits} (two per block:
+// the low and high words), stored write-through with agent-scope atomics; no
+// counters, no flag. Wave 0 of every block sweeps all G <= 256 blocks'
+// granules until every tag matches, then sums the values in a fixed order
+// (lane l: blocks l, l + 64, ..., then a fixed xor butterfly; lane 0's value),
+// so every block derives the same bits. Tags must be unique among the words
+// a region holds between zeroings. Every spin is bounded: on timeout the
+// kernel raises ctrl->status = KRY_EDEVICE and the abort word, and every
+// block leaves.
+constexpr unsigned kSpinLimit = 1u << 20;
+
+__device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned tag, double v) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, t | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 only; returns the same value in every lane (false = timed out / aborted).
+__device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out) {
+  const int lane = threadIdx.x;
+  unsigned long long g[4][2];
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = lane + 64 * i;
+      if (b < G) {
+        g[i][0] = __hip_atomic_load(gr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[i][1] = __hip_atomic_load(gr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && (unsigned)(g[i][0] >> 32) == tag && (unsigned)(g[i][1] >> 32) == tag;
+      }
+    }
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    ++spins;
+    if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      return false;
+    if (spins > kSpinLimit) {
+      if (lane == 0) {
+        __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = lane + 64 * i;
+    if (b < G) s += __longlong_as_double((long long)((g[i][1] << 32) | (g[i][0] & 0xffffffffull)));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) *out = s;
+  return true;
+}
+
+// Deterministic block sum for one column: each wave sums by a fixed xor
+// butterfly (lane 0's value is used), one barrier, then wave 0 adds the wave
+// sums by a fixed butterfly over lanes 0..nwaves-1 (blockDim <= 1024). The result is
+// returned in thread 0 (no trailing barrier); block_sum1 also stores it to
+// *out and makes it visible to the block.
+__device__ __forceinline__ double block_sum1_t0(double v, double *wsum) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wsum[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (wv == 0) {
+    s = lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0;
+    for (int off = 1; off < (int)(blockDim.x >> 6); off <<= 1) s += __shfl_xor(s, off);
+  }
+  return s;
+}
+__device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
+  const double s = block_sum1_t0(v, wsum);
+  if (threadIdx.x == 0) *out = s;
+  __syncthreads();
+}
+
 // guarded divisor, np.where(d != 0, d, 1.0)
 template <typename S>
 __device__ __forceinline__ S safe(S d) {

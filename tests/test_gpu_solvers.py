@@ -323,3 +323,60 @@ def test_gmres_persistent_mgs_matches_pass_kernels(monkeypatch, k, ortho):
         _, ref = krylov_ref.gmres(R, b, maxiter=30, tol=1e-9)
         assert ref.numsteps == fast.numsteps
         np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,dtype", [(30, np.float64), (300, np.float64), (1000, np.float64), (300, np.float32)])
+def test_cg_persistent_matches_pass_kernels(monkeypatch, m, dtype):
+    """The persistent small-n CG loop (one launch per chunk, two in-launch
+    all-gathers per iteration, KRY_CG_PERSIST=2 makes it mandatory) against
+    the launch-per-pass path (KRY_CG_PERSIST=0) and the oracle: same step
+    count, histories to round-off (the dot products are summed in different
+    fixed orders), same iterate. m = 30 is one partly filled block, m = 1000
+    the largest size it takes (4 slices per wave)."""
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref
+
+    R = problems.poisson2d(m).astype(dtype)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(3).standard_normal(R.shape[0]).astype(dtype)
+    tol = 1e-9 if dtype == np.float64 else 1e-4
+    rt = 1e-10 if dtype == np.float64 else 1e-4
+    monkeypatch.setenv("KRY_CG_PERSIST", "2")
+    _, fast = krylov_amd.cg(A, b, tol=tol, maxiter=400)
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    _, slow = krylov_amd.cg(A, b, tol=tol, maxiter=400)
+    assert fast.numsteps == slow.numsteps
+    f, s = np.asarray(fast.resnorms), np.asarray(slow.resnorms)
+    np.testing.assert_allclose(f[:-1], s[:-1], rtol=rt)
+    np.testing.assert_allclose(fast.xk, slow.xk, rtol=rt, atol=rt * np.abs(slow.xk).max())
+    if m <= 300:
+        _, ref = krylov_ref.cg(R, b, tol=tol, maxiter=400)
+        assert ref.numsteps == fast.numsteps
+        np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=rt)
+
+
+@pytest.mark.gpu
+def test_cg_persistent_chunk_boundaries(monkeypatch):
+    """maxiter cut mid-chunk and a callback (one step per launch): the state
+    the persistent loop leaves (y, r, p, scalars) carries across launches."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    R = problems.poisson2d(200)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(4).standard_normal(R.shape[0])
+    out = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("KRY_CG_PERSIST", mode)
+        seen = []
+        _, info = krylov_amd.cg(A, b, tol=0.0, maxiter=45)
+        _, info_cb = krylov_amd.cg(A, b, tol=0.0, maxiter=10, callback=lambda x, r: seen.append(float(np.linalg.norm(r))))
+        out[mode] = (info, info_cb, seen)
+    f, s = out["2"], out["0"]
+    assert f[0].numsteps == s[0].numsteps == 45
+    np.testing.assert_allclose(f[0].resnorms, s[0].resnorms, rtol=1e-10)
+    np.testing.assert_allclose(f[0].xk, s[0].xk, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(f[1].resnorms, s[1].resnorms, rtol=1e-10)
+    np.testing.assert_allclose(f[2], s[2], rtol=1e-10)
