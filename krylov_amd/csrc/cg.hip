@@ -328,8 +328,19 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
     const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
     int64_t nslices, int64_t n, V *__restrict__ Y, V *R, V *P0, V *P1, double *scal, double *hist,
-    unsigned *words, Ctrl *ctrl, int max_steps, int dbg) {
+    unsigned *words, Ctrl *ctrl, int max_steps, unsigned long long *tbuf) {
   if (halted(ctrl, 0)) return;
+  // optional phase trace (tbuf != null, KRY_CGP_TRACE): thread 0's wall-clock
+  // split of an iteration into SpMV / all-gather #1 wait / r update / store
+  // drain / all-gather #2 wait / y and p update
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto tmark = [&](int k) {
+    if (tbuf && threadIdx.x == 0) {
+      const unsigned long long now = wall_clock64();
+      if (k >= 0) tacc[k] += now - tlast;
+      tlast = now;
+    }
+  };
   constexpr int UNR = 4;     // 8 spills at 128 VGPRs (two gathers per slot)
   constexpr int ROWS = SPW * kCgpBlock;  // rows of this block: [row0, row0 + ROWS)
   __shared__ double wsum[kCgpWaves];
@@ -361,11 +372,13 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   // `data`: R / P stores precede it (write-through: drained, then acquire)
   auto exchange = [&](double part, int t, int xid, bool data) -> bool {
     const double bp = block_sum1_t0(part, wsum);
+    tmark(xid == 0 ? 0 : 2);
     unsigned long long *gr = gran + (size_t)(xid * 2 + (t & 1)) * 2 * 256;
     const unsigned tag = ((unsigned)(t + 1) << 2) | (unsigned)(xid + 1);
     if (data) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      tmark(3);
     }
     if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, bp);
     if (tid < 64) {
@@ -379,9 +392,11 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       }
     }
     __syncthreads();
+    tmark(xid == 0 ? 1 : 4);
     return flag != 0;
   };
   int t = 0;
+  tmark(-1);
   for (; t < max_steps; ++t) {
     // p_t of the block's rows into LDS
 #pragma unroll
@@ -417,7 +432,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
 #pragma unroll
           for (int u = 0; u < UNR; ++u) {
             const int64_t lc = (int64_t)col[u] - row0;
-            if ((uint64_t)lc < (uint64_t)ROWS && !(dbg & 1)) {
+            if ((uint64_t)lc < (uint64_t)ROWS) {
               xv[u] = ps[lc];
             } else if (col[u] < 0) {
               xv[u] = V(0);
@@ -469,6 +484,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       p[i] = r[i] + tt;  // cg.py:178
       if (s0 + i < nslices && row < n) st_wt(Pnext + row, p[i]);
     }
+    tmark(5);
     const S nrm = sqrt(rrS);
     if (blockIdx.x == 0 && tid == 0) {
       scal[S_ALPHA] = (double)alpha;
@@ -486,6 +502,8 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       break;
     }
   }
+  if (tbuf && tid == 0)
+    for (int k = 0; k < 6; ++k) tbuf[blockIdx.x * 8 + k] = tacc[k];
   // leave the fused path's state: y, r (already stored), the current p in P0
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
@@ -578,14 +596,41 @@ bool cgp_launch_t(kry_cg *s, int max_steps) {
   const int G = (int)((A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw));
   hipStream_t st = s->ctx->stream;
   KRY_HIP(hipMemsetAsync(s->cgp_words, 0, kCgpBytes, st));
+  unsigned long long *tb = nullptr;
+  if (getenv("KRY_CGP_TRACE")) {
+    KRY_HIP(hipMalloc(&tb, (size_t)G * 64));
+    KRY_HIP(hipMemsetAsync(tb, 0, (size_t)G * 64, st));
+  }
   ProfScope ps(s->ctx, PROF_OTHER);
   hipLaunchKernelGGL(kern_for(spw), dim3(G), dim3(kCgpBlock), 0, st, static_cast<const int64_t *>(A->sptr),
                      static_cast<const int *>(A->swidth), static_cast<const I *>(A->sidx),
                      static_cast<const uint16_t *>(A->sdelta), static_cast<const int *>(A->scbase),
                      static_cast<const MV *>(A->sval), A->nslices, A->n, static_cast<V *>(s->y),
                      static_cast<V *>(s->r), static_cast<V *>(s->p), static_cast<V *>(s->pb), s->scal, s->hist,
-                     s->cgp_words, s->ctrl, max_steps, getenv("KRY_CGP_DBG") ? atoi(getenv("KRY_CGP_DBG")) : 0);
+                     s->cgp_words, s->ctrl, max_steps, tb);
   KRY_HIP(hipGetLastError());
+  if (tb) {  // KRY_CGP_TRACE: per-phase split, per-block sums of wall_clock64 ticks (100 MHz), to stderr
+    std::vector<unsigned long long> h((size_t)G * 8);
+    KRY_HIP(hipMemcpyAsync(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+    Ctrl c;
+    KRY_HIP(hipMemcpy(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    const int its = c.stop_at < max_steps ? c.stop_at : max_steps;
+    const char *names[6] = {"spmv", "x1wait", "rupd", "drain", "x2wait", "pupd"};
+    fprintf(stderr, "cgp trace G=%d its=%d (us/it: mean / min / max over blocks):", G, its);
+    for (int k = 0; k < 6; ++k) {
+      double mn = 1e30, mx = 0, sm = 0;
+      for (int b = 0; b < G; ++b) {
+        const double v = h[(size_t)b * 8 + k] * 0.01 / (its > 0 ? its : 1);
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+        sm += v;
+      }
+      fprintf(stderr, " %s %.2f/%.2f/%.2f", names[k], sm / G, mn, mx);
+    }
+    fprintf(stderr, "\n");
+    KRY_HIP(hipFree(tb));
+  }
   return true;
 }
 
