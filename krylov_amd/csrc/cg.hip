@@ -159,11 +159,14 @@ __global__ void cg_start_finalize(const double *part, int P, int k, double *scal
 }
 
 // alpha = rhos[-1] / np.where(pAp != 0, pAp, 1.0)  (cg.py:183-185)
+// 1024 threads: the SpMV's partials (up to 8192 blocks x k) in 32-load rounds
+constexpr int kAlphaBlock = 1024;
 template <typename S>
-__global__ void cg_alpha_kernel(const double *part, int P, int k, double *scal, const Ctrl *ctrl, int step) {
+__global__ __launch_bounds__(kAlphaBlock) void cg_alpha_kernel(const double *part, int P, int k, double *scal,
+                                                               const Ctrl *ctrl, int step) {
   if (halted(ctrl, step)) return;
-  __shared__ double red[kBlock];
-  reduce_partials(part, P, k, red);
+  __shared__ double red[kAlphaBlock];
+  reduce_partials<kAlphaBlock>(part, P, k, red);
   const int c = threadIdx.x;
   if (c < k) {
     const S pAp = (S)red[c];
@@ -676,9 +679,9 @@ void cg_run_impl(kry_cg *s, int max_steps) {
       }
     }
     if (s->scalar_f32)
-      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
     else
-      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
     double *gb = s->comm ? s->gbuf : nullptr;
     if (!s->M && k <= 8) {  // r pass, then the fused rho / y / p pass
       {

@@ -612,15 +612,24 @@ struct VIO {
 // ------------------------------------------------------- partial reducers
 // Sum part[p * k + c] over p < P for every column c < k into red[c]
 // (fixed order; all of one block). Must be called by every thread.
+// NT threads (the block size), red[NT]
+template <int NT = kBlock>
 __device__ __forceinline__ void reduce_partials(const double *part, int P, int k, double *red) {
   const int tid = threadIdx.x;
   const int c = tid & (k - 1);
-  const int step = kBlock / k;
+  const int step = NT / k;
   double s = 0.0;
-  // loads issued 8 at a time (independent), added in the fixed sequential
-  // order: latency of one L2 round trip per 8 partials, same bits as a plain
-  // loop
+  // loads issued 32 (then 8) at a time (independent), added in the fixed
+  // sequential order: one L2 round trip per 32 partials (k = 8 over 8192
+  // blocks: 256 partials per thread), same bits as a plain loop
   int p = tid / k;
+  for (; p + 31 * step < P; p += 32 * step) {
+    double v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = part[(int64_t)(p + u * step) * k + c];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += v[u];
+  }
   for (; p + 7 * step < P; p += 8 * step) {
     double v[8];
 #pragma unroll
@@ -630,7 +639,7 @@ __device__ __forceinline__ void reduce_partials(const double *part, int P, int k
   }
   for (; p < P; p += step) s += part[(int64_t)p * k + c];
   red[tid] = s;
-  block_tree_reduce(red, kBlock, k);
+  block_tree_reduce(red, NT, k);
 }
 
 // one-block finalize: out[c] = sum over the partials of column c

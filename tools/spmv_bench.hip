@@ -1339,7 +1339,133 @@ static int cg_only(int m, int reps) {
   return 0;
 }
 
+
+// Persistent-CG premise probe (`spmv_bench pstudy m reps`): the CG SpMV run
+// as ONE resident block of 1024 threads per CU (the shape a persistent
+// large-n CG would have), each wave over a contiguous slice range, with the
+// result kept on chip (LDS) for the first LSL slices of each wave and
+// stored to y for the rest. LSL = 0: all stored; LSL = 1 << 30: none stored
+// (LDS slots reused round-robin).
+template <int UNR, int LSL>
+__global__ __launch_bounds__(1024) void spmv_1pc(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase,
+                                                 const double *__restrict__ sval, int64_t nslices, int64_t n,
+                                                 const double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ part) {
+  __shared__ double keep[16 * 1024];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t W = (int64_t)gridDim.x * 16, wg = (int64_t)blockIdx.x * 16 + wid;
+  const int64_t sb = nslices * wg / W, se = nslices * (wg + 1) / W;
+  double dacc = 0.0;
+  for (int64_t s = sb; s < se; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const uint16_t *cd = sdelta + base + lane;
+    const int *cb = scbase + (base >> 6);
+    const double *cv = sval + base + lane;
+    double acc = 0.0;
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      int col[UNR];
+      double a[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const bool in = j0 + u < w;
+        const unsigned d = in ? (unsigned)__builtin_nontemporal_load(cd + (int64_t)(j0 + u) * 64) : 0xFFFFu;
+        const int b = in ? cb[j0 + u] : 0;
+        col[u] = d != 0xFFFFu ? b + (int)d : -1;
+        a[u] = in ? __builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : 0.0;
+      }
+      double xv[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) xv[u] = col[u] >= 0 ? x[col[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (col[u] >= 0) acc = acc + a[u] * xv[u];
+    }
+    const int64_t row = s * 64 + lane;
+    if (row < n) {
+      dacc += acc * x[row];
+      const int64_t j = s - sb;
+      if (j < LSL)
+        keep[wid * 1024 + (int)(j & 15) * 64 + lane] = acc;
+      else
+        __builtin_nontemporal_store(acc, y + row);
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) dacc += __shfl_xor(dacc, off);
+  if (lane == 0) keep[wid] += dacc;  // keep the LDS writes live
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0;
+    for (int i = 0; i < 16; ++i) t += keep[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+static int persist_study(int m, int reps) {
+  std::vector<int> ip, ix;
+  std::vector<double> dv;
+  build_stencil(m, ip, ix, dv);
+  const int64_t n = ip.size() - 1, nnz = ix.size();
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  kry_csr *A;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+  if (!A->compact) {
+    printf("not compact\n");
+    return 1;
+  }
+  double *d_p, *d_ap, *part;
+  CK(hipMalloc(&d_p, n * 8));
+  CK(hipMalloc(&d_ap, n * 8));
+  CK(hipMalloc(&part, kMaxGrid * 8));
+  CK(hipMemset(d_p, 0, n * 8));
+  int dev = 0, ncu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto time = [&](const char *name, auto launch) {
+    launch();
+    CK(hipDeviceSynchronize());
+    float tot = 0;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      tot += ms;
+    }
+    printf("%-44s %.4f ms\n", name, tot / reps);
+  };
+  time("library CG SpMV (EpiApDot)", [&] {
+    launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_p, 1}, EpiApDot<double>{d_ap, nullptr, 1}, part,
+                                     nullptr, nullptr, 0, 0);
+  });
+  auto one = [&](const char *name, auto kern) {
+    time(name, [&] {
+      hipLaunchKernelGGL(kern, dim3(ncu), dim3(1024), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                         (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices, n,
+                         d_p, d_ap, part);
+    });
+  };
+  one("1 block/CU, UNR8, all stored", spmv_1pc<8, 0>);
+  one("1 block/CU, UNR8, first 16 slices/wave kept", spmv_1pc<8, 16>);
+  one("1 block/CU, UNR8, first 32 slices/wave kept", spmv_1pc<8, 32>);
+  one("1 block/CU, UNR8, none stored", spmv_1pc<8, (1 << 30)>);
+  one("1 block/CU, UNR16, all stored", spmv_1pc<16, 0>);
+  one("1 block/CU, UNR16, none stored", spmv_1pc<16, (1 << 30)>);
+  KC(kry_csr_destroy(A));
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "pstudy") == 0)
+    return persist_study(argc > 2 ? atoi(argv[2]) : 216, argc > 3 ? atoi(argv[3]) : 20);
   if (argc > 1 && strcmp(argv[1], "cgonly") == 0)
     return cg_only(argc > 2 ? atoi(argv[2]) : 216, argc > 3 ? atoi(argv[3]) : 20);
   if (argc > 1 && strcmp(argv[1], "block") == 0)
