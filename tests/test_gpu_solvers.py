@@ -380,3 +380,41 @@ def test_cg_persistent_chunk_boundaries(monkeypatch):
     np.testing.assert_allclose(f[0].xk, s[0].xk, rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(f[1].resnorms, s[1].resnorms, rtol=1e-10)
     np.testing.assert_allclose(f[2], s[2], rtol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["wide_columns", "f32_matrix_f64_vectors"])
+def test_cg_persistent_image_variants(monkeypatch, variant):
+    """The persistent CG loop on the full SELL image (column spans beyond the
+    compact image's 65534: couplings 80,000 rows apart) and on a float32
+    matrix under float64 vectors: against the launch-per-pass path and the
+    oracle."""
+    import scipy.sparse as sp
+
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref
+
+    R = problems.poisson2d(300).tocsr()
+    n = R.shape[0]
+    if variant == "wide_columns":
+        i = np.arange(0, n - 80_000, 7)
+        C = sp.coo_matrix((np.full(i.size, -0.25), (i, i + 80_000)), shape=(n, n))
+        R = (R + C + C.T + sp.identity(n) * 0.5).tocsr()
+        R.sort_indices()
+    else:
+        R = R.astype(np.float32)
+    A = krylov_amd.CsrOperator(R)
+    lay = A.layout()
+    assert lay["irregular"] == 0 and lay["col_blocks"] == 0
+    assert lay["compact"] == (variant != "wide_columns")
+    b = np.random.default_rng(5).standard_normal(n)
+    monkeypatch.setenv("KRY_CG_PERSIST", "2")
+    _, fast = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    _, slow = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    assert fast.numsteps == slow.numsteps
+    np.testing.assert_allclose(np.asarray(fast.resnorms)[:-1], np.asarray(slow.resnorms)[:-1], rtol=1e-10)
+    _, ref = krylov_ref.cg(R, b, tol=1e-9, maxiter=500)
+    assert ref.numsteps == fast.numsteps
+    np.testing.assert_allclose(np.asarray(fast.resnorms)[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
