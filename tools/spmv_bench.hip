@@ -235,6 +235,8 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
   const int64_t W = (int64_t)gridDim.x * 4;
   const int64_t m = (int64_t)g * 4 + wid;
   const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  double pend = 0.0;
+  int64_t prow = -1;
   for (int64_t s = s_begin; s < s_end; ++s) {
     const int w = swidth[s];
     const int64_t base = sptr[s];
@@ -248,12 +250,23 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
       a[u] = in ? __builtin_nontemporal_load(sval + base + (int64_t)u * 64 + lane) : 0.0;
       b[u] = in ? scbase[(base >> 6) + u] : 0;
     }
+    if (MODE == 6 || MODE == 7) {
+      // the previous slice's y store issued behind this slice's loads: with
+      // in-order vmcnt its ack no longer gates this slice's first use
+      asm volatile("" ::: "memory");
+      if (prow >= 0 && prow < n) y[prow] = pend;
+    }
     double xv[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       // 1: no gather, y stored; 3: no gather, no y store; 4: no gather,
-      // nontemporal y store; 5: no gather, y stored to a small target
-      xv[u] = 1.0;
+      // nontemporal y store; 5: no gather, y stored to a small target;
+      // 6: no gather, y store deferred behind the next slice's loads;
+      // 7: with the x gather, y store deferred; 8: with the gather, y stored
+      if (MODE == 7 || MODE == 8)
+        xv[u] = (u < w && d[u] != 0xFFFFu) ? x[b[u] + (int)d[u]] : 0.0;
+      else
+        xv[u] = 1.0;
     }
     double acc = 0.0;
 #pragma unroll
@@ -271,10 +284,14 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
       // same store count into a small L2-resident target (bounded by n)
       const int64_t idx = ((int64_t)blockIdx.x * 4 + wid) * 64 + lane;
       if (row < n && idx < n) y[idx] = acc;
+    } else if (MODE == 6 || MODE == 7) {
+      pend = acc;
+      prow = row;
     } else if (row < n) {
       y[row] = acc;
     }
   }
+  if ((MODE == 6 || MODE == 7) && prow >= 0 && prow < n) y[prow] = pend;
 }
 
 // ---- prototype: the d16 SpMV with XCD-interleaved slice order. XCD x owns a
@@ -1560,6 +1577,32 @@ int main(int argc, char **argv) {
     printf("  %-38s bitwise mismatches vs host csr_matvec: %ld\n", name, bad);
   };
 
+  if (getenv("SPMV_STORE_PROBE")) {  // the y-store cost only: library kernel vs probe modes
+    report("SELL d16 y = A x (library)", S, [&] {
+      launch_spmv<double, double, int>(A, 1, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr, nullptr,
+                                       nullptr, 0, 0);
+    });
+    check("SELL d16 y = A x (library)", d_y, yref);
+    for (int mode : {8, 7, 1, 6, 3}) {
+      char nm[96];
+      snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather, store" : mode == 3 ? "no gather, no store" : mode == 6 ? "no gather, deferred store" : mode == 7 ? "gather, deferred store" : "gather, store");
+      CK(hipMemset(d_y, 0, n * 8));
+      report(nm, S, [&] {
+        auto go = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(8192), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
+                             (const uint16_t *)A->sdelta, (const int *)A->scbase, (const double *)A->sval, A->nslices,
+                             n, d_x, d_y);
+        };
+        if (mode == 1) go(spmv_probe<16, 1>);
+        else if (mode == 3) go(spmv_probe<16, 3>);
+        else if (mode == 6) go(spmv_probe<16, 6>);
+        else if (mode == 7) go(spmv_probe<16, 7>);
+        else go(spmv_probe<16, 8>);
+      });
+      if (mode == 7 || mode == 8) check(nm, d_y, yref);
+    }
+    return 0;
+  }
   report("read ceiling (SELL idx+val, 16 B/lane)", nnz * 12.0, [&] {
     hipLaunchKernelGGL(read_ceiling, dim3(2048), dim3(256), 0, 0, (const int4 *)A32->sidx, nnz / 4,
                        (const double2 *)A32->sval, nnz / 2, d_out);
@@ -1706,9 +1749,9 @@ int main(int argc, char **argv) {
     });
     check(nm, d_y, yref);
   }
-  for (int mode = 1; mode < 6; mode += (mode == 1 ? 2 : 1)) {
+  for (int mode = 1; mode < 8; mode += (mode == 1 ? 2 : 1)) {
     char nm[96];
-    snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather" : mode == 3 ? "no gather, no store" : mode == 4 ? "no gather, nt store" : "no gather, store to 8 MB");
+    snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather" : mode == 3 ? "no gather, no store" : mode == 4 ? "no gather, nt store" : mode == 5 ? "no gather, store to 8 MB" : mode == 6 ? "no gather, deferred store" : "gather, deferred store");
     report(nm, S, [&] {
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(8192), dim3(256), 0, 0, (const int64_t *)A->sptr, (const int *)A->swidth,
@@ -1718,7 +1761,9 @@ int main(int argc, char **argv) {
       if (mode == 1) go(spmv_probe<16, 1>);
       else if (mode == 3) go(spmv_probe<16, 3>);
       else if (mode == 4) go(spmv_probe<16, 4>);
-      else go(spmv_probe<16, 5>);
+      else if (mode == 5) go(spmv_probe<16, 5>);
+      else if (mode == 6) go(spmv_probe<16, 6>);
+      else go(spmv_probe<16, 7>);
     });
   }
   report("CG p pass p = r + om p_old (3 vectors)", 24.0 * n, [&] {
