@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
       // nontemporal y store; 5: no gather, y stored to a small target;
       // 6: no gather, y store deferred behind the next slice's loads;
       // 7: with the x gather, y store deferred; 8: with the gather, y stored
-      if (MODE == 7 || MODE == 8)
+      if (MODE >= 7)
         xv[u] = (u < w && d[u] != 0xFFFFu) ? x[b[u] + (int)d[u]] : 0.0;
       else
         xv[u] = 1.0;
@@ -287,6 +287,12 @@ __global__ __launch_bounds__(256) void spmv_probe(const int64_t *__restrict__ sp
     } else if (MODE == 6 || MODE == 7) {
       pend = acc;
       prow = row;
+    } else if (MODE == 9) {  // gather; y store with cache-policy bits
+      if (row < n) asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(y + row), "v"(acc) : "memory");
+    } else if (MODE == 10) {
+      if (row < n) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(y + row), "v"(acc) : "memory");
+    } else if (MODE == 11) {
+      if (row < n) asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(y + row), "v"(acc) : "memory");
     } else if (row < n) {
       y[row] = acc;
     }
@@ -1583,9 +1589,9 @@ int main(int argc, char **argv) {
                                        nullptr, 0, 0);
     });
     check("SELL d16 y = A x (library)", d_y, yref);
-    for (int mode : {8, 7, 1, 6, 3}) {
+    for (int mode : {8, 9, 10, 11, 7, 1, 6, 3}) {
       char nm[96];
-      snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather, store" : mode == 3 ? "no gather, no store" : mode == 6 ? "no gather, deferred store" : mode == 7 ? "gather, deferred store" : "gather, store");
+      snprintf(nm, 96, "probe mode %d (%s)", mode, mode == 1 ? "no gather, store" : mode == 3 ? "no gather, no store" : mode == 6 ? "no gather, deferred store" : mode == 7 ? "gather, deferred store" : mode == 9 ? "gather, store sc0 sc1" : mode == 10 ? "gather, store sc1" : mode == 11 ? "gather, store sc0 sc1 nt" : "gather, store");
       CK(hipMemset(d_y, 0, n * 8));
       report(nm, S, [&] {
         auto go = [&](auto kern) {
@@ -1597,9 +1603,12 @@ int main(int argc, char **argv) {
         else if (mode == 3) go(spmv_probe<16, 3>);
         else if (mode == 6) go(spmv_probe<16, 6>);
         else if (mode == 7) go(spmv_probe<16, 7>);
+        else if (mode == 9) go(spmv_probe<16, 9>);
+        else if (mode == 10) go(spmv_probe<16, 10>);
+        else if (mode == 11) go(spmv_probe<16, 11>);
         else go(spmv_probe<16, 8>);
       });
-      if (mode == 7 || mode == 8) check(nm, d_y, yref);
+      if (mode >= 7) check(nm, d_y, yref);
     }
     return 0;
   }
