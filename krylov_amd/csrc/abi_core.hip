@@ -223,6 +223,7 @@ int kry_ctx_destroy(kry_ctx *ctx) {
   (void)hipEventDestroy(ctx->t0);
   (void)hipEventDestroy(ctx->t1);
   dev_free(ctx->scratch);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   KRY_API_END

@@ -293,16 +293,18 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 // ------------------------------------- persistent CG for launch-bound sizes
 // One launch runs a whole chunk of iterations of the fused path (no M / Ml,
 // one RHS, default inner) on at most one 1024-thread block per CU, all
-// resident. Wave gw owns SPW consecutive SELL slices; each lane keeps y, r and
-// p of its rows in registers across iterations. Per iteration:
+// resident. Wave gw owns SPW consecutive SELL slices; each lane keeps r and p
+// of its rows in registers across iterations (y and Ap in LDS). Per iteration:
 //   SpMV of the own rows, <p, Ap> block partial   -> all-gather #1 -> alpha
-//   r -= alpha Ap (stored), <r, r> block partial  -> release, all-gather #2,
-//                                                    acquire -> rho, omega
-//   y += alpha p, p = r + omega p (p stored to the ping-pong buffer)
-// The SpMV gathers p_t(j) of other rows as r_t(j) + omega_{t-1} p_{t-1}(j)
-// (the owner's exact operations): r_t was stored before all-gather #2 of the
-// previous iteration and p_{t-1} one iteration earlier, so both are visible
-// after its acquire, and the loop needs two grid-wide exchanges, not three.
+//   r -= alpha Ap (stored write-through), <r, r>  -> drain, all-gather #2
+//                                                    -> rho, omega
+//   y += alpha p, p = r + omega p (p stored write-through, ping-pong buffer)
+// The SpMV gathers p_t(j) of the block's own rows from LDS and of other
+// blocks' rows as r_t(j) + omega_{t-1} p_{t-1}(j) (the owner's exact
+// operations) with agent-scope loads: r_t was stored before all-gather #2 of
+// the previous iteration and p_{t-1} one iteration earlier, so both are
+// visible once it has been observed, and the loop needs two grid-wide
+// exchanges, not three.
 // Scalar arithmetic is that of cg_alpha_kernel / cg_yp_kernel and every
 // block derives the same bits (fixed-order sums); the dot products are summed
 // in another order than the launch-per-pass path's, so the two agree to
@@ -315,7 +317,7 @@ constexpr size_t kCgpBytes = 64 + (size_t)kCgpGran * 8;  // 16 barrier words, th
 
 // write-through store (sc1): visible at agent scope once the wave's vmcnt
 // drains, so the exchange needs no L2 writeback (buffer_wbl2) on its release
-// side; the readers' acquire (buffer_inv) drops their stale lines
+// side
 template <typename V>
 __device__ __forceinline__ void st_wt(V *p, V v) {
   if constexpr (sizeof(V) == 8)
@@ -324,6 +326,18 @@ __device__ __forceinline__ void st_wt(V *p, V v) {
   else
     __hip_atomic_store(reinterpret_cast<unsigned *>(p), __float_as_uint((float)v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// its reader: an agent-scope (sc1) load sees the write-through stores once the
+// writer's all-gather has been observed, with no L2 invalidate (buffer_inv)
+template <typename V>
+__device__ __forceinline__ V ld_wt(const V *p) {
+  if constexpr (sizeof(V) == 8)
+    return (V)__longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  else
+    return (V)__uint_as_float(
+        __hip_atomic_load(reinterpret_cast<const unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 template <typename V, typename S, typename MV, typename I, bool D16, int SPW>
@@ -372,7 +386,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   const double crit = scal[S_CRIT];
   V om_prev = V(0);
   // all-gather of one double per block (fixed-order sum, same in every block);
-  // `data`: R / P stores precede it (write-through: drained, then acquire)
+  // `data`: R / P stores precede it (write-through: drained before the publish)
   auto exchange = [&](double part, int t, int xid, bool data) -> bool {
     const double bp = block_sum1_t0(part, wsum);
     tmark(xid == 0 ? 0 : 2);
@@ -388,10 +402,6 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       const bool ok = sweep_partials(gr, G, tag, words, ctrl, &shv[0]);
       if (tid == 0) {
         flag = ok ? 1 : 0;
-        if (data) {  // the other blocks' R / P stores are visible to this block's loads
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
       }
     }
     __syncthreads();
@@ -442,7 +452,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
             } else if (t == 0) {
               xv[u] = P0[col[u]];
             } else {
-              const V rj = R[col[u]], pj = Pprev[col[u]];
+              const V rj = ld_wt(R + col[u]), pj = ld_wt(Pprev + col[u]);
               const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
               xv[u] = rj + tt;
             }
@@ -643,7 +653,7 @@ bool cgp_launch(kry_cg *s, int max_steps) {
   const kry_csr *A = s->A;
   bool taken = false;
   if (s->cgp_spw != 0 && s->k == 1 && !s->M && !s->Ml && !s->w && !s->comm && A->nirregular == 0 && A->cb_nb == 0 &&
-      A->sptr && max_steps > 0) {
+      A->sptr && A->nslices > 0 && max_steps > 0) {
     const bool f32 = s->scalar_f32;
     if (A->compact)
       taken = f32 ? cgp_launch_t<V, float, MV, I, true>(s, max_steps) : cgp_launch_t<V, double, MV, I, true>(s, max_steps);
@@ -893,14 +903,8 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   reset_ctrl(s->ctrl, st);
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
   Ctrl c;
-  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
-  KRY_HIP(hipStreamSynchronize(st));
+  const int done = read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, hk, resnorms, &c);
   KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: an in-launch exchange timed out");
-  const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
-  if (done > 0) {
-    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));
-    KRY_HIP(hipStreamSynchronize(st));
-  }
   s->it += done;
   *steps_done = done;
   KRY_API_END

@@ -594,14 +594,7 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   reset_ctrl(s->ctrl, st);
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
   Ctrl c;
-  KRY_HIP(hipMemcpyAsync(&c, s->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
-  KRY_HIP(hipStreamSynchronize(st));
-  const int done = c.stop_at < max_steps ? c.stop_at : max_steps;
-  if (done > 0) {
-    const int hk = s->comm ? s->total_k : s->k;
-    KRY_HIP(hipMemcpyAsync(resnorms, s->hist, (size_t)done * hk * 8, hipMemcpyDeviceToHost, st));
-    KRY_HIP(hipStreamSynchronize(st));
-  }
+  const int done = read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, s->comm ? s->total_k : s->k, resnorms, &c);
   s->it += done;
   s->wflip = (s->wflip + done) & 1;
   s->invariant = c.invariant != 0;

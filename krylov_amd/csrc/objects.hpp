@@ -22,6 +22,9 @@ struct kry_ctx {
   // scratch for one-shot reductions and scalar staging (blas.hip, kry_dot)
   double *scratch = nullptr;
   size_t scratch_bytes = 0;
+  // pinned host staging for the per-chunk readback (control word + history)
+  void *pinned = nullptr;
+  size_t pinned_bytes = 0;
 };
 
 struct kry_csr {

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <climits>
+#include <cstring>
 
 #include <rccl/rccl.h>
 
@@ -122,10 +123,44 @@ __device__ __forceinline__ bool all_le(const double *vals, const double *crit, i
   return r;
 }
 
-// Host helper: reset the control word to "run everything".
+template <int D = 0>
+__global__ void ctrl_reset_kernel(Ctrl *c) {
+  c->stop_at = INT_MAX;
+  c->invariant = 0;
+  c->status = 0;
+  c->pad = 0;
+}
+
+// Host helper: reset the control word to "run everything" (a one-thread
+// kernel on the stream: no pageable host copy in the chunk's critical path).
 inline void reset_ctrl(Ctrl *d_ctrl, hipStream_t st) {
-  static const Ctrl fresh = {INT_MAX, 0, 0, 0};
-  KRY_HIP(hipMemcpyAsync(d_ctrl, &fresh, sizeof(Ctrl), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(ctrl_reset_kernel<0>, dim3(1), dim3(1), 0, st, d_ctrl);
+  KRY_HIP(hipGetLastError());
+}
+
+// End of a chunk: the control word and the chunk's history rows (all
+// max_steps of them, a few KB) through pinned staging with ONE host sync;
+// returns the steps done (min(stop_at, max_steps)) and copies their rows.
+inline int read_chunk(kry_ctx *ctx, hipStream_t st, const Ctrl *d_ctrl, const double *d_hist, int max_steps, int hk,
+                      double *resnorms, Ctrl *c) {
+  const size_t hb = (size_t)(max_steps > 0 ? max_steps : 0) * hk * 8;
+  const size_t need = 64 + hb;
+  if (ctx->pinned_bytes < need) {
+    if (ctx->pinned) KRY_HIP(hipHostFree(ctx->pinned));
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+    const size_t sz = need < 65536 ? 65536 : need;
+    KRY_HIP(hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault));
+    ctx->pinned_bytes = sz;
+  }
+  char *h = static_cast<char *>(ctx->pinned);
+  KRY_HIP(hipMemcpyAsync(h, d_ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, st));
+  if (hb) KRY_HIP(hipMemcpyAsync(h + 64, d_hist, hb, hipMemcpyDeviceToHost, st));
+  KRY_HIP(hipStreamSynchronize(st));
+  memcpy(c, h, sizeof(Ctrl));
+  const int done = c->stop_at < max_steps ? c->stop_at : max_steps;
+  if (done > 0) memcpy(resnorms, h + 64, (size_t)done * hk * 8);
+  return done;
 }
 
 inline void check_vec(const kry_vec *v, int64_t n, int k, int dtype, const char *what) {
