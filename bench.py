@@ -3,8 +3,9 @@
 Workload (BASELINE.json metric): CG on the 3-D 15-point stencil
 216^3 (n = 10,077,696, nnz = 149,770,936, fp64, int32 indices), b = ones,
 tol = 0 (fixed iteration count). One step = one CG iteration: the SpMV
-(+ <p,Ap>) launch, the fused x/r update (+ <r,r>) launch, the p pass and two
-one-block scalar kernels, no host sync inside a 32-iteration chunk.
+(+ <p,Ap>) launch, the one-block alpha kernel, the r pass (+ <r,r>) and the
+fused rho / y / p pass; no host sync inside a chunk (kry_cg_preferred_chunk:
+32 iterations here, 256 on the persistent small-n loop of cfg2).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--quick]
 
@@ -114,13 +115,14 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     A = krylov_amd.CsrOperator(A_host, device=local)
     comm = distributed.ShardComm.from_torch(device=local) if pg is not None else None
     st, ncols = _cg_state(A, np.ones(A.n), comm, rank, world)
-    _iterate(st, warmup, ncols)
+    chunk = st.preferred_chunk()
+    _iterate(st, warmup, ncols, chunk)
     ctx.synchronize()
     ctx.profile(True)
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
-    _iterate(st, steps, ncols)
+    _iterate(st, steps, ncols, chunk)
     ctx.synchronize()
     t1 = time.perf_counter()
     barrier(pg)
@@ -143,10 +145,11 @@ def run_cg_config(A_host, B, steps, warmup=5):
     ctx = get_context()
     A = krylov_amd.CsrOperator(A_host)
     st, ncols = _cg_state(A, B)
-    _iterate(st, warmup, ncols)
+    chunk = st.preferred_chunk()  # as krylov_amd.cg drives this solve
+    _iterate(st, warmup, ncols, chunk)
     ctx.synchronize()
     t0 = time.perf_counter()
-    _iterate(st, steps, ncols)
+    _iterate(st, steps, ncols, chunk)
     ctx.synchronize()
     t = time.perf_counter() - t0
     k = 1 if B.ndim == 1 else B.shape[1]

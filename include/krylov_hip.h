@@ -142,6 +142,11 @@ int kry_cg_set_preconditioners(kry_cg *s, kry_csr *M, kry_csr *Ml);
 int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0);
 int kry_cg_set_criterion(kry_cg *s, const double *criterion);
 int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnorms);
+/* Iterations per kry_cg_run call this solve is best driven with (after
+ * kry_cg_start): 256 when it runs the persistent small-n loop (one launch per
+ * call, nothing launched past convergence), 32 otherwise. The driver-side
+ * chunking of the reference's loop (cg.py:155-234) is free to use any value. */
+int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
 int kry_cg_scalars(kry_cg *s, double *out);

@@ -3,8 +3,8 @@
 The loop structure, stop rule, explicit-residual recheck and ``Info`` record
 are the reference's; every iteration's arithmetic (SpMV, inner products, the
 x/r/p updates and the scalar recurrences) runs on the GPU through
-``kry_cg_run`` in chunks of up to ``CHUNK`` iterations with one host sync per
-chunk. The device stops a chunk right after the first iteration whose
+``kry_cg_run`` in chunks of up to ``kry_cg_preferred_chunk`` iterations (32;
+256 on the persistent small-n loop) with one host sync per chunk. The device stops a chunk right after the first iteration whose
 residual norms satisfy the criterion, so the host sees exactly the
 iterations the reference performs.
 """
@@ -48,6 +48,13 @@ class _CGState:
         check(lib.kry_cg_run(self.h, int(steps), ctypes.byref(done), _lib.dptr(out)))
         return out[: done.value]
 
+    def preferred_chunk(self):
+        """Iterations per run call (after start): 256 on the persistent
+        small-n loop, 32 on the launch-per-pass path."""
+        n = ctypes.c_int32()
+        check(lib.kry_cg_preferred_chunk(self.h, ctypes.byref(n)))
+        return n.value
+
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)
         check(lib.kry_cg_residual(self.h, _lib.dptr(out)))
@@ -86,6 +93,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
 
     st = _CGState(prob)
     rho0 = st.start()
+    chunk = st.preferred_chunk()
     rn0 = _norm_from_sq(prob, rho0)
     if callback is not None:
         callback(x0_host, prob.unpad_vec(st.get(1), prob.r0_dtype))
@@ -105,7 +113,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
                 break
         if k == maxiter:
             break
-        steps = 1 if (callback is not None or lanczos is not None) else min(_helpers.CHUNK, maxiter - k)
+        steps = 1 if (callback is not None or lanczos is not None) else min(chunk, maxiter - k)
         hist = st.run(steps)
         for row in hist:
             resnorms.append(prob.colvals(row))

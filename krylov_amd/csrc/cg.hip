@@ -573,7 +573,7 @@ void cg_start_impl(kry_cg *s) {
 // launch-per-pass path. Decided once per solver (s->cgp_spw); the words are
 // zeroed per launch so the granule tags restart at step 0.
 template <typename V, typename S, typename MV, typename I, bool D16>
-bool cgp_launch_t(kry_cg *s, int max_steps) {
+bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   const kry_csr *A = s->A;
   auto kern_for = [](int spw) {
     switch (spw) {
@@ -605,6 +605,7 @@ bool cgp_launch_t(kry_cg *s, int max_steps) {
     }
   }
   if (s->cgp_spw == 0) return false;
+  if (decide_only) return true;
   const int spw = s->cgp_spw;
   const int G = (int)((A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw));
   hipStream_t st = s->ctx->stream;
@@ -648,18 +649,22 @@ bool cgp_launch_t(kry_cg *s, int max_steps) {
 }
 
 // KRY_CG_PERSIST=0 disables the persistent loop; =2 requires it (tests).
+// decide_only: report eligibility (deciding it once) without launching.
 template <typename V, typename MV, typename I>
-bool cgp_launch(kry_cg *s, int max_steps) {
+bool cgp_launch(kry_cg *s, int max_steps, bool decide_only = false) {
   const kry_csr *A = s->A;
   bool taken = false;
   if (s->cgp_spw != 0 && s->k == 1 && !s->M && !s->Ml && !s->w && !s->comm && A->nirregular == 0 && A->cb_nb == 0 &&
       A->sptr && A->nslices > 0 && max_steps > 0) {
     const bool f32 = s->scalar_f32;
     if (A->compact)
-      taken = f32 ? cgp_launch_t<V, float, MV, I, true>(s, max_steps) : cgp_launch_t<V, double, MV, I, true>(s, max_steps);
+      taken = f32 ? cgp_launch_t<V, float, MV, I, true>(s, max_steps, decide_only)
+                  : cgp_launch_t<V, double, MV, I, true>(s, max_steps, decide_only);
     else
-      taken = f32 ? cgp_launch_t<V, float, MV, I, false>(s, max_steps) : cgp_launch_t<V, double, MV, I, false>(s, max_steps);
+      taken = f32 ? cgp_launch_t<V, float, MV, I, false>(s, max_steps, decide_only)
+                  : cgp_launch_t<V, double, MV, I, false>(s, max_steps, decide_only);
   }
+  if (decide_only) return taken;
   const char *e = getenv("KRY_CG_PERSIST");
   KRY_REQUIRE(taken || max_steps <= 0 || !(e && atoi(e) == 2), KRY_EUNSUPPORTED,
               "KRY_CG_PERSIST=2: this solve is not eligible for the persistent CG loop");
@@ -907,6 +912,21 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: an in-launch exchange timed out");
   s->it += done;
   *steps_done = done;
+  KRY_API_END
+}
+
+int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && steps, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(s->started, KRY_EINVAL, "kry_cg_start has not been called");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  bool persist = false;
+  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) {
+    persist = cgp_launch<decltype(v0), decltype(m0), decltype(i0)>(s, 1, true);
+  });
+  // one launch per chunk and no halted launches after convergence: long
+  // chunks cost nothing; the launch-per-pass path keeps 32
+  *steps = persist ? 256 : 32;
   KRY_API_END
 }
 

@@ -418,3 +418,27 @@ def test_cg_persistent_image_variants(monkeypatch, variant):
     _, ref = krylov_ref.cg(R, b, tol=1e-9, maxiter=500)
     assert ref.numsteps == fast.numsteps
     np.testing.assert_allclose(np.asarray(fast.resnorms)[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+
+
+@pytest.mark.gpu
+def test_cg_preferred_chunk(monkeypatch):
+    """kry_cg_preferred_chunk: 256 iterations per call on the persistent
+    small-n loop, 32 on the launch-per-pass path (KRY_CG_PERSIST=0, or a
+    weighted inner product)."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+
+    R = problems.poisson2d(100)
+    A = krylov_amd.CsrOperator(R)
+    b = np.ones(R.shape[0])
+
+    def chunk(inner=None):
+        st = _CGState(_helpers.Problem(A, b, None, inner))
+        st.start()
+        return st.preferred_chunk()
+
+    assert chunk() == 256
+    assert chunk(krylov_amd.WeightedInner(np.full(R.shape[0], 2.0))) == 32
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    assert chunk() == 32
