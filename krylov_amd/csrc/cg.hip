@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       tlast = now;
     }
   };
-  constexpr int UNR = 4;     // 8 spills at 128 VGPRs (two gathers per slot)
+  constexpr int UNR = 5;  // a 5-point row in one round of loads; 8 spills at 128 VGPRs
   constexpr int ROWS = SPW * kCgpBlock;  // rows of this block: [row0, row0 + ROWS)
   __shared__ double wsum[kCgpWaves];
   __shared__ double shv[2];
@@ -373,14 +373,14 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int64_t s0 = ((int64_t)blockIdx.x * kCgpWaves + wid) * SPW;
   const int lr0 = wid * SPW * 64 + lane;  // local row of slice i: lr0 + 64 i
-  V r[SPW], p[SPW];
+  V r[SPW];  // p_t of the block's rows lives in LDS (ps), by local row
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
     const bool own = s0 + i < nslices && row < n;
     ys[i * kCgpBlock + tid] = own ? Y[row] : V(0);
     r[i] = own ? R[row] : V(0);
-    p[i] = own ? P0[row] : V(0);
+    ps[lr0 + 64 * i] = own ? P0[row] : V(0);
   }
   S rho = (S)scal[S_RHO];
   const double crit = scal[S_CRIT];
@@ -411,10 +411,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   int t = 0;
   tmark(-1);
   for (; t < max_steps; ++t) {
-    // p_t of the block's rows into LDS
-#pragma unroll
-    for (int i = 0; i < SPW; ++i) ps[lr0 + 64 * i] = p[i];
-    __syncthreads();
+    __syncthreads();  // p_t of the block's rows complete in LDS
     // p_t(j) of other blocks' rows: at t = 0 from P0 (kernel boundary); after
     // that r_t(j) + omega p_{t-1}(j), the owner's operations
     const V *Pprev = (t & 1) ? P0 : P1;  // holds p_{t-1} (t >= 1)
@@ -464,7 +461,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
               acc = acc + pr;
             }
         }
-        if (sl * 64 + lane < n) pap += dterm((double)p[i], (double)acc);
+        if (sl * 64 + lane < n) pap += dterm((double)ps[lr0 + 64 * i], (double)acc);
       }
       aps[i * kCgpBlock + tid] = acc;
     }
@@ -491,11 +488,13 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
       const int64_t row = (s0 + i) * 64 + lane;
-      const V t1 = a * p[i];
+      const V pv = ps[lr0 + 64 * i];
+      const V t1 = a * pv;
       ys[i * kCgpBlock + tid] = ys[i * kCgpBlock + tid] + t1;  // cg.py:196
-      const V tt = omV * p[i];
-      p[i] = r[i] + tt;  // cg.py:178
-      if (s0 + i < nslices && row < n) st_wt(Pnext + row, p[i]);
+      const V tt = omV * pv;
+      const V pn = r[i] + tt;  // cg.py:178
+      ps[lr0 + 64 * i] = pn;  // every wave is past this iteration's SpMV (exchange barriers)
+      if (s0 + i < nslices && row < n) st_wt(Pnext + row, pn);
     }
     tmark(5);
     const S nrm = sqrt(rrS);
@@ -523,7 +522,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t row = (s0 + i) * 64 + lane;
     if (s0 + i < nslices && row < n) {
       Y[row] = ys[i * kCgpBlock + tid];
-      P0[row] = p[i];
+      P0[row] = ps[lr0 + 64 * i];
     }
   }
 }
