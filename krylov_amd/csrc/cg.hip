@@ -293,8 +293,8 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 // ------------------------------------- persistent CG for launch-bound sizes
 // One launch runs a whole chunk of iterations of the fused path (no M / Ml,
 // one RHS, default inner) on at most one 1024-thread block per CU, all
-// resident. Wave gw owns SPW consecutive SELL slices; each lane keeps r and p
-// of its rows in registers across iterations (y and Ap in LDS). Per iteration:
+// resident. Wave gw owns SPW consecutive SELL slices; each lane keeps r of its
+// rows in registers across iterations, y, Ap and p_t in LDS. Per iteration:
 //   SpMV of the own rows, <p, Ap> block partial   -> all-gather #1 -> alpha
 //   r -= alpha Ap (stored write-through), <r, r>  -> drain, all-gather #2
 //                                                    -> rho, omega
@@ -363,9 +363,9 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   __shared__ double wsum[kCgpWaves];
   __shared__ double shv[2];
   __shared__ int flag;
-  // LDS: y and Ap of the block's rows (r and p stay in registers) and p_t of
-  // the block's rows by local row, so that in-block columns (most of a
-  // banded matrix's) are gathered from LDS; SPW = 4 doubles is 96 KB of 160
+  // LDS: y and Ap of the block's rows (r stays in registers) and p_t of the
+  // block's rows by local row, so that in-block columns (most of a banded
+  // matrix's) are gathered from LDS; SPW = 4 doubles is 96 KB of 160
   __shared__ V ys[ROWS], aps[ROWS], ps[ROWS];
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int64_t s0 = ((int64_t)blockIdx.x * kCgpWaves + wid) * SPW;
   const int lr0 = wid * SPW * 64 + lane;  // local row of slice i: lr0 + 64 i
-  V r[SPW];  // p_t of the block's rows lives in LDS (ps), by local row
+  V r[SPW];
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
