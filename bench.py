@@ -153,8 +153,13 @@ def run_cg_config(A_host, B, steps, warmup=5):
     ctx.synchronize()
     t = time.perf_counter() - t0
     k = 1 if B.ndim == 1 else B.shape[1]
+    # algorithmic_gbs: SURVEY §8(d)'s per-iteration bytes of the launch-per-pass
+    # CG over the measured time. The persistent small-n loop (cfg2) keeps y and
+    # Ap on chip and moves about half of them (profiles/r01_pmc_cfg2.json), so
+    # there this figure is an effective rate, not HBM traffic.
     return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "rhs": k, "n": A.n, "nnz": A.nnz,
-            "gbs": cg_iteration_bytes(A.n, A.nnz, k) * steps / t / 1e9}
+            "algorithmic_gbs": cg_iteration_bytes(A.n, A.nnz, k) * steps / t / 1e9,
+            "persistent_loop": chunk == 256}
 
 
 def run_gmres():

@@ -147,6 +147,15 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
  * call, nothing launched past convergence), 32 otherwise. The driver-side
  * chunking of the reference's loop (cg.py:155-234) is free to use any value. */
 int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps);
+/* Which path the last kry_cg_run chunk took (host-side bookkeeping, no
+ * device work): info[0] = 1 if it ran as the persistent small-n loop (one
+ * cooperative launch per chunk), 0 if launch per pass; info[1] = chunks that
+ * were rerun launch per pass after an in-launch exchange timed out (a block
+ * that never became resident). The rerun starts from the chunk-start state,
+ * which the persistent loop never overwrites, so the history is that of an
+ * uninterrupted solve. Fault injection for tests: KRY_CGP_FAULT=t makes the
+ * last block drop out at iteration t of a chunk. */
+int kry_cg_path(kry_cg *s, int32_t *info);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
 int kry_cg_scalars(kry_cg *s, double *out);
@@ -181,6 +190,13 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done,
 int kry_gmres_solution(kry_gmres *s);
 int kry_gmres_residual(kry_gmres *s, double *resnorm);
 int kry_gmres_get(kry_gmres *s, int which, void *host);
+/* info[0] = 1 while Arnoldi steps run their MGS passes as one persistent
+ * launch (gm_mgsp_kernel), 0 launch per pass (not eligible, or switched off
+ * after a timeout); info[1] = chunks finished launch per pass after a
+ * persistent MGS exchange timed out. The timed-out step is rerun from its
+ * SpMV, so the history is that of an uninterrupted solve. Fault injection
+ * for tests: KRY_MGS_FAULT=s makes the last block drop out at chunk step s. */
+int kry_gmres_path(kry_gmres *s, int32_t *info);
 /* multi_solve_triangular (gmres.py:24-38) as a standalone call: per column c
  * of k, out[:, c] = R[:, :, c]^-1 y[:, c] for upper-triangular R (m x m x k,
  * C order) and y (m x k), host float64 arrays; arithmetic in `dtype`

@@ -8,7 +8,7 @@ import os
 
 import numpy as np
 
-from .errors import ArgumentError
+from .errors import exception_for
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
@@ -69,6 +69,7 @@ _SIGNATURES = {
     "kry_cg_set_criterion": [_vp, _dp],
     "kry_cg_run": [_vp, _i32, _ip32, _dp],
     "kry_cg_preferred_chunk": [_vp, _ip32],
+    "kry_cg_path": [_vp, _ip32],
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
     "kry_cg_scalars": [_vp, _dp],
@@ -86,6 +87,7 @@ _SIGNATURES = {
     "kry_gmres_solution": [_vp],
     "kry_gmres_residual": [_vp, _dp],
     "kry_gmres_get": [_vp, _int, _vp],
+    "kry_gmres_path": [_vp, _ip32],
     "kry_minres_create": [_vp, _vp, _i32, _int, _pvp],
     "kry_minres_destroy": [_vp],
     "kry_minres_start": [_vp, _vp, _vp, _vp, _dp],
@@ -119,21 +121,10 @@ EXPORTED = sorted(list(_SIGNATURES) + ["kry_version", "kry_last_error"])
 
 
 def check(rc):
-    """Map a C-ABI status to the exception the reference would raise."""
+    """Raise the exception the reference would raise for a C-ABI status."""
     if rc == KRY_OK:
         return
-    msg = (lib.kry_last_error() or b"").decode(errors="replace")
-    if rc == KRY_EINVARIANT:
-        raise ArgumentError(msg)
-    if rc == KRY_ENOMEM:
-        raise MemoryError(msg)
-    if rc in (KRY_EINVAL, KRY_ENONFINITE):
-        raise ValueError(msg)
-    if rc == KRY_EUNSUPPORTED:
-        raise NotImplementedError(msg)
-    if rc == KRY_ESINGULAR:
-        raise np.linalg.LinAlgError(msg)
-    raise RuntimeError(f"libkrylov_hip error {rc}: {msg}")
+    raise exception_for(rc, (lib.kry_last_error() or b"").decode(errors="replace"))
 
 
 def dtype_code(dt):

@@ -55,6 +55,14 @@ class _CGState:
         check(lib.kry_cg_preferred_chunk(self.h, ctypes.byref(n)))
         return n.value
 
+    def path(self):
+        """(persistent, fallbacks): whether the last run chunk was one
+        persistent launch, and how many chunks were rerun launch per pass
+        after an in-launch exchange timed out (kry_cg_path)."""
+        info = (ctypes.c_int32 * 2)()
+        check(lib.kry_cg_path(self.h, info))
+        return bool(info[0]), int(info[1])
+
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)
         check(lib.kry_cg_residual(self.h, _lib.dptr(out)))

@@ -20,6 +20,10 @@
 //  residual-norm vector and a tiny global stop test.)
 // The p update is its own streaming pass (not folded into the SpMV's gather):
 // the SpMV then gathers one vector instead of two, which is what bounds it.
+#include <string>
+#include <tuple>
+#include <utility>
+
 #include "solver_common.hpp"
 
 using namespace kry;
@@ -49,11 +53,18 @@ struct kry_cg {
   int col_offset = 0, total_k = 0;
   double *gbuf = nullptr;  // total_k (allreduced residual norms)
   double *gcrit = nullptr; // total_k
-  // persistent small-n loop (cg_persist_kernel): second p buffer, barrier
-  // and granule words; cgp_spw = -1 undecided, 0 not used, else slices/wave
-  void *pb = nullptr;
+  // persistent small-n loop (cg_persist_kernel): its scratch r, two p
+  // buffers, the y output, the scalar staging slots, barrier and granule
+  // words; cgp_spw = -1 undecided, 0 not used, else slices/wave. The kernel
+  // never writes the solver's own y, r, p or scalar slots: after a clean
+  // chunk the host swaps the buffers in, after a timed-out one it keeps the
+  // chunk-start state and reruns the chunk on the launch-per-pass path.
+  void *rs = nullptr, *pb = nullptr, *pb2 = nullptr, *yb = nullptr;
+  double *cgp_scal = nullptr;  // S_COUNT slots
   unsigned *cgp_words = nullptr;
   int cgp_spw = -1;
+  int cgp_fallbacks = 0;  // chunks rerun on the launch-per-pass path after a timeout
+  bool cgp_last = false;  // the last kry_cg_run chunk ran the persistent loop
 };
 
 namespace {
@@ -308,8 +319,11 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 // Scalar arithmetic is that of cg_alpha_kernel / cg_yp_kernel and every
 // block derives the same bits (fixed-order sums); the dot products are summed
 // in another order than the launch-per-pass path's, so the two agree to
-// rounding, not bitwise. The state left behind (y, r, p in s->p, the scalar
-// slots, the history, the stop word) has the fused path's layout.
+// rounding, not bitwise.
+// Inputs are read-only: r_t lives in Rs, p_{t+1} in Pb[t & 1], y in LDS and,
+// after a clean chunk, in Yout; the scalar slots go to Sout. A timed-out
+// exchange (a block that is not resident, kSpinLimit) therefore leaves the
+// chunk-start state intact, whichever blocks got how far.
 constexpr int kCgpBlock = 1024;
 constexpr int kCgpWaves = kCgpBlock / 64;
 constexpr int kCgpGran = 4 * 2 * 256;                 // (exchange, parity) regions x 2 words x G <= 256
@@ -340,12 +354,20 @@ __device__ __forceinline__ V ld_wt(const V *p) {
         __hip_atomic_load(reinterpret_cast<const unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+template <typename V>
+struct CgpBufs {
+  const V *Yin, *Rin, *Pin;  // chunk-start state (never written)
+  V *Yout, *Rs, *Pa, *Pb;    // y after a clean chunk; scratch r; p_{t+1} in (t & 1 ? Pb : Pa)
+  const double *Sin;         // scalar slots (read)
+  double *Sout;              // scalar slots after a clean chunk
+};
+
 template <typename V, typename S, typename MV, typename I, bool D16, int SPW>
 __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
     const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
-    int64_t nslices, int64_t n, V *__restrict__ Y, V *R, V *P0, V *P1, double *scal, double *hist,
-    unsigned *words, Ctrl *ctrl, int max_steps, unsigned long long *tbuf) {
+    int64_t nslices, int64_t n, CgpBufs<V> B, double *hist, unsigned *words, Ctrl *ctrl, int max_steps,
+    unsigned long long *tbuf, int fault_step) {
   if (halted(ctrl, 0)) return;
   // optional phase trace (tbuf != null, KRY_CGP_TRACE): thread 0's wall-clock
   // split of an iteration into SpMV / all-gather #1 wait / r update / store
@@ -370,6 +392,10 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = gridDim.x;
+  // fault injection (tests): the last block stops publishing at iteration
+  // fault_step, as a block that never became resident would
+  const bool faulty = fault_step >= 0 && (int)blockIdx.x == G - 1;
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int64_t s0 = ((int64_t)blockIdx.x * kCgpWaves + wid) * SPW;
   const int lr0 = wid * SPW * 64 + lane;  // local row of slice i: lr0 + 64 i
@@ -378,12 +404,13 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
     const bool own = s0 + i < nslices && row < n;
-    ys[i * kCgpBlock + tid] = own ? Y[row] : V(0);
-    r[i] = own ? R[row] : V(0);
-    ps[lr0 + 64 * i] = own ? P0[row] : V(0);
+    ys[i * kCgpBlock + tid] = own ? B.Yin[row] : V(0);
+    r[i] = own ? B.Rin[row] : V(0);
+    ps[lr0 + 64 * i] = own ? B.Pin[row] : V(0);
   }
-  S rho = (S)scal[S_RHO];
-  const double crit = scal[S_CRIT];
+  S rho = (S)B.Sin[S_RHO];
+  const double crit = B.Sin[S_CRIT];
+  S alpha = (S)B.Sin[S_ALPHA], rho_prev = (S)B.Sin[S_RHO_PREV], omega = (S)B.Sin[S_OMEGA];
   V om_prev = V(0);
   // all-gather of one double per block (fixed-order sum, same in every block);
   // `data`: R / P stores precede it (write-through: drained before the publish)
@@ -399,7 +426,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     }
     if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, bp);
     if (tid < 64) {
-      const bool ok = sweep_partials(gr, G, tag, words, ctrl, &shv[0]);
+      const bool ok = sweep_partials(gr, G, tag, words, ctrl, &shv[0], spin_limit);
       if (tid == 0) {
         flag = ok ? 1 : 0;
       }
@@ -412,9 +439,9 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   tmark(-1);
   for (; t < max_steps; ++t) {
     __syncthreads();  // p_t of the block's rows complete in LDS
-    // p_t(j) of other blocks' rows: at t = 0 from P0 (kernel boundary); after
+    // p_t(j) of other blocks' rows: at t = 0 from Pin (kernel boundary); after
     // that r_t(j) + omega p_{t-1}(j), the owner's operations
-    const V *Pprev = (t & 1) ? P0 : P1;  // holds p_{t-1} (t >= 1)
+    const V *Pprev = t == 1 ? B.Pin : ((t & 1) ? B.Pb : B.Pa);  // holds p_{t-1} (t >= 1)
     double pap = 0.0;
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
@@ -447,9 +474,9 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
             } else if (col[u] < 0) {
               xv[u] = V(0);
             } else if (t == 0) {
-              xv[u] = P0[col[u]];
+              xv[u] = B.Pin[col[u]];
             } else {
-              const V rj = ld_wt(R + col[u]), pj = ld_wt(Pprev + col[u]);
+              const V rj = ld_wt(B.Rs + col[u]), pj = ld_wt(Pprev + col[u]);
               const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
               xv[u] = rj + tt;
             }
@@ -465,9 +492,10 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       }
       aps[i * kCgpBlock + tid] = acc;
     }
+    if (faulty && t == fault_step) return;
     if (!exchange(pap, t, 0, false)) return;
     const S pAp = (S)shv[0];
-    const S alpha = rho / safe<S>(pAp);  // cg.py:183-185
+    alpha = rho / safe<S>(pAp);  // cg.py:183-185
     const V a = (V)(double)alpha;
     double rr = 0.0;
 #pragma unroll
@@ -476,7 +504,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       const V t2 = a * aps[i * kCgpBlock + tid];
       r[i] = r[i] - t2;  // cg.py:200
       if (s0 + i < nslices && row < n) {
-        st_wt(R + row, r[i]);
+        st_wt(B.Rs + row, r[i]);
         rr += dterm((double)r[i], (double)r[i]);
       }
     }
@@ -484,7 +512,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const S rrS = (S)shv[0];
     const S om = rrS / safe<S>(rho);
     const V omV = (V)(double)om;
-    V *Pnext = (t & 1) ? P0 : P1;  // p_{t+1}
+    V *Pnext = (t & 1) ? B.Pb : B.Pa;  // p_{t+1}
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
       const int64_t row = (s0 + i) * 64 + lane;
@@ -498,15 +526,10 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     }
     tmark(5);
     const S nrm = sqrt(rrS);
-    if (blockIdx.x == 0 && tid == 0) {
-      scal[S_ALPHA] = (double)alpha;
-      scal[S_RHO_OLD] = (double)rho;
-      scal[S_RHO_PREV] = (double)rho;
-      scal[S_RHO] = (double)rrS;
-      scal[S_OMEGA] = (double)om;
-      hist[t] = (double)nrm;
-    }
+    if (blockIdx.x == 0 && tid == 0) hist[t] = (double)nrm;
+    rho_prev = rho;
     rho = rrS;
+    omega = om;
     om_prev = omV;
     if ((double)nrm <= crit) {  // cg.py:156 (uniform: every block has the same bits)
       if (blockIdx.x == 0 && tid == 0) ctrl->stop_at = t + 1;
@@ -516,14 +539,21 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   }
   if (tbuf && tid == 0)
     for (int k = 0; k < 6; ++k) tbuf[blockIdx.x * 8 + k] = tacc[k];
-  // leave the fused path's state: y, r (already stored), the current p in P0
+  // a clean chunk: y to Yout (r and p are already in Rs and Pb), the scalar
+  // slots to Sout (the fused path's layout; S_RHO_OLD = the rho alpha used)
+  if (blockIdx.x == 0 && tid == 0 && t > 0) {
+    B.Sout[S_ALPHA] = (double)alpha;
+    B.Sout[S_RHO_OLD] = (double)rho_prev;
+    B.Sout[S_RHO_PREV] = (double)rho_prev;
+    B.Sout[S_RHO] = (double)rho;
+    B.Sout[S_OMEGA] = (double)omega;
+    B.Sout[S_CRIT] = crit;
+    B.Sout[S_TMP] = B.Sin[S_TMP];
+  }
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
-    if (s0 + i < nslices && row < n) {
-      Y[row] = ys[i * kCgpBlock + tid];
-      P0[row] = ps[lr0 + 64 * i];
-    }
+    if (s0 + i < nslices && row < n) B.Yout[row] = ys[i * kCgpBlock + tid];
   }
 }
 
@@ -571,6 +601,14 @@ void cg_start_impl(kry_cg *s) {
 // (SPW slices per wave, SPW in 1..4: n <= 1 M at 256 CUs; 8 spills); false = use the
 // launch-per-pass path. Decided once per solver (s->cgp_spw); the words are
 // zeroed per launch so the granule tags restart at step 0.
+// The launch is cooperative: the runtime refuses a grid larger than the
+// occupancy query admits (hipErrorCooperativeLaunchTooLarge), and the solve
+// then stays on the launch-per-pass path. That check is all a cooperative
+// launch adds on this chip (MI355X_MICROARCH.md "coop-launch": same residency
+// as a plain launch, +15-19 us per launch = < 0.1 us per iteration at 256
+// iterations per chunk); CUs held by another stream or process can still keep
+// a block from becoming resident, which the bounded exchanges and the host's
+// rerun (kry_cg_run) cover.
 template <typename V, typename S, typename MV, typename I, bool D16>
 bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   const kry_csr *A = s->A;
@@ -585,11 +623,12 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
     s->cgp_spw = 0;
     const char *e = getenv("KRY_CG_PERSIST");
     if (!(e && atoi(e) == 0)) {
-      int dev = 0, ncu = 0;
+      int dev = 0, ncu = 0, coop = 0;
       KRY_HIP(hipGetDevice(&dev));
       KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      KRY_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
       const int gmax = ncu < 256 ? ncu : 256;
-      for (int spw = 1; spw <= 4; spw *= 2) {
+      for (int spw = 1; coop && spw <= 4; spw *= 2) {
         const int64_t G = (A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw);
         if (G > gmax) continue;
         int per_cu = 0;
@@ -598,7 +637,12 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
         break;
       }
       if (s->cgp_spw > 0) {
-        s->pb = dev_alloc(((size_t)s->n + 15) / 16 * 16 * sizeof(V));
+        const size_t vb = ((size_t)s->n + 15) / 16 * 16 * sizeof(V);
+        s->rs = dev_alloc(vb);
+        s->pb = dev_alloc(vb);
+        s->pb2 = dev_alloc(vb);
+        s->yb = dev_alloc(vb);
+        s->cgp_scal = static_cast<double *>(dev_alloc(S_COUNT * 8));
         s->cgp_words = static_cast<unsigned *>(dev_alloc(kCgpBytes));
       }
     }
@@ -609,19 +653,41 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   const int G = (int)((A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw));
   hipStream_t st = s->ctx->stream;
   KRY_HIP(hipMemsetAsync(s->cgp_words, 0, kCgpBytes, st));
+  KRY_HIP(hipMemcpyAsync(s->cgp_scal, s->scal, S_COUNT * 8, hipMemcpyDeviceToDevice, st));
   unsigned long long *tb = nullptr;
   if (getenv("KRY_CGP_TRACE")) {
     KRY_HIP(hipMalloc(&tb, (size_t)G * 64));
     KRY_HIP(hipMemsetAsync(tb, 0, (size_t)G * 64, st));
   }
-  ProfScope ps(s->ctx, PROF_OTHER);
-  hipLaunchKernelGGL(kern_for(spw), dim3(G), dim3(kCgpBlock), 0, st, static_cast<const int64_t *>(A->sptr),
-                     static_cast<const int *>(A->swidth), static_cast<const I *>(A->sidx),
-                     static_cast<const uint16_t *>(A->sdelta), static_cast<const int *>(A->scbase),
-                     static_cast<const MV *>(A->sval), A->nslices, A->n, static_cast<V *>(s->y),
-                     static_cast<V *>(s->r), static_cast<V *>(s->p), static_cast<V *>(s->pb), s->scal, s->hist,
-                     s->cgp_words, s->ctrl, max_steps, tb);
-  KRY_HIP(hipGetLastError());
+  const char *fe = getenv("KRY_CGP_FAULT");  // fault injection (tests): iteration at which a block drops out
+  int fault_step = fe ? atoi(fe) : -1;
+  CgpBufs<V> bufs{static_cast<const V *>(s->y), static_cast<const V *>(s->r), static_cast<const V *>(s->p),
+                  static_cast<V *>(s->yb),      static_cast<V *>(s->rs),      static_cast<V *>(s->pb),
+                  static_cast<V *>(s->pb2),     s->scal,                      s->cgp_scal};
+  const int64_t *a_sptr = static_cast<const int64_t *>(A->sptr);
+  const int *a_swidth = static_cast<const int *>(A->swidth);
+  const I *a_sidx = static_cast<const I *>(A->sidx);
+  const uint16_t *a_sdelta = static_cast<const uint16_t *>(A->sdelta);
+  const int *a_scbase = static_cast<const int *>(A->scbase);
+  const MV *a_sval = static_cast<const MV *>(A->sval);
+  int64_t nsl = A->nslices, n = A->n;
+  double *hist = s->hist;
+  unsigned *words = s->cgp_words;
+  Ctrl *ctrl = s->ctrl;
+  void *args[] = {&a_sptr, &a_swidth, &a_sidx, &a_sdelta, &a_scbase, &a_sval, &nsl, &n,
+                  &bufs,   &hist,     &words,  &ctrl,     &max_steps, &tb,    &fault_step};
+  hipError_t le;
+  {
+    ProfScope ps(s->ctx, PROF_OTHER);
+    le = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern_for(spw)), dim3(G), dim3(kCgpBlock), args, 0,
+                                    st);
+  }
+  if (le != hipSuccess) {
+    (void)hipGetLastError();  // clear the refusal; the solve continues on the launch-per-pass path
+    s->cgp_spw = 0;
+    if (tb) KRY_HIP(hipFree(tb));
+    return false;
+  }
   if (tb) {  // KRY_CGP_TRACE: per-phase split, per-block sums of wall_clock64 ticks (100 MHz), to stderr
     std::vector<unsigned long long> h((size_t)G * 8);
     KRY_HIP(hipMemcpyAsync(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost, st));
@@ -647,6 +713,20 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   return true;
 }
 
+// After a persistent chunk of `done` clean iterations: the state it left in
+// its own buffers becomes the solver's (r_T in rs, p_T in pb / pb2 by the
+// parity of T, y_T in yb, the scalar slots in cgp_scal).
+static void cgp_commit(kry_cg *s, int done) {
+  if (done <= 0) return;
+  std::swap(s->r, s->rs);
+  std::swap(s->y, s->yb);
+  if ((done - 1) & 1)
+    std::swap(s->p, s->pb2);
+  else
+    std::swap(s->p, s->pb);
+  KRY_HIP(hipMemcpyAsync(s->scal, s->cgp_scal, S_COUNT * 8, hipMemcpyDeviceToDevice, s->ctx->stream));
+}
+
 // KRY_CG_PERSIST=0 disables the persistent loop; =2 requires it (tests).
 // decide_only: report eligibility (deciding it once) without launching.
 template <typename V, typename MV, typename I>
@@ -670,12 +750,13 @@ bool cgp_launch(kry_cg *s, int max_steps, bool decide_only = false) {
   return taken;
 }
 
+// Returns true when the chunk ran as one persistent launch.
 template <typename V, typename MV, typename I>
-void cg_run_impl(kry_cg *s, int max_steps) {
+bool cg_run_impl(kry_cg *s, int max_steps) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
-  if (cgp_launch<V, MV, I>(s, max_steps)) return;
+  if (cgp_launch<V, MV, I>(s, max_steps)) return true;
   double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
   for (int step = 0; step < max_steps; ++step) {
     V *p = static_cast<V *>(s->p);
@@ -752,6 +833,7 @@ void cg_run_impl(kry_cg *s, int max_steps) {
       KRY_HIP(hipGetLastError());
     }
   }
+  return false;
 }
 
 template <typename V, typename MV, typename I>
@@ -787,8 +869,10 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
   }
 
 static void cg_free(kry_cg *s) {
-  void *bufs[] = {s->b, s->x0, s->y, s->r, s->p, s->Ap, s->z, s->t, s->xk, s->rt, s->w, s->part, s->scal, s->hist,
-                  s->ctrl, s->gbuf, s->gcrit, s->pb, s->cgp_words};
+  void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
+                  s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
+                  s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
+                  s->cgp_scal, s->cgp_words};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -904,11 +988,27 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * hk * 8));
     s->chunk_cap = max_steps;
   }
-  reset_ctrl(s->ctrl, st);
-  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  auto run_chunk = [&](Ctrl *c) -> std::pair<int, bool> {
+    reset_ctrl(s->ctrl, st);
+    bool persistent = false;
+    dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) {
+      persistent = cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps);
+    });
+    return {read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, hk, resnorms, c), persistent};
+  };
   Ctrl c;
-  const int done = read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, hk, resnorms, &c);
-  KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: an in-launch exchange timed out");
+  auto [done, persistent] = run_chunk(&c);
+  if (persistent && c.status == KRY_EDEVICE) {
+    // an in-launch exchange timed out (a block was not resident): the kernel
+    // left the chunk-start state untouched; rerun the chunk launch per pass
+    s->cgp_spw = 0;
+    ++s->cgp_fallbacks;
+    std::tie(done, persistent) = run_chunk(&c);
+  } else if (persistent) {
+    cgp_commit(s, done);
+  }
+  KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: device error status " + std::to_string(c.status));
+  s->cgp_last = persistent;
   s->it += done;
   *steps_done = done;
   KRY_API_END
@@ -926,6 +1026,14 @@ int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps) {
   // one launch per chunk and no halted launches after convergence: long
   // chunks cost nothing; the launch-per-pass path keeps 32
   *steps = persist ? 256 : 32;
+  KRY_API_END
+}
+
+int kry_cg_path(kry_cg *s, int32_t *info) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
+  info[0] = s->cgp_last ? 1 : 0;
+  info[1] = s->cgp_fallbacks;
   KRY_API_END
 }
 

@@ -67,6 +67,7 @@ struct kry_gmres {
   int col_offset = 0, total_k = 0;
   int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
   int mgsp_grid = 0;
+  int mgsp_fallbacks = 0;  // chunks finished launch per pass after a persistent MGS timeout
   double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
   int chunk_cap = 0;
   int steps = 0;           // Arnoldi iterations done (arnoldi.iter)
@@ -218,7 +219,7 @@ __device__ __forceinline__ void mgs_arrive(unsigned *bar, unsigned epoch) {
 // Wait for every block's arrival. Every spin is bounded: on timeout the block
 // raises ctrl->status = KRY_EDEVICE and the abort word, and every block
 // leaves. Returns false (in every thread) in that case.
-__device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag) {
+__device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag, unsigned spin_limit = kSpinLimit) {
   if (threadIdx.x == 0) {
     const int G = gridDim.x;
     const unsigned ngroups = G < 8 ? (unsigned)G : 8u;
@@ -231,7 +232,7 @@ __device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag) {
         ok = 0;
         break;
       }
-      if (spins > kSpinLimit) {
+      if (spins > spin_limit) {
         __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
                                                             int sweeps, const double *__restrict__ part0, int P0,
                                                             double *__restrict__ pbuf, double *__restrict__ h,
                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
-                                                            int step) {
+                                                            int step, int fault_step) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int NV = E / W;
@@ -302,6 +303,17 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int G = gridDim.x;
+  // fault injection (tests, KRY_MGS_FAULT): the last block never takes part
+  // in chunk step fault_step, as a block that never became resident
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  // A timed-out exchange ends the launch with w (this step's A V_k) and the
+  // partial buffers as they were, and halts the rest of the chunk from this
+  // step on (stop_at); kry_gmres_run reruns the step on the launch-per-pass
+  // path, whose first sweep rewrites every h[j] this launch may have touched.
+  auto abort_step = [&]() {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+  };
   const int64_t base = (int64_t)blockIdx.x * NV * kMgsBlock;
   V wr[NV][W], vc[NV][W], vn[NV][W];
   auto ld = [&](const V *src, V(&dst)[NV][W]) {
@@ -383,11 +395,11 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
       if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
       if (const V *q2 = next_of(p + 1)) ld(q2, vn);
       if (tid < 64) {
-        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha);
+        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
         if (tid == 0) flag = ok ? 1 : 0;
       }
       __syncthreads();
-      if (!flag) return;
+      if (!flag) return abort_step();
       continue;
     }
     if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
     // prefetch the vector after next only now: the drain in mgs_arrive must
     // not wait for it (vmcnt is in order); it travels during the wait
     if (const V *q2 = next_of(p + 1)) ld(q2, vn);
-    if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag)) return;
+    if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
     reduce_rows<kMgsBlock, true>(slot, G, k, red);
     if (tid < k) alpha[tid] = red[tid];
     __syncthreads();
@@ -1010,9 +1022,11 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(s->bar + (size_t)s->chunk_cap * kBarWords);
   double *pbuf = s->part2;  // [pass parity 0 | parity 1 | last pass], G * k each
   ProfScope ps(s->ctx, PROF_MGS);
+  const char *fe = getenv("KRY_MGS_FAULT");  // fault injection (tests): chunk step at which a block drops out
+  const int fault_step = fe ? atoi(fe) : -1;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
-                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step);
+                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step);
   };
   if (E == 8) go(gm_mgsp_kernel<V, 8>);
   else if (E == 16) go(gm_mgsp_kernel<V, 16>);
@@ -1378,11 +1392,28 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
     s->bar = static_cast<unsigned *>(dev_alloc(bar_bytes(max_steps)));
     s->chunk_cap = max_steps;
   }
-  reset_ctrl(s->ctrl, st);
-  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  const int hk = s->comm ? s->total_k : s->k;
+  auto run_chunk = [&](int steps, double *rows, Ctrl *c) {
+    reset_ctrl(s->ctrl, st);
+    dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { gm_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, steps); });
+    return read_chunk(s->ctx, st, s->ctrl, s->hist, steps, hk, rows, c);
+  };
   Ctrl c;
-  const int done = read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, s->comm ? s->total_k : s->k, resnorms, &c);
-  if (c.status == KRY_EDEVICE) throw Error{KRY_EDEVICE, "persistent MGS kernel: grid barrier timed out"};
+  int done = run_chunk(max_steps, resnorms, &c);
+  if (c.status == KRY_EDEVICE && s->mgsp_E > 0) {
+    // the persistent MGS kernel timed out at step `done` (a block was not
+    // resident) and halted the chunk there: keep the steps before it and run
+    // the rest of the chunk launch per pass, from that step's SpMV (V_k is in
+    // the basis; the step's h entries are rewritten by its first sweep)
+    s->steps += done;
+    s->mgsp_E = 0;
+    s->vpending = false;
+    ++s->mgsp_fallbacks;
+    const int more = run_chunk(max_steps - done, resnorms + (size_t)done * hk, &c);
+    s->steps -= done;
+    done += more;
+  }
+  if (c.status == KRY_EDEVICE) throw Error{KRY_EDEVICE, "GMRES: device error during the chunk"};
   s->steps += done;
   s->invariant = c.invariant != 0;
   s->have_solution = false;
@@ -1420,6 +1451,14 @@ int kry_gmres_residual(kry_gmres *s, double *norm2) {
 // (= V without M), m = steps (steps - 1 after an invariant step), each n x k;
 // 3: the Hessenberg matrix H, (maxiter + 1) x maxiter x k, column j filled
 // for j < steps (arnoldi.py:158-196, the relation A V_m = V_{m+1} H).
+int kry_gmres_path(kry_gmres *s, int32_t *info) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
+  info[0] = s->mgsp_E > 0 ? 1 : 0;
+  info[1] = s->mgsp_fallbacks;
+  KRY_API_END
+}
+
 int kry_gmres_get(kry_gmres *s, int which, void *host) {
   KRY_API_BEGIN
   KRY_REQUIRE(s && host && which >= 0 && which <= 3, KRY_EINVAL, "bad argument");

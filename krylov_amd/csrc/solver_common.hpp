@@ -28,8 +28,36 @@ namespace kry {
 // so every block derives the same bits. Tags must be unique among the words
 // a region holds between zeroings. Every spin is bounded: on timeout the
 // kernel raises ctrl->status = KRY_EDEVICE and the abort word, and every
-// block leaves.
+// block leaves; the host then reruns the work on the launch-per-pass path
+// (kry_cg_run / kry_gmres_run), which needs no co-residency.
+//
+// Memory-ordering argument (gfx950 only, see the guard below). The protocol
+// uses relaxed operations only, and rests on how gfx950 lowers them
+// (MI355X_MICROARCH.md, "Valid forms" and its hand-off table, row 1):
+//  - data handed to other blocks (CG's r and p, the MGS partials) is stored
+//    with agent-scope relaxed atomic stores = `global_store ... sc1`, which
+//    write through the XCD's L2 to the fabric;
+//  - every storing wave runs `s_waitcnt vmcnt(0)` and then the workgroup
+//    barrier before ONE lane publishes the block's granule (also `sc1`), so
+//    every data store has been acknowledged before the tag can be seen;
+//  - the reader polls the granules with agent-scope relaxed loads
+//    (`global_load ... sc1`, which bypass the CU's L1), then a workgroup
+//    barrier, and reads the data only with `sc1` loads (ld_wt / ld_agent):
+//    never from L1, so no `buffer_inv` is needed.
+// The granule itself is a single naturally aligned 8-byte store, observed
+// untorn. None of this is promised by the HIP memory model: a different
+// target (gfx942's non-coherent per-XCD L2 with other cache policies) or a
+// compiler that reorders relaxed atomics across the inline-asm wait could
+// read stale data. Hence the compile-time guard, and the cross-XCD parity
+// tests (CG at G = 245 blocks, tests/test_gpu_solvers.py) as the guard for
+// compiler upgrades.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "the in-launch exchanges of the persistent kernels are validated for gfx950 (MI355X) only"
+#endif
 constexpr unsigned kSpinLimit = 1u << 20;
+// Shorter bound for the fault-injection runs (KRY_CGP_FAULT / KRY_MGS_FAULT),
+// so that a test of the timeout path finishes in milliseconds.
+constexpr unsigned kSpinLimitFault = 1u << 12;
 
 __device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned tag, double v) {
   const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
@@ -39,7 +67,8 @@ __device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned 
 }
 
 // Wave 0 only; returns the same value in every lane (false = timed out / aborted).
-__device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out) {
+__device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out,
+                                      unsigned spin_limit = kSpinLimit) {
   const int lane = threadIdx.x;
   unsigned long long g[4][2];
   unsigned spins = 0;
@@ -59,7 +88,7 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
     ++spins;
     if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
       return false;
-    if (spins > kSpinLimit) {
+    if (spins > spin_limit) {
       if (lane == 0) {
         __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -82,6 +82,14 @@ class _GmresState:
     def solution(self):
         check(lib.kry_gmres_solution(self.h))
 
+    def path(self):
+        """(persistent, fallbacks): whether Arnoldi steps run their MGS as one
+        persistent launch, and how many chunks finished launch per pass after a
+        persistent MGS exchange timed out (kry_gmres_path)."""
+        info = (ctypes.c_int32 * 2)()
+        check(lib.kry_gmres_path(self.h, info))
+        return bool(info[0]), int(info[1])
+
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)
         check(lib.kry_gmres_residual(self.h, _lib.dptr(out)))

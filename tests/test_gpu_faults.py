@@ -1,0 +1,105 @@
+"""Timeout path of the persistent kernels (fault injection).
+
+The persistent CG loop and the persistent MGS kernel exchange partial sums
+between blocks inside one launch, so they need every block resident. A block
+that never becomes resident (CUs held by another stream or process) makes the
+others' bounded spins time out. These tests force that with
+KRY_CGP_FAULT / KRY_MGS_FAULT (the last block drops out at a given step, and
+the spin bound shrinks to milliseconds) and check that the solve still
+returns the reference's iterations: the kernel leaves the chunk-start state
+(CG) or the step's input (GMRES) untouched, and the host reruns the work on
+the launch-per-pass path, which needs no co-residency.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fault_step", [0, 3])
+def test_cg_persistent_timeout_falls_back(monkeypatch, fault_step):
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref
+
+    R = problems.poisson2d(300)  # 88 blocks of 1024 threads
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(11).standard_normal(R.shape[0])
+    _, clean = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.setenv("KRY_CGP_FAULT", str(fault_step))
+    _, faulted = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    assert faulted.numsteps == clean.numsteps
+    f, c = np.asarray(faulted.resnorms), np.asarray(clean.resnorms)
+    np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-10)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-10, atol=1e-12 * np.abs(clean.xk).max())
+    _, ref = krylov_ref.cg(R, b, tol=1e-9, maxiter=500)
+    assert ref.numsteps == faulted.numsteps
+    np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+
+
+def test_cg_timeout_after_committed_chunks(monkeypatch):
+    """Clean persistent chunks first (their state swapped in), then a chunk
+    that times out and is rerun launch per pass: the whole history equals a
+    launch-per-pass solve's to round-off."""
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+    import krylov_amd
+
+    R = problems.poisson2d(200)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(12).standard_normal(R.shape[0])
+
+    def state():
+        st = _CGState(_helpers.Problem(A, b, None, None))
+        st.start()
+        st.set_criterion(np.zeros(1))
+        return st
+
+    st = state()
+    h1 = st.run(7)
+    h2 = st.run(5)
+    assert st.path() == (True, 0)
+    monkeypatch.setenv("KRY_CGP_FAULT", "2")
+    h3 = st.run(40)
+    assert st.path() == (False, 1)
+    h4 = st.run(9)  # stays launch per pass
+    assert st.path() == (False, 1)
+    got = np.concatenate([h1, h2, h3, h4])[:, 0]
+    x_got = st.get(0)[:, 0]
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    monkeypatch.delenv("KRY_CGP_FAULT")
+    ref = state()
+    want = ref.run(61)[:, 0]
+    assert ref.path() == (False, 0)
+    np.testing.assert_allclose(got, want, rtol=1e-10)
+    np.testing.assert_allclose(x_got, ref.get(0)[:, 0], rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("ortho", ["mgs", "mgs2"])
+def test_gmres_persistent_mgs_timeout_falls_back(monkeypatch, ortho):
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.gmres import _GmresState
+    from oracle import krylov_ref
+
+    R = problems.random_nonsym(200_000)
+    A = krylov_amd.CsrOperator(R)
+    b = np.ones(R.shape[0])
+    _, clean = krylov_amd.gmres(A, b, ortho=ortho, maxiter=30, tol=1e-9)
+    monkeypatch.setenv("KRY_MGS_FAULT", "2")
+    _, faulted = krylov_amd.gmres(A, b, ortho=ortho, maxiter=30, tol=1e-9)
+    assert faulted.numsteps == clean.numsteps
+    f, c = np.asarray(faulted.resnorms), np.asarray(clean.resnorms)
+    np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-11)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-9, atol=1e-12)
+    if ortho == "mgs":
+        _, ref = krylov_ref.gmres(R, b, maxiter=30, tol=1e-9)
+        assert ref.numsteps == faulted.numsteps
+        np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+    # the state reports the switch
+    st = _GmresState(_helpers.Problem(A, b, None, None), 30, 1 if ortho == "mgs" else 2)
+    st.start()
+    st.set_criterion(np.zeros(1))
+    hist, _ = st.run(6)
+    assert len(hist) == 6
+    assert st.path() == (False, 1)
