@@ -81,12 +81,16 @@ int kry_csr_destroy(kry_csr *A);
  * kernel walks in CSR form instead. */
 int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
                    int64_t *nslots, int64_t *nirregular);
-/* The device image kry_csr_create built: info[0..4] = slices, slots,
+/* The device image kry_csr_create built: info[0..6] = slices, slots,
  * irregular slices, compact (1 when the column indices are stored as uint16
  * deltas over per-slot-column int32 bases: every slot column spans <= 65534
- * columns, int32 indices and KRY_SELL_COMPACT != 0 in the environment), and
- * the number of column blocks of the column-blocked image used by
- * single-RHS SpMVs on scattered sparsity (0 = none; KRY_SPMV_CB=0 disables). */
+ * columns, int32 indices and KRY_SELL_COMPACT != 0 in the environment), the
+ * number of column blocks of the column-blocked image used by single-RHS
+ * SpMVs on scattered sparsity (0 = none; KRY_SPMV_CB=0 disables), dia (1 when
+ * the diagonal-offset image serves single-RHS SpMVs: int32 indices, every row
+ * strictly sorted, the rows of each 64-row slice sharing a short list of
+ * column offsets; KRY_SPMV_DIA=0 disables) and that image's slot count.
+ * `info` must hold 7 values. */
 int kry_csr_info(const kry_csr *A, int64_t *info);
 
 /* ---- vectors (n x k row-major blocks) ---------------------------------- */

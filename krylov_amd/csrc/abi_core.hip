@@ -244,6 +244,8 @@ int kry_csr_info(const kry_csr *A, int64_t *info) {
   info[2] = A->nirregular;
   info[3] = A->compact ? 1 : 0;
   info[4] = A->cb_nb;
+  info[5] = A->dia ? 1 : 0;
+  info[6] = A->dia_nslots;
   KRY_API_END
 }
 
@@ -304,6 +306,98 @@ static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int
   for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
   for (auto &x : th) x.join();
   return ok.load();
+}
+
+// Diagonal-offset image (see kry_csr::dia_*). Pass 1 collects every slice's
+// sorted offset list (col - row over its entries) and checks that each row is
+// strictly sorted, so a row's entries occur in the slot order of their
+// offsets: the per-row summation order stays the stored order (bitwise
+// csr_matvec). Pass 2 places entry (row, col) in the slot column of offset
+// col - row and sets the lane's mask bit. Returns false (nothing built) for
+// unsorted or duplicate entries, or when the image would hold more than
+// 1.25x the SELL image's slots (offsets not shared across the slice's rows).
+template <typename MV>
+struct DiaHost {
+  std::vector<int64_t> sptr;
+  std::vector<int32_t> width;
+  std::vector<DiaCol> meta;
+  std::vector<MV> val;
+  int max_width = 0;
+};
+
+template <typename I, typename MV>
+static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, DiaHost<MV> &d) {
+  if (sizeof(I) != 4 || n == 0) return false;
+  const int64_t ns = (n + kSlice - 1) / kSlice;
+  std::vector<std::vector<int32_t>> offs(ns);
+  std::atomic<bool> ok{true};
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 4096) nt = 1;
+  auto pass1 = [&](int64_t sa, int64_t sb) {
+    std::vector<int32_t> o;
+    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
+      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+      o.clear();
+      for (int64_t r = r0; r < r1; ++r)
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
+          if (e > ip[r] && ix[e] <= ix[e - 1]) {  // unsorted or duplicate: stored order is not offset order
+            ok = false;
+            return;
+          }
+          o.push_back((int32_t)((int64_t)ix[e] - r));
+        }
+      std::sort(o.begin(), o.end());
+      o.erase(std::unique(o.begin(), o.end()), o.end());
+      if ((int64_t)o.size() * kSlice > 2 * ((int64_t)ip[r1] - (int64_t)ip[r0]) + 1024) {
+        ok = false;  // offsets not shared across the slice's rows
+        return;
+      }
+      offs[s] = o;
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass1, ns * t / nt, ns * (t + 1) / nt);
+    for (auto &x : th) x.join();
+  }
+  if (!ok) return false;
+  d.sptr.assign(ns + 1, 0);
+  d.width.assign(ns, 0);
+  for (int64_t s = 0; s < ns; ++s) {
+    d.width[s] = (int32_t)offs[s].size();
+    d.max_width = std::max(d.max_width, d.width[s]);
+    d.sptr[s + 1] = d.sptr[s] + (int64_t)kSlice * d.width[s];
+  }
+  const int64_t slots = d.sptr[ns];
+  if (slots * 4 > sell_slots * 5) return false;
+  d.meta.assign(slots / kSlice + kDiaPad, DiaCol{0, 0, 0});
+  d.val.assign(slots + 256, MV(0));
+  auto pass2 = [&](int64_t sa, int64_t sb) {
+    for (int64_t s = sa; s < sb; ++s) {
+      const std::vector<int32_t> &o = offs[s];
+      const int64_t base = d.sptr[s];
+      DiaCol *m = d.meta.data() + base / kSlice;
+      for (size_t j = 0; j < o.size(); ++j) m[j].off = o[j];
+      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+      for (int64_t r = r0; r < r1; ++r) {
+        const int lane = (int)(r - r0);
+        size_t j = 0;
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
+          const int32_t off = (int32_t)((int64_t)ix[e] - r);
+          while (o[j] != off) ++j;  // the row's offsets ascend, as the list's do
+          m[j].mask |= uint64_t(1) << lane;
+          d.val[base + (int64_t)j * kSlice + lane] = dv[e];
+          ++j;
+        }
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass2, ns * t / nt, ns * (t + 1) / nt);
+    for (auto &x : th) x.join();
+  }
+  return true;
 }
 
 // Column-blocked image (see kry_csr::cb_*). Returns false when not useful or
@@ -441,9 +535,28 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
   if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
   KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+  // diagonal-offset image for structured single-RHS SpMVs (KRY_SPMV_DIA=0 disables)
+  const char *denv = getenv("KRY_SPMV_DIA");
+  if (!(denv && atoi(denv) == 0)) {
+    DiaHost<MV> dh;
+    if (dia_build(n, ip, ix, dv, A->nslots, dh)) {
+      A->dia = true;
+      A->dia_nslots = dh.sptr.back();
+      A->dia_max_width = dh.max_width;
+      A->dia_sptr = dev_alloc(dh.sptr.size() * 8);
+      A->dia_width = dev_alloc(dh.width.size() * 4 + 4);
+      A->dia_meta = dev_alloc(dh.meta.size() * sizeof(DiaCol));
+      A->dia_val = dev_alloc(dh.val.size() * sizeof(MV));
+      KRY_HIP(hipMemcpyAsync(A->dia_sptr, dh.sptr.data(), dh.sptr.size() * 8, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->dia_width, dh.width.data(), dh.width.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->dia_meta, dh.meta.data(), dh.meta.size() * sizeof(DiaCol), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->dia_val, dh.val.data(), dh.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipStreamSynchronize(st));
+    }
+  }
   // column-blocked image for scattered single-RHS SpMVs (KRY_SPMV_CB=0 disables)
   const char *cbenv = getenv("KRY_SPMV_CB");
-  if (!(cbenv && atoi(cbenv) == 0)) {
+  if (!A->dia && !(cbenv && atoi(cbenv) == 0)) {
     CbHost<MV> cb;
     if (cb_build(n, ip, ix, dv, cb)) {
       A->cb_nb = cb.nb;
@@ -476,8 +589,9 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 }  // namespace
 
 static void csr_free(kry_csr *A) {
-  void *bufs[] = {A->sptr,   A->swidth, A->sidx,   A->sval,   A->indptr, A->indices, A->data,
-                  A->sdelta, A->scbase, A->cb_gptr, A->cb_roff, A->cb_col, A->cb_val,  A->cb_y};
+  void *bufs[] = {A->sptr,   A->swidth,   A->sidx,     A->sval,     A->indptr,    A->indices,
+                  A->data,   A->sdelta,   A->scbase,   A->cb_gptr,  A->cb_roff,   A->cb_col,
+                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_meta, A->dia_val};
   for (void *b : bufs) dev_free(b);
 }
 

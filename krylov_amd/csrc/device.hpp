@@ -520,6 +520,76 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
 }
 
 
+// -------------------------------------------- diagonal-offset SpMV (k = 1)
+// The SELL-64/DIA image (kry_csr::dia_*): lane l of the wave owns row
+// 64 s + l of slice s; slot column j of the slice holds, for every lane whose
+// mask bit is set, the entry at column row + off_j. The slot column's
+// descriptor {off_j, mask_j} is wave-uniform (one scalar load), the values are
+// one contiguous 64-lane load, and the x values of a slot column are the
+// contiguous run x[64 s + off_j, 64 s + off_j + 64): no index stream at all.
+// The offsets of a slice ascend and every row is sorted, so each row is still
+// summed from 0 in stored order, one rounding per product and per add:
+// bitwise csr_matvec.
+template <typename V, typename MV, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restrict__ sptr,
+                                                          const int *__restrict__ swidth,
+                                                          const DiaCol *__restrict__ meta,
+                                                          const MV *__restrict__ val, int64_t nslices, int64_t n,
+                                                          Src src, Epi epi, double *__restrict__ part,
+                                                          const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const auto bs = src.template bind<1>(0);
+  double dacc = 0.0;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * 64 + lane;
+    const DiaCol *mc = meta + (base >> 6);  // wave-uniform: scalar loads
+    const MV *cv = val + base + lane;
+    V acc = V(0);
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      // descriptors: read unconditionally (the array is padded by kDiaPad
+      // columns), all scalar loads in flight before the first use; values:
+      // behind the wave-uniform `in` (a scalar branch, no wait); gathers:
+      // unconditional, a hole's address clamped to x[0], its product dropped
+      // by a select (never added: an inf or NaN there cannot leak in)
+      DiaCol d[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) d[u] = mc[j0 + u];
+      V a[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) a[u] = j0 + u < w ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
+      bool on[UNR];
+      V xv[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        on[u] = j0 + u < w && ((d[u].mask >> lane) & 1u) != 0;
+        xv[u] = bs(on[u] ? row + d[u].off : 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const V p = a[u] * xv[u];
+        const V t = acc + p;
+        acc = on[u] ? t : acc;
+      }
+    }
+    if (row < n) dacc += epi(row, 0, acc, bs(row, 0));
+  }
+  if (part != nullptr) {
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[g] = red[0];
+  }
+}
+
 // ---------------------------------------------------- elementwise passes
 // Op(e, N, acc) handles the W = 16/sizeof(V) consecutive elements at flat
 // index e (a multiple of W) and adds its dot terms to acc[0..W). Each block
@@ -976,6 +1046,19 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
   if constexpr (sizeof(I) == 4) {
+    if (k == 1 && A->dia) {
+      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->nslices + 3) / 4));
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->dia_sptr),
+                           static_cast<const int *>(A->dia_width), static_cast<const DiaCol *>(A->dia_meta),
+                           static_cast<const MV *>(A->dia_val), A->nslices, A->n, src, epi, part, ctrl, step);
+      };
+      if (A->dia_max_width <= 8) go(spmv_dia_kernel<V, MV, 8, Src, Epi>);
+      else go(spmv_dia_kernel<V, MV, 16, Src, Epi>);
+      KRY_HIP(hipGetLastError());
+      if (grid_out) *grid_out = grid;
+      return;
+    }
     if (k == 1 && A->cb_nb > 0 && A->cb_ng <= (int64_t)kCbPersistGrid * kCbMaxOwn) {
       grid = (int)std::min<int64_t>(A->cb_ng, kCbPersistGrid);
       hipLaunchKernelGGL((spmv_cbp_kernel<V, MV, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n,

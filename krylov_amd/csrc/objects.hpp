@@ -56,6 +56,22 @@ struct kry_csr {
   void *cb_col = nullptr;   // int32, nnz (+ pad)
   void *cb_val = nullptr;   // dtype, nnz (+ pad)
   void *cb_y = nullptr;     // double, n: running row sums between passes
+  // diagonal-offset image (SELL-64/DIA, structured matrices, k = 1): in
+  // every slice the columns of each row are row + o_j for a short sorted list
+  // of offsets o_j shared by the slice, so slot column j holds the entry at
+  // offset o_j of every lane (or a masked-off hole). Per slot column one
+  // 16-byte descriptor {int32 offset, pad, uint64 lane mask} replaces the 64
+  // per-lane indices: the matrix stream is the values alone, and the x
+  // gathers of a slot column are one contiguous 64-element run. Built only
+  // for int32 inputs whose every row is strictly sorted, and only when the
+  // slot count stays within 1.25x of the SELL image's.
+  bool dia = false;
+  int64_t dia_nslots = 0;
+  int dia_max_width = 0;
+  void *dia_sptr = nullptr;   // int64, nslices + 1
+  void *dia_width = nullptr;  // int32, nslices
+  void *dia_meta = nullptr;   // DiaCol, dia_nslots / 64 (+ pad)
+  void *dia_val = nullptr;    // dtype, dia_nslots (+ pad); holes are 0
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;

@@ -71,11 +71,12 @@ class CsrOperator:
         return self.ctx.device
 
     def layout(self):
-        """The device image: {"slices", "slots", "irregular", "compact", "col_blocks"}."""
-        info = np.zeros(5, dtype=np.int64)
+        """The device image: {"slices", "slots", "irregular", "compact",
+        "col_blocks", "dia", "dia_slots"}."""
+        info = np.zeros(7, dtype=np.int64)
         check(lib.kry_csr_info(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3]),
-                "col_blocks": int(info[4])}
+                "col_blocks": int(info[4]), "dia": bool(info[5]), "dia_slots": int(info[6])}
 
     def matvec_device(self, x, y):
         """y = A x for DeviceVectors (no host traffic)."""

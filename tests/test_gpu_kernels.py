@@ -62,7 +62,7 @@ def test_spmv_int64_image_through_abi(golden, key):
     _lib.check(_lib.lib.kry_csr_create(ctx.handle, n, ix.shape[0], _lib.ptr(ip), _lib.ptr(ix), _lib.ptr(dv),
                                        _lib.dtype_code(dv.dtype), _lib.KRY_I64, ctypes.byref(h)))
     try:
-        info = np.zeros(4, dtype=np.int64)
+        info = np.zeros(7, dtype=np.int64)
         _lib.check(_lib.lib.kry_csr_info(h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         assert info[3] == 0
         x = DeviceVector.from_host(ctx, d[f"{key}_x"])

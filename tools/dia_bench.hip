@@ -1,0 +1,280 @@
+// Microbenchmark of the diagonal-offset (SELL-64/DIA) SpMV on gfx950
+// (development tool, not product). Uploads the BASELINE metric matrix
+// (3-D 15-point stencil m^3) through the library's C-ABI, then times the
+// library's CG SpMV (Ap stored + <p, Ap> partials) next to probe variants on
+// the same image: no store, no gathers, the value stream alone, a smaller
+// unroll, the next slice's values loaded ahead, interleaved slice order.
+// Every full variant is checked bitwise against the library kernel.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     tools/dia_bench.hip -o tools/dia_bench -Lkrylov_amd -lkrylov_hip -Wl,-rpath,'$ORIGIN/../krylov_amd'
+//   ./tools/dia_bench [m=216] [reps=20]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/krylov_hip.h"
+#include "../krylov_amd/csrc/device.hpp"
+
+using namespace kry;
+
+#define CK(x)                                                                         \
+  do {                                                                                \
+    hipError_t e = (x);                                                               \
+    if (e != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                        \
+    }                                                                                 \
+  } while (0)
+#define KC(x)                                                                             \
+  do {                                                                                    \
+    int r = (x);                                                                          \
+    if (r != KRY_OK) {                                                                    \
+      fprintf(stderr, "%s:%d %s: %d %s\n", __FILE__, __LINE__, #x, r, kry_last_error()); \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+static void build_stencil(int m, std::vector<int> &ip, std::vector<int> &ix, std::vector<double> &dv) {
+  const int64_t n = (int64_t)m * m * m;
+  ip.assign(n + 1, 0);
+  ix.clear();
+  dv.clear();
+  ix.reserve(n * 15);
+  dv.reserve(n * 15);
+  struct Nb {
+    int64_t off;
+    int di, dj, dk;
+  };
+  std::vector<Nb> nb;
+  for (int dk = -1; dk <= 1; ++dk)
+    for (int dj = -1; dj <= 1; ++dj)
+      for (int di = -1; di <= 1; ++di) {
+        int nz = (di != 0) + (dj != 0) + (dk != 0);
+        if (nz == 0 || nz == 1 || nz == 3) nb.push_back({(int64_t)dk * m * m + dj * m + di, di, dj, dk});
+      }
+  std::sort(nb.begin(), nb.end(), [](const Nb &a, const Nb &b) { return a.off < b.off; });
+  for (int64_t r = 0; r < n; ++r) {
+    int i = r % m, j = (r / m) % m, k = r / ((int64_t)m * m);
+    for (auto &q : nb) {
+      int ii = i + q.di, jj = j + q.dj, kk = k + q.dk;
+      if (ii < 0 || ii >= m || jj < 0 || jj >= m || kk < 0 || kk >= m) continue;
+      ix.push_back((int)(r + q.off));
+      dv.push_back(q.off == 0 ? 14.0 : -1.0);
+    }
+    ip[r + 1] = (int)ix.size();
+  }
+}
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void read_ceiling(const d2v *__restrict__ b, int64_t nb, double *out) {
+  double s = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) {
+    d2v v = __builtin_nontemporal_load(b + i);
+    s += v.x + v.y;
+  }
+  if (s == 12345.678) out[0] = s;
+}
+
+// MODE bits: 1 no store, 2 no gathers, 4 values only (no meta, no gathers,
+// no store), 8 next slice's values loaded ahead, 16 interleaved slice order
+template <int UNR, int MODE>
+__global__ __launch_bounds__(256) void dia_probe(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const DiaCol *__restrict__ meta, const double *__restrict__ val,
+                                                 int64_t nslices, int64_t n, const double *__restrict__ x,
+                                                 double *__restrict__ y, double *__restrict__ part) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  int64_t s_begin, s_end, s_step;
+  if (MODE & 16) {
+    s_begin = m;
+    s_end = nslices;
+    s_step = W;
+  } else {
+    s_begin = nslices * m / W;
+    s_end = nslices * (m + 1) / W;
+    s_step = 1;
+  }
+  double dacc = 0.0;
+  double an[UNR];
+  if (MODE & 8) {
+    if (s_begin < s_end) {
+      const int w = swidth[s_begin];
+      const double *cv = val + sptr[s_begin] + lane;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) an[u] = u < w ? __builtin_nontemporal_load(cv + u * 64) : 0.0;
+    }
+  }
+  for (int64_t s = s_begin; s < s_end; s += s_step) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * 64 + lane;
+    const DiaCol *mc = meta + (base >> 6);
+    const double *cv = val + base + lane;
+    double acc = 0.0;
+    if (MODE & 4) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (u < w) acc += __builtin_nontemporal_load(cv + u * 64);
+    } else {
+      for (int j0 = 0; j0 < w; j0 += UNR) {
+        DiaCol d[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) d[u] = mc[j0 + u];
+        double a[UNR];
+        if (MODE & 8) {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) a[u] = an[u];
+          const int64_t sn = s + s_step;
+          if (sn < s_end) {
+            const int wn = swidth[sn];
+            const double *cvn = val + sptr[sn] + lane;
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) an[u] = u < wn ? __builtin_nontemporal_load(cvn + u * 64) : 0.0;
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) a[u] = j0 + u < w ? __builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : 0.0;
+        }
+        bool on[UNR];
+        double xv[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          on[u] = j0 + u < w && ((d[u].mask >> lane) & 1u) != 0;
+          xv[u] = (MODE & 2) ? 1.0 : x[on[u] ? row + d[u].off : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const double p = a[u] * xv[u];
+          const double t = acc + p;
+          acc = on[u] ? t : acc;
+        }
+      }
+    }
+    if (row < n) {
+      if (!(MODE & 1) && !(MODE & 4)) {
+        if (MODE & 32) __builtin_nontemporal_store(acc, y + (row & ((1 << 20) - 1)));  // 8 MB window
+        else if (MODE & 64) y[row] = acc;                                             // plain store
+        else __builtin_nontemporal_store(acc, y + row);
+      }
+      dacc += (MODE & 4) ? acc : x[row] * acc;
+    }
+  }
+  red[tid] = dacc;
+  block_tree_reduce(red, 256, 1);
+  if (tid == 0) part[g] = red[0];
+}
+
+int main(int argc, char **argv) {
+  const int m = argc > 1 ? atoi(argv[1]) : 216;
+  const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  std::vector<int> ip, ix;
+  std::vector<double> dv;
+  build_stencil(m, ip, ix, dv);
+  const int64_t n = (int64_t)ip.size() - 1, nnz = ix.size();
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  kry_csr *A;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+  if (!A->dia) {
+    fprintf(stderr, "no DIA image\n");
+    return 1;
+  }
+  printf("m=%d n=%ld nnz=%ld slices=%ld dia_slots=%ld max_width=%d\n", m, (long)n, (long)nnz, (long)A->nslices,
+         (long)A->dia_nslots, A->dia_max_width);
+  std::vector<double> xh(n);
+  for (int64_t i = 0; i < n; ++i) xh[i] = 1.0 + (double)((i * 7919) % 1000) * 1e-3;
+  double *x, *y, *yref, *part, *dummy;
+  CK(hipMalloc(&x, n * 8));
+  CK(hipMalloc(&y, n * 8));
+  CK(hipMalloc(&yref, n * 8));
+  CK(hipMalloc(&part, kMaxGrid * 8));
+  CK(hipMalloc(&dummy, 64));
+  CK(hipMemcpy(x, xh.data(), n * 8, hipMemcpyHostToDevice));
+  hipStream_t st = ctx->stream;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double S = (double)nnz * 12 + (double)(n + 1) * 4 + 2.0 * n * 8;
+  const double phys = (double)A->dia_nslots * 8 + (double)A->dia_nslots / 64 * 16 + 2.0 * n * 8;
+  auto timeit = [&](const char *name, auto launch) {
+    launch();
+    CK(hipStreamSynchronize(st));
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, st));
+      launch();
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ts.push_back(t);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double ms = ts[ts.size() / 2];
+    printf("%-44s %.4f ms  S-rate %.0f GB/s  image-rate %.0f GB/s\n", name, ms, S / ms / 1e6, phys / ms / 1e6);
+    return ms;
+  };
+  // the library kernel (CG SpMV epilogue)
+  timeit("library spmv_dia (EpiApDot)", [&] {
+    int P;
+    launch_spmv<double, double, int>(A, 1, SrcPlain<double>{x, 1}, EpiApDot<double>{yref, nullptr, 1}, part, &P,
+                                     nullptr, 0, st);
+  });
+  std::vector<double> ref(n), got(n);
+  CK(hipMemcpy(ref.data(), yref, n * 8, hipMemcpyDeviceToHost));
+  const int grid = (int)std::min<int64_t>(kMaxGrid, (A->nslices + 3) / 4);
+  auto check = [&](const char *name) {
+    CK(hipMemcpy(got.data(), y, n * 8, hipMemcpyDeviceToHost));
+    if (memcmp(got.data(), ref.data(), n * 8) != 0) printf("  !! %s differs from the library kernel\n", name);
+  };
+  const double vals_bytes = (double)A->dia_nslots * 8;
+  {
+    const int64_t nb = A->dia_nslots / 2;
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, st));
+      hipLaunchKernelGGL(read_ceiling, dim3(4096), dim3(256), 0, st, (const d2v *)A->dia_val, nb, dummy);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ts.push_back(t);
+    }
+    std::sort(ts.begin(), ts.end());
+    printf("%-44s %.4f ms  %.0f GB/s\n", "read ceiling (value array, 16 B/lane)", ts[reps / 2],
+           vals_bytes / ts[reps / 2] / 1e6);
+  }
+#define PROBE(U, MODE, NAME, CHECK)                                                                              \
+  timeit(NAME, [&] {                                                                                            \
+    hipLaunchKernelGGL((dia_probe<U, MODE>), dim3(grid), dim3(256), 0, st, (const int64_t *)A->dia_sptr,        \
+                       (const int *)A->dia_width, (const DiaCol *)A->dia_meta, (const double *)A->dia_val,      \
+                       A->nslices, n, (const double *)x, y, part);                                              \
+  });                                                                                                           \
+  if (CHECK) check(NAME);
+  PROBE(16, 0, "probe: full (same as library)", true);
+  PROBE(16, 1, "probe: no store", false);
+  PROBE(16, 2, "probe: no gathers", false);
+  PROBE(16, 3, "probe: no gathers, no store", false);
+  PROBE(16, 4, "probe: values only", false);
+  PROBE(8, 0, "probe: UNR 8", true);
+  PROBE(16, 8, "probe: next slice's values ahead", true);
+  PROBE(16, 16, "probe: interleaved slices", true);
+  PROBE(16, 24, "probe: interleaved + values ahead", true);
+  PROBE(16, 32, "probe: store into an 8 MB window", false);
+  PROBE(16, 64, "probe: plain (not nt) store", true);
+  PROBE(16, 80, "probe: interleaved, plain store", true);
+  PROBE(16, 48, "probe: interleaved, 8 MB window", false);
+  KC(kry_csr_destroy(A));
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
