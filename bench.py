@@ -133,8 +133,23 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     del st
     if comm is not None:
         comm.close()
+    layout = A.layout()
     return {"elapsed": elapsed, "spmv_count": cnt, "spmv_ms": spmv_ms, "update_count": ucnt, "update_ms": upd_ms,
-            "n": A.n, "nnz": A.nnz}
+            "n": A.n, "nnz": A.nnz, "layout": layout}
+
+
+def spmv_kernel_desc(layout):
+    """The CG SpMV kernel launch_spmv picks for k = 1 on this image, and the
+    bytes that image moves per launch (next to SURVEY's algorithmic S)."""
+    if layout["dia"]:
+        return ("spmv_dia_kernel<double,double,16,SrcPlain,EpiApDot> (SELL-64/DIA diagonal-offset image: values "
+                "only, one {offset, lane mask} descriptor per slot column; Ap stored + <p,Ap> partials)",
+                "the DIA image moves dia_slots*8 + dia_slots/64*16 for the matrix, no index stream")
+    if layout["compact"]:
+        return ("spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact index "
+                "image, Ap stored + <p,Ap> partials)", "the compact image moves nnz*(8+2) for the matrix")
+    return ("spmv_sell_kernel<double,double,int,1,16,false,SrcPlain,EpiApDot> (SELL-64 SpMV, int32 indices)",
+            "the SELL image moves slots*(8+4) for the matrix")
 
 
 def run_cg_config(A_host, B, steps, warmup=5):
@@ -218,22 +233,26 @@ def run_minres_cfg5(steps=100):
             "config": "cfg5 shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights (vectors f64 as in the reference)"}
 
 
-def pmc_traffic(n, nnz):
+PMC_SUMMARY = "r02_pmc_traffic.json"
+
+
+def pmc_traffic(n, nnz, kernel):
     """HBM bytes per launch of the fused CG SpMV from the committed PMC
     summary (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes, read side
     calibrated on a same-width stream of known size), if it was taken on this
-    workload. PMC needs its own rocprofv3 runs, so it cannot be live here."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    workload and this kernel. PMC needs its own rocprofv3 runs, so it cannot
+    be live here."""
+    path = os.path.join(REPO, "profiles", PMC_SUMMARY)
     try:
         with open(path) as f:
             d = json.load(f)
     except OSError:
         return {}
-    if d.get("n") != n or d.get("nnz") != nnz:
+    if d.get("n") != n or d.get("nnz") != nnz or kernel.split("<")[0] not in d.get("kernel", ""):
         return {}
     return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
-            "source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f "
-                      "calibrated)" % d["read_scale_from_calibration"]}
+            "source": "profiles/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f "
+                      "calibrated)" % (PMC_SUMMARY, d["read_scale_from_calibration"])}
 
 
 def cpu_baseline(A_host, target_s=12.0):
@@ -286,7 +305,8 @@ def main():
     spmv_avg_s = res["spmv_ms"] / max(res["spmv_count"], 1) / 1e3
     spmv_bytes = spmv_S(n, nnz)
     achieved = spmv_bytes / spmv_avg_s / 1e9
-    traffic = pmc_traffic(n, nnz)
+    kname, image_note = spmv_kernel_desc(res["layout"])
+    traffic = pmc_traffic(n, nnz, kname)
     out = {
         "metric": "CG iters/sec + SpMV GB/s (fp64, n=10M, nnz=150M); GMRES(30) iters/sec",
         "value": world * args.steps / T,
@@ -319,11 +339,10 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("traffic_bytes_per_launch"),
             "traffic_source": traffic.get("source"),
-            "kernel": "spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact "
-                      "index image, Ap stored + <p,Ap> partials)",
+            "kernel": kname,
             "bytes_per_launch": spmv_bytes,
-            "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; the "
-                             "compact image moves nnz*(8+2) for the matrix)",
+            "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; "
+                             + image_note + ")",
             "launches_timed": res["spmv_count"],
         },
     }

@@ -2,9 +2,10 @@
 
 Reads <dir>/{micro,bench}_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv,
 averages the counters per kernel name (KiB per dispatch -> bytes), derives
-the read-side scale from the calibration kernel (known bytes = 10 * nslots of
-the 216^3 compact SELL-64 image) and reports the CG SpMV kernel's corrected
-traffic per launch next to its algorithmic bytes.
+the read-side scale from the calibration kernel (tools/dia_bench's
+"values only" probe: known bytes = 8 * dia_slots of the 216^3 diagonal-offset
+image) and reports the CG SpMV kernel's corrected traffic per launch next to
+its algorithmic bytes.
 """
 import csv
 import json
@@ -32,31 +33,43 @@ def find(d, *parts):
     return d[hits[0]][0], hits[0]
 
 
+def dia_slots(out):
+    """dia_slots as printed by tools/dia_bench's first line."""
+    with open(os.path.join(out, "micro_FETCH_SIZE.log")) as f:
+        for tok in f.readline().split():
+            if tok.startswith("dia_slots="):
+                return int(tok.split("=")[1])
+    raise SystemExit("dia_bench header not found")
+
+
 def main(out):
     import bench
-    from krylov_amd import _lib, problems
+    from krylov_amd import problems
 
     A = problems.stencil15_3d(216)
     n, nnz = A.shape[0], int(A.nnz)
-    nslices, nslots, nirr = _lib.csr_layout(A.indptr)
+    slots = dia_slots(out)
     f = lambda w, c: per_kernel(os.path.join(out, f"{w}_{c}", "run_counter_collection.csv"), c)
-    mf, mw, bf, bw = f("micro", "FETCH_SIZE"), f("micro", "WRITE_SIZE"), f("bench", "FETCH_SIZE"), f("bench", "WRITE_SIZE")
-    cal_fetch, _ = find(mf, "sell_stream_calib<unsigned short>")
-    scale = 10.0 * nslots / cal_fetch
-    fetch, name = find(bf, "spmv_sell_kernel", "true", "EpiApDot")
-    write, _ = find(bw, "spmv_sell_kernel", "true", "EpiApDot")
+    mf, bf, bw = f("micro", "FETCH_SIZE"), f("bench", "FETCH_SIZE"), f("bench", "WRITE_SIZE")
+    cal_fetch, _ = find(mf, "dia_probe<16, 4>")
+    scale = 8.0 * slots / cal_fetch
+    fetch, name = find(bf, "spmv_dia_kernel", "EpiApDot")
+    write, _ = find(bw, "spmv_dia_kernel", "EpiApDot")
     alg = bench.spmv_S(n, nnz)
+    phys = 8.0 * slots + 16.0 * slots / 64 + 2.0 * n * 8
     res = {
         "kernel": name,
         "fetch_raw_bytes": fetch,
         "write_bytes": write,
         "read_scale_from_calibration": scale,
-        "calibration": "sell_stream_calib<uint16>: the compact image's 2 + 8 B/lane nontemporal matrix stream, "
-                       "10 B x nslots known bytes, FETCH_SIZE x 1024 measured",
+        "calibration": "dia_probe<16,4> (tools/dia_bench 'values only'): the diagonal-offset image's 8 B/lane "
+                       "nontemporal value stream, 8 B x dia_slots known bytes, FETCH_SIZE x 1024 measured",
         "traffic_bytes_per_launch": fetch * scale + write,
         "algorithmic_bytes_per_launch": alg,
+        "image_bytes_per_launch": phys,
         "traffic_over_algorithmic": (fetch * scale + write) / alg,
-        "nslots": nslots,
+        "traffic_over_image": (fetch * scale + write) / phys,
+        "dia_slots": slots,
         "n": n,
         "nnz": nnz,
     }
