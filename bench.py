@@ -142,9 +142,9 @@ def spmv_kernel_desc(layout):
     """The CG SpMV kernel launch_spmv picks for k = 1 on this image, and the
     bytes that image moves per launch (next to SURVEY's algorithmic S)."""
     if layout["dia"]:
-        return ("spmv_dia_kernel<double,double,16,SrcPlain,EpiApDot> (SELL-64/DIA diagonal-offset image: values "
-                "only, one {offset, lane mask} descriptor per slot column; Ap stored + <p,Ap> partials)",
-                "the DIA image moves dia_slots*8 + dia_slots/64*16 for the matrix, no index stream")
+        return ("spmv_dia_kernel<double,double,16,SrcPlain,EpiApDot> (SELL-128/DIA diagonal-offset image, two rows "
+                "per lane: values only, one offset + two lane masks per slot column; Ap stored + <p,Ap> partials)",
+                "the DIA image moves dia_slots*8 + dia_slots/128*20 for the matrix, no index stream")
     if layout["compact"]:
         return ("spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact index "
                 "image, Ap stored + <p,Ap> partials)", "the compact image moves nnz*(8+2) for the matrix")

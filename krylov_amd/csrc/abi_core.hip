@@ -14,18 +14,24 @@ namespace kry {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 
+// Every device buffer carries kAllocSlack bytes of readable slack before and
+// after it: the diagonal-offset SpMV loads x[j], x[j + 1] as one pair even
+// when one of them is a masked-off hole at j = -1 or j + 1 = n (the value is
+// never used, the address only has to be mapped).
+constexpr size_t kAllocSlack = 256;
+
 void *dev_alloc(size_t bytes) {
   void *p = nullptr;
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc(&p, bytes);
+  hipError_t e = hipMalloc(&p, bytes + 2 * kAllocSlack);
   if (e != hipSuccess)
     throw Error{e == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE,
                 std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e)};
-  return p;
+  return static_cast<char *>(p) + kAllocSlack;
 }
 
 void dev_free(void *p) {
-  if (p) (void)hipFree(p);
+  if (p) (void)hipFree(static_cast<char *>(p) - kAllocSlack);
 }
 
 double *ctx_scratch(kry_ctx *ctx, size_t bytes) {
@@ -313,14 +319,15 @@ static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int
 // strictly sorted, so a row's entries occur in the slot order of their
 // offsets: the per-row summation order stays the stored order (bitwise
 // csr_matvec). Pass 2 places entry (row, col) in the slot column of offset
-// col - row and sets the lane's mask bit. Returns false (nothing built) for
+// col - row and sets the row's mask bit. Returns false (nothing built) for
 // unsorted or duplicate entries, or when the image would hold more than
 // 1.25x the SELL image's slots (offsets not shared across the slice's rows).
 template <typename MV>
 struct DiaHost {
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
-  std::vector<DiaCol> meta;
+  std::vector<int32_t> off;
+  std::vector<uint64_t> mask;
   std::vector<MV> val;
   int max_width = 0;
 };
@@ -328,15 +335,16 @@ struct DiaHost {
 template <typename I, typename MV>
 static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, DiaHost<MV> &d) {
   if (sizeof(I) != 4 || n == 0) return false;
-  const int64_t ns = (n + kSlice - 1) / kSlice;
+  constexpr int H = kDiaSlice;
+  const int64_t ns = (n + H - 1) / H;
   std::vector<std::vector<int32_t>> offs(ns);
   std::atomic<bool> ok{true};
   unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ns < 4096) nt = 1;
+  if (ns < 2048) nt = 1;
   auto pass1 = [&](int64_t sa, int64_t sb) {
     std::vector<int32_t> o;
     for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
-      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H);
       o.clear();
       for (int64_t r = r0; r < r1; ++r)
         for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
@@ -348,7 +356,7 @@ static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t
         }
       std::sort(o.begin(), o.end());
       o.erase(std::unique(o.begin(), o.end()), o.end());
-      if ((int64_t)o.size() * kSlice > 2 * ((int64_t)ip[r1] - (int64_t)ip[r0]) + 1024) {
+      if ((int64_t)o.size() * H > 2 * ((int64_t)ip[r1] - (int64_t)ip[r0]) + 2048) {
         ok = false;  // offsets not shared across the slice's rows
         return;
       }
@@ -366,27 +374,29 @@ static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t
   for (int64_t s = 0; s < ns; ++s) {
     d.width[s] = (int32_t)offs[s].size();
     d.max_width = std::max(d.max_width, d.width[s]);
-    d.sptr[s + 1] = d.sptr[s] + (int64_t)kSlice * d.width[s];
+    d.sptr[s + 1] = d.sptr[s] + (int64_t)H * d.width[s];
   }
   const int64_t slots = d.sptr[ns];
-  if (slots * 4 > sell_slots * 5) return false;
-  d.meta.assign(slots / kSlice + kDiaPad, DiaCol{0, 0, 0});
-  d.val.assign(slots + 256, MV(0));
+  // the 128-row slices may hold up to one slice more padding than SELL-64's
+  if (slots * 4 > sell_slots * 5 + (int64_t)4 * H * d.max_width) return false;
+  const int64_t cols = slots / H;
+  d.off.assign(cols + kDiaPad, 0);
+  d.mask.assign(2 * (cols + kDiaPad), 0);
+  d.val.assign(slots + 2 * H, MV(0));
   auto pass2 = [&](int64_t sa, int64_t sb) {
     for (int64_t s = sa; s < sb; ++s) {
       const std::vector<int32_t> &o = offs[s];
-      const int64_t base = d.sptr[s];
-      DiaCol *m = d.meta.data() + base / kSlice;
-      for (size_t j = 0; j < o.size(); ++j) m[j].off = o[j];
-      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
+      const int64_t base = d.sptr[s], c0 = base / H;
+      for (size_t j = 0; j < o.size(); ++j) d.off[c0 + j] = o[j];
+      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H);
       for (int64_t r = r0; r < r1; ++r) {
-        const int lane = (int)(r - r0);
+        const int rl = (int)(r - r0);
         size_t j = 0;
         for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
           const int32_t off = (int32_t)((int64_t)ix[e] - r);
           while (o[j] != off) ++j;  // the row's offsets ascend, as the list's do
-          m[j].mask |= uint64_t(1) << lane;
-          d.val[base + (int64_t)j * kSlice + lane] = dv[e];
+          d.mask[2 * (c0 + j) + (rl & 1)] |= uint64_t(1) << (rl >> 1);
+          d.val[base + (int64_t)j * H + rl] = dv[e];
           ++j;
         }
       }
@@ -541,15 +551,18 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
     DiaHost<MV> dh;
     if (dia_build(n, ip, ix, dv, A->nslots, dh)) {
       A->dia = true;
+      A->dia_nslices = (int64_t)dh.width.size();
       A->dia_nslots = dh.sptr.back();
       A->dia_max_width = dh.max_width;
       A->dia_sptr = dev_alloc(dh.sptr.size() * 8);
       A->dia_width = dev_alloc(dh.width.size() * 4 + 4);
-      A->dia_meta = dev_alloc(dh.meta.size() * sizeof(DiaCol));
+      A->dia_off = dev_alloc(dh.off.size() * 4);
+      A->dia_mask = dev_alloc(dh.mask.size() * 8);
       A->dia_val = dev_alloc(dh.val.size() * sizeof(MV));
       KRY_HIP(hipMemcpyAsync(A->dia_sptr, dh.sptr.data(), dh.sptr.size() * 8, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->dia_width, dh.width.data(), dh.width.size() * 4, hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->dia_meta, dh.meta.data(), dh.meta.size() * sizeof(DiaCol), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->dia_off, dh.off.data(), dh.off.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->dia_mask, dh.mask.data(), dh.mask.size() * 8, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->dia_val, dh.val.data(), dh.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
     }
@@ -591,7 +604,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 static void csr_free(kry_csr *A) {
   void *bufs[] = {A->sptr,   A->swidth,   A->sidx,     A->sval,     A->indptr,    A->indices,
                   A->data,   A->sdelta,   A->scbase,   A->cb_gptr,  A->cb_roff,   A->cb_col,
-                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_meta, A->dia_val};
+                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val};
   for (void *b : bufs) dev_free(b);
 }
 

@@ -18,13 +18,10 @@ constexpr int kWave = 64;            // CDNA wavefront
 constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
 constexpr int kSlice = 64;           // SELL slice height = one wavefront
-// slot-column descriptor of the diagonal-offset image (kry_csr::dia_meta)
-constexpr int kDiaPad = 32;  // descriptors past the last slot column (unconditional reads of a round)
-struct DiaCol {
-  int32_t off;    // column = row + off for every lane whose mask bit is set
-  int32_t pad;
-  uint64_t mask;  // bit l: lane l has an entry in this slot column
-};
+// diagonal-offset image (kry_csr::dia_*): slices of kDiaSlice rows, lane l
+// of the wave owns rows 2l and 2l + 1 of its slice
+constexpr int kDiaSlice = 128;
+constexpr int kDiaPad = 32;  // slot-column descriptors past the last one (unconditional reads of a round)
 constexpr int kCbRows = 256;         // rows per column-blocked segment (one per thread)
 constexpr int kCbCap = 1024;         // products staged in LDS per chunk
 constexpr int kNumXcd = 8;

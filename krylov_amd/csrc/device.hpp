@@ -66,6 +66,43 @@ __device__ __forceinline__ void vstore_row(V *p, const V (&o)[C]) {
   }
 }
 
+// Two consecutive values at p, aligned to the element only (the
+// diagonal-offset SpMV's x pairs start at row + offset): one 16-byte access
+// for double, 8-byte for float.
+template <typename V>
+struct PairT;
+template <>
+struct PairT<double> {
+  typedef double T __attribute__((ext_vector_type(2), aligned(8)));
+};
+template <>
+struct PairT<float> {
+  typedef float T __attribute__((ext_vector_type(2), aligned(4)));
+};
+template <typename V>
+__device__ __forceinline__ void pload(const V *p, V (&o)[2]) {
+  const typename PairT<V>::T t = *reinterpret_cast<const typename PairT<V>::T *>(p);
+  o[0] = t.x;
+  o[1] = t.y;
+}
+template <typename V>
+__device__ __forceinline__ void pload_nt(const V *p, V (&o)[2]) {
+  const typename PairT<V>::T t = __builtin_nontemporal_load(reinterpret_cast<const typename PairT<V>::T *>(p));
+  o[0] = t.x;
+  o[1] = t.y;
+}
+template <typename V, bool NT = false>
+__device__ __forceinline__ void pstore(V *p, const V (&o)[2]) {
+  const typename PairT<V>::T t = {o[0], o[1]};
+  if (NT) __builtin_nontemporal_store(t, reinterpret_cast<typename PairT<V>::T *>(p));
+  else *reinterpret_cast<typename PairT<V>::T *>(p) = t;
+}
+// dot terms of two consecutive rows i, i + 1 (one column), summed in order
+__device__ __forceinline__ double dterm2(const double *w, int64_t i, double x0, double y0, double x1, double y1) {
+  if (w) return dterm_w(x0, w[i], y0) + dterm_w(x1, w[i + 1], y1);
+  return dterm(x0, y0) + dterm(x1, y1);
+}
+
 // The SpMV input x[j, c] may be materialised on the fly from other vectors
 // (the p-update of CG, the normalisation of GMRES), so the gather never
 // needs a separate pass over HBM. The owner row writes the same value out.
@@ -84,6 +121,8 @@ struct SrcPlain {
     __device__ __forceinline__ V operator()(int64_t j, int c) const { return x[j * k + c0 + c]; }
     // the KT values of row j (lane-group kernel, KT in {2, 4})
     __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const { vload_row<V, KT>(x + j * k + c0, o); }
+    // rows j and j + 1 of a single column (k = 1, diagonal-offset kernel)
+    __device__ __forceinline__ void pair(int64_t j, V (&o)[2]) const { pload<V>(x + j, o); }
   };
   template <int KT>
   __device__ __forceinline__ Bound<KT> bind(int c0) const {
@@ -116,6 +155,17 @@ struct SrcCgP {
       if (first) return rj;
       const V t = om[c] * pold[j * k + c0 + c];
       return rj + t;
+    }
+    __device__ __forceinline__ void pair(int64_t j, V (&o)[2]) const {
+      pload<V>(r + j, o);
+      if (first) return;
+      V q[2];
+      pload<V>(pold + j, q);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const V t = om[0] * q[c];
+        o[c] = o[c] + t;
+      }
     }
     __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const {
       vload_row<V, KT>(r + j * k + c0, o);
@@ -157,6 +207,11 @@ struct SrcScaled {
     V h[KT];
     int k, c0;
     __device__ __forceinline__ V operator()(int64_t j, int c) const { return w[j * k + c0 + c] / h[c]; }
+    __device__ __forceinline__ void pair(int64_t j, V (&o)[2]) const {
+      pload<V>(w + j, o);
+      o[0] = o[0] / h[0];
+      o[1] = o[1] / h[0];
+    }
     __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const {
       vload_row<V, KT>(w + j * k + c0, o);
 #pragma unroll
@@ -192,6 +247,11 @@ struct EpiStore {
   __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
     vstore_row<V, C>(y + i * k + c0, s);
   }
+  // rows i and i + 1 of a single column (k = 1, diagonal-offset kernel)
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V>(y + i, s);
+    return 0.0;
+  }
 };
 
 // y = A v and the first MGS inner product <q, y> (arnoldi.py:176,159).
@@ -214,6 +274,12 @@ struct EpiStoreDot {
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)qv[c], w[i], (double)s[c]) : dterm((double)qv[c], (double)s[c]);
   }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V>(y + i, s);
+    V qv[2];
+    pload<V>(q + i, qv);
+    return dterm2(w, i, (double)qv[0], (double)s[0], (double)qv[1], (double)s[1]);
+  }
 };
 
 // y = A x and <y, y> (weighted): a preconditioned residual M_l r and its norm.
@@ -232,6 +298,10 @@ struct EpiStoreNorm {
     vstore_row<V, C>(y + i * k + c0, s);
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)s[c], w[i], (double)s[c]) : dterm((double)s[c], (double)s[c]);
+  }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V>(y + i, s);
+    return dterm2(w, i, (double)s[0], (double)s[0], (double)s[1], (double)s[1]);
   }
 };
 
@@ -257,6 +327,16 @@ struct EpiAddStore {
       for (int c = 0; c < C; ++c) o[c] = s[c];
     }
     vstore_row<V, C>(out + i * k + c0, o);
+  }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    V o[2] = {s[0], s[1]};
+    if (x0) {
+      pload<V>(x0 + i, o);
+      o[0] = o[0] + s[0];
+      o[1] = o[1] + s[1];
+    }
+    pstore<V>(out + i, o);
+    return 0.0;
   }
 };
 
@@ -284,6 +364,13 @@ struct EpiStoreDotV {
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)qv[c], w[i], (double)s[c]) : dterm((double)qv[c], (double)s[c]);
   }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V>(vout + i, xi);
+    pstore<V>(y + i, s);
+    V qv[2];
+    pload<V>(q + i, qv);
+    return dterm2(w, i, (double)qv[0], (double)s[0], (double)qv[1], (double)s[1]);
+  }
 };
 
 // r = b - A z and <r, r> (cg.py:86-90, gmres.py:106-108).
@@ -309,6 +396,14 @@ struct EpiResidual {
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)ri[c], w[i], (double)ri[c]) : dterm((double)ri[c], (double)ri[c]);
   }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    V ri[2];
+    pload<V>(b + i, ri);
+    ri[0] = ri[0] - s[0];
+    ri[1] = ri[1] - s[1];
+    pstore<V>(r + i, ri);
+    return dterm2(w, i, (double)ri[0], (double)ri[0], (double)ri[1], (double)ri[1]);
+  }
 };
 
 // CG: Ap = A p, write p (materialised by SrcCgP), <p, Ap> (cg.py:178-183).
@@ -333,6 +428,11 @@ struct EpiCgAp {
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
   }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V>(pnew + i, xi);
+    pstore<V, true>(Ap + i, s);
+    return dterm2(w, i, (double)xi[0], (double)s[0], (double)xi[1], (double)s[1]);
+  }
 };
 
 // CG: Ap = A p (nontemporal: read once, by the update pass) and <p, Ap>
@@ -352,6 +452,10 @@ struct EpiApDot {
     vstore_row<V, C, true>(Ap + i * k + c0, s);
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
+  }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    pstore<V, true>(Ap + i, s);
+    return dterm2(w, i, (double)xi[0], (double)s[0], (double)xi[1], (double)s[1]);
   }
 };
 
@@ -393,6 +497,22 @@ struct EpiLanczos {
     vload_row<V, C>(v + i * k + c0, vv);
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)vv[c], w[i], (double)o[c]) : dterm((double)vv[c], (double)o[c]);
+  }
+  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
+    V o[2] = {s[0], s[1]};
+    if (pold) {
+      V po[2];
+      pload<V>(pold + i, po);
+      const V h = (V)h0[0];
+      const V t0 = h * po[0];
+      const V t1 = h * po[1];
+      o[0] = o[0] - t0;
+      o[1] = o[1] - t1;
+    }
+    pstore<V>(out + i, o);
+    V vv[2];
+    pload<V>(v + i, vv);
+    return dterm2(w, i, (double)vv[0], (double)o[0], (double)vv[1], (double)o[1]);
   }
 };
 
@@ -521,19 +641,25 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
 
 
 // -------------------------------------------- diagonal-offset SpMV (k = 1)
-// The SELL-64/DIA image (kry_csr::dia_*): lane l of the wave owns row
-// 64 s + l of slice s; slot column j of the slice holds, for every lane whose
-// mask bit is set, the entry at column row + off_j. The slot column's
-// descriptor {off_j, mask_j} is wave-uniform (one scalar load), the values are
-// one contiguous 64-lane load, and the x values of a slot column are the
-// contiguous run x[64 s + off_j, 64 s + off_j + 64): no index stream at all.
+// The SELL-128/DIA image (kry_csr::dia_*): lane l of the wave owns rows
+// 128 s + 2l and 128 s + 2l + 1 of slice s; slot column j of the slice holds,
+// for every row whose mask bit is set, the entry at column row + off_j. The
+// slot column's offset and its two lane masks are wave-uniform (scalar
+// loads); per slot column a lane makes one 16-byte value load, one 16-byte x
+// load (x[row + off_j], x[row + 1 + off_j]: the wave reads the contiguous run
+// x[128 s + off_j, 128 s + off_j + 128)) and, at the end of the slice, one
+// 16-byte store: no index stream, and half the memory instructions of one
+// row per lane. A hole's x entry is loaded with its partner (at worst one
+// element past either end of x, inside the allocation slack) and its product
+// is dropped by a select, never added: an inf or NaN there cannot leak in.
 // The offsets of a slice ascend and every row is sorted, so each row is still
 // summed from 0 in stored order, one rounding per product and per add:
 // bitwise csr_matvec.
 template <typename V, typename MV, int UNR, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restrict__ sptr,
                                                           const int *__restrict__ swidth,
-                                                          const DiaCol *__restrict__ meta,
+                                                          const int *__restrict__ doff,
+                                                          const uint64_t *__restrict__ dmask,
                                                           const MV *__restrict__ val, int64_t nslices, int64_t n,
                                                           Src src, Epi epi, double *__restrict__ part,
                                                           const Ctrl *ctrl, int step) {
@@ -551,37 +677,60 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
   for (int64_t s = s_begin; s < s_end; ++s) {
     const int w = swidth[s];
     const int64_t base = sptr[s];
-    const int64_t row = s * 64 + lane;
-    const DiaCol *mc = meta + (base >> 6);  // wave-uniform: scalar loads
-    const MV *cv = val + base + lane;
-    V acc = V(0);
+    const int64_t row = s * kDiaSlice + 2 * lane;
+    const int64_t c0 = base / kDiaSlice;
+    const int *mo = doff + c0;  // wave-uniform: scalar loads
+    const uint64_t *mk = dmask + 2 * c0;
+    const MV *cv = val + base + 2 * lane;
+    V acc0 = V(0), acc1 = V(0);
     for (int j0 = 0; j0 < w; j0 += UNR) {
-      // descriptors: read unconditionally (the array is padded by kDiaPad
+      // descriptors: read unconditionally (the arrays are padded by kDiaPad
       // columns), all scalar loads in flight before the first use; values:
-      // behind the wave-uniform `in` (a scalar branch, no wait); gathers:
-      // unconditional, a hole's address clamped to x[0], its product dropped
-      // by a select (never added: an inf or NaN there cannot leak in)
-      DiaCol d[UNR];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) d[u] = mc[j0 + u];
-      V a[UNR];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) a[u] = j0 + u < w ? (V)__builtin_nontemporal_load(cv + (int64_t)(j0 + u) * 64) : V(0);
-      bool on[UNR];
-      V xv[UNR];
+      // behind the wave-uniform `j0 + u < w` (a scalar branch, no wait)
+      int off[UNR];
+      uint64_t me[UNR], md[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        on[u] = j0 + u < w && ((d[u].mask >> lane) & 1u) != 0;
-        xv[u] = bs(on[u] ? row + d[u].off : 0, 0);
+        off[u] = mo[j0 + u];
+        me[u] = mk[2 * (j0 + u)];
+        md[u] = mk[2 * (j0 + u) + 1];
+      }
+      MV a[UNR][2];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (j0 + u < w) {
+          pload_nt<MV>(cv + (int64_t)(j0 + u) * kDiaSlice, a[u]);
+        } else {
+          a[u][0] = MV(0);
+          a[u][1] = MV(0);
+        }
+      }
+      bool on0[UNR], on1[UNR];
+      V xv[UNR][2];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        on0[u] = j0 + u < w && ((me[u] >> lane) & 1u) != 0;
+        on1[u] = j0 + u < w && ((md[u] >> lane) & 1u) != 0;
+        bs.pair((on0[u] || on1[u]) ? row + off[u] : 0, xv[u]);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const V p = a[u] * xv[u];
-        const V t = acc + p;
-        acc = on[u] ? t : acc;
+        const V p0 = (V)a[u][0] * xv[u][0];
+        const V p1 = (V)a[u][1] * xv[u][1];
+        const V t0 = acc0 + p0;
+        const V t1 = acc1 + p1;
+        acc0 = on0[u] ? t0 : acc0;
+        acc1 = on1[u] ? t1 : acc1;
       }
     }
-    if (row < n) dacc += epi(row, 0, acc, bs(row, 0));
+    if (row + 1 < n) {
+      const V sv[2] = {acc0, acc1};
+      V xi[2];
+      bs.pair(row, xi);
+      dacc += epi.rows2(row, sv, xi);
+    } else if (row < n) {
+      dacc += epi(row, 0, acc0, bs(row, 0));
+    }
   }
   if (part != nullptr) {
     red[tid] = dacc;
@@ -1047,11 +1196,12 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   int grid;
   if constexpr (sizeof(I) == 4) {
     if (k == 1 && A->dia) {
-      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->nslices + 3) / 4));
+      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->dia_nslices + 3) / 4));
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->dia_sptr),
-                           static_cast<const int *>(A->dia_width), static_cast<const DiaCol *>(A->dia_meta),
-                           static_cast<const MV *>(A->dia_val), A->nslices, A->n, src, epi, part, ctrl, step);
+                           static_cast<const int *>(A->dia_width), static_cast<const int *>(A->dia_off),
+                           static_cast<const uint64_t *>(A->dia_mask), static_cast<const MV *>(A->dia_val),
+                           A->dia_nslices, A->n, src, epi, part, ctrl, step);
       };
       if (A->dia_max_width <= 8) go(spmv_dia_kernel<V, MV, 8, Src, Epi>);
       else go(spmv_dia_kernel<V, MV, 16, Src, Epi>);

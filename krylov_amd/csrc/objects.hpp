@@ -56,22 +56,27 @@ struct kry_csr {
   void *cb_col = nullptr;   // int32, nnz (+ pad)
   void *cb_val = nullptr;   // dtype, nnz (+ pad)
   void *cb_y = nullptr;     // double, n: running row sums between passes
-  // diagonal-offset image (SELL-64/DIA, structured matrices, k = 1): in
-  // every slice the columns of each row are row + o_j for a short sorted list
-  // of offsets o_j shared by the slice, so slot column j holds the entry at
-  // offset o_j of every lane (or a masked-off hole). Per slot column one
-  // 16-byte descriptor {int32 offset, pad, uint64 lane mask} replaces the 64
-  // per-lane indices: the matrix stream is the values alone, and the x
-  // gathers of a slot column are one contiguous 64-element run. Built only
-  // for int32 inputs whose every row is strictly sorted, and only when the
-  // slot count stays within 1.25x of the SELL image's.
+  // diagonal-offset image (SELL-128/DIA, structured matrices, k = 1): in
+  // every slice of 128 rows the columns of each row are row + o_j for a short
+  // sorted list of offsets o_j shared by the slice, so slot column j holds the
+  // entry at offset o_j of every row (or a masked-off hole). Lane l of the
+  // wave owns rows 2l and 2l + 1: per slot column its two values, its two x
+  // entries x[row + o_j], x[row + 1 + o_j] and (at the end) its two results
+  // are each one 16-byte access (8 bytes for float). Per slot column one
+  // int32 offset and two uint64 lane masks (even rows, odd rows), read with
+  // scalar loads, replace the 128 per-row indices: the matrix stream is the
+  // values alone. Built only for int32 inputs whose every row is strictly
+  // sorted, and only when the slot count stays within 1.25x of the SELL
+  // image's.
   bool dia = false;
+  int64_t dia_nslices = 0;
   int64_t dia_nslots = 0;
   int dia_max_width = 0;
-  void *dia_sptr = nullptr;   // int64, nslices + 1
-  void *dia_width = nullptr;  // int32, nslices
-  void *dia_meta = nullptr;   // DiaCol, dia_nslots / 64 (+ pad)
-  void *dia_val = nullptr;    // dtype, dia_nslots (+ pad); holes are 0
+  void *dia_sptr = nullptr;   // int64, dia_nslices + 1 (slots; kDiaSlice per slot column)
+  void *dia_width = nullptr;  // int32, dia_nslices
+  void *dia_off = nullptr;    // int32, dia_nslots / kDiaSlice (+ kDiaPad)
+  void *dia_mask = nullptr;   // uint64 x 2 per slot column: bit l of word q = row 2l + q present
+  void *dia_val = nullptr;    // dtype, dia_nslots (+ pad), row order within a slot column; holes are 0
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;

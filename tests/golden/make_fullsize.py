@@ -1,0 +1,114 @@
+"""Full-size golden histories: the REFERENCE solvers run here on the BASELINE
+configurations themselves (SURVEY.md §8(d) / App. A generators).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_fullsize.py
+
+The reference is imported read-only exactly as in make_golden.py (NumPy-2
+names re-added on the numpy module object). Only inputs' descriptions and
+outputs are stored: the residual-norm history, numsteps, success, and for the
+solution a few size-independent summaries (sum|x|, ||x||_2, max|x|, the
+reference's own golden statistics of tests/test_solvers.py:126-128) plus the
+entries at 4096 fixed sample positions. ~6 minutes on 8 cores, ~12 GB RSS.
+
+Output: tests/golden/fullsize.npz. The matrices are pinned by
+tests/golden/problems.json (SHA-256 of the generated CSR arrays).
+"""
+import contextlib
+import io
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from krylov_amd import problems  # noqa: E402
+from make_golden import _import_reference  # noqa: E402
+
+NSAMPLE = 4096
+
+
+def sample_idx(n):
+    return np.sort(np.random.default_rng(12345).choice(n, NSAMPLE, replace=False))
+
+
+def _store(prefix, sol, info, out):
+    x = np.asarray(info.xk)
+    out[f"{prefix}_success"] = np.array(info.success)
+    out[f"{prefix}_numsteps"] = np.array(info.numsteps)
+    out[f"{prefix}_resnorms"] = np.asarray(info.resnorms, dtype=np.float64)
+    xa = np.abs(x.astype(np.float64))
+    out[f"{prefix}_xstats"] = np.array([xa.sum(axis=0), np.sqrt((xa * xa).sum(axis=0)), xa.max(axis=0)])
+    out[f"{prefix}_xsample"] = x[sample_idx(x.shape[0])]
+
+
+def main():
+    krylov = _import_reference()
+    quiet = contextlib.redirect_stdout(io.StringIO())  # gmres.py:201-205 prints every iteration
+    out = {"nsample": np.array(NSAMPLE)}
+    only = sys.argv[1:]
+
+    def want(name):
+        return not only or name in only
+
+    if want("metric_cg") or want("metric_gmres30"):
+        A = problems.stencil15_3d(216)
+        b = np.ones(A.shape[0])
+        if want("metric_cg"):
+            t = time.time()
+            sol, info = krylov.cg(A, b, tol=1e-8)  # BASELINE metric, to convergence (363 steps)
+            _store("metric_cg", sol, info, out)
+            print("metric_cg", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        if want("metric_gmres30"):
+            t = time.time()
+            with quiet:
+                sol, info = krylov.gmres(A, b, maxiter=30, tol=0.0)  # north_star: GMRES(30) on the same matrix
+            _store("metric_gmres30", sol, info, out)
+            print("metric_gmres30", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        del A
+    if want("cfg2_cg"):
+        P = problems.poisson2d(1000)
+        t = time.time()
+        sol, info = krylov.cg(P, np.ones(P.shape[0]), tol=1e-8)
+        _store("cfg2_cg", sol, info, out)
+        print("cfg2_cg", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        del P
+    if want("cfg3_gmres30"):
+        R = problems.random_nonsym(2_000_000)
+        t = time.time()
+        with quiet:
+            sol, info = krylov.gmres(R, np.ones(R.shape[0]), maxiter=30, tol=0.0)
+        _store("cfg3_gmres30", sol, info, out)
+        print("cfg3_gmres30", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        del R
+    if want("cfg4_blockcg"):
+        P = problems.poisson2d(3163)
+        B = np.random.default_rng(0).standard_normal((P.shape[0], 8))
+        t = time.time()
+        sol, info = krylov.cg(P, B, tol=0.0, maxiter=40)
+        _store("cfg4_blockcg", sol, info, out)
+        print("cfg4_blockcg", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        del P, B
+    if want("cfg5_minres"):
+        W, w = problems.shifted_lap3d_weighted(200)
+        bW = np.ones(W.shape[0], dtype=np.float32)
+
+        def inner(x, y):  # tests/test_solvers.py:157-161 form
+            return np.dot(x.T, w * y)
+
+        t = time.time()
+        with quiet:
+            sol, info = krylov.minres(W, bW, inner=inner, tol=0.0, maxiter=100)
+        _store("cfg5_minres", sol, info, out)
+        print("cfg5_minres", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+    path = os.path.join(HERE, "fullsize.npz" if not only else "fullsize_part.npz")
+    np.savez_compressed(path, **out)
+    print("written", path)
+
+
+if __name__ == "__main__":
+    main()

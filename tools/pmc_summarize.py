@@ -56,7 +56,7 @@ def main(out):
     fetch, name = find(bf, "spmv_dia_kernel", "EpiApDot")
     write, _ = find(bw, "spmv_dia_kernel", "EpiApDot")
     alg = bench.spmv_S(n, nnz)
-    phys = 8.0 * slots + 16.0 * slots / 64 + 2.0 * n * 8
+    phys = 8.0 * slots + 20.0 * slots / 128 + 2.0 * n * 8  # values, per-column offset + 2 masks, x and Ap
     res = {
         "kernel": name,
         "fetch_raw_bytes": fetch,
