@@ -167,3 +167,17 @@ def test_oracle_preconditioned(case):
     solver, A, b, kw = solver_cases.build(case)
     sol, info = getattr(K, solver)(A, b, **kw)
     _check(case[0], sol, info, d)
+
+
+def test_oracle_fullsize_cfg3_gmres30():
+    """The oracle at a BASELINE size against the reference's own full-size
+    history (tests/golden/fullsize.npz, cfg3: random nonsymmetric n = 2e6,
+    GMRES(30)): the restatement is pinned at scale, not only on small cases."""
+    F = np.load(os.path.join(os.path.dirname(__file__), "golden", "fullsize.npz"))
+    R = problems.random_nonsym(2_000_000)
+    _, info = K.gmres(R, np.ones(R.shape[0]), maxiter=30, tol=0.0)
+    assert info.numsteps == int(F["cfg3_gmres30_numsteps"])
+    np.testing.assert_allclose(np.asarray(info.resnorms, dtype=np.float64), F["cfg3_gmres30_resnorms"],
+                               rtol=1e-12, atol=0)
+    idx = np.sort(np.random.default_rng(12345).choice(R.shape[0], int(F["nsample"]), replace=False))
+    np.testing.assert_allclose(info.xk[idx], F["cfg3_gmres30_xsample"], rtol=1e-12, atol=0)
