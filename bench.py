@@ -177,13 +177,16 @@ def run_cg_config(A_host, B, steps, warmup=5):
             "persistent_loop": chunk == 256}
 
 
-def run_gmres():
+def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"):
+    """GMRES(30) iterations/s, one 30-step cycle (tol = 0) incl. the final
+    x = x0 + V y; median of 3 after one warm-up cycle. Default matrix: cfg3."""
     import krylov_amd
     from krylov_amd import _helpers, problems
     from krylov_amd.device import get_context
     from krylov_amd.gmres import _GmresState
 
-    R = problems.random_nonsym(2_000_000)
+    if R is None:
+        R = problems.random_nonsym(2_000_000)
     A = krylov_amd.CsrOperator(R)
     prob = _helpers.Problem(A, np.ones(R.shape[0]), None, None)
     ctx = get_context()
@@ -203,7 +206,7 @@ def run_gmres():
             times.append(t1 - t0)
     t = float(np.median(times))
     return {"it_per_s": 30.0 / t, "cycle_ms": 1e3 * t, "gbs": gmres_cycle_bytes(R.shape[0], R.nnz) / t / 1e9,
-            "n": R.shape[0], "nnz": int(R.nnz), "config": "cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"}
+            "n": R.shape[0], "nnz": int(R.nnz), "config": label}
 
 
 def run_minres_cfg5(steps=100):
@@ -306,6 +309,10 @@ def main():
     spmv_bytes = spmv_S(n, nnz)
     achieved = spmv_bytes / spmv_avg_s / 1e9
     kname, image_note = spmv_kernel_desc(res["layout"])
+    image_bytes = None
+    if res["layout"]["dia"]:  # the bytes the DIA image moves per launch (next to the algorithmic S)
+        ds = res["layout"]["dia_slots"]
+        image_bytes = ds * 8 + ds / 128 * 20 + 2 * n * 8
     traffic = pmc_traffic(n, nnz, kname)
     out = {
         "metric": "CG iters/sec + SpMV GB/s (fp64, n=10M, nnz=150M); GMRES(30) iters/sec",
@@ -344,12 +351,17 @@ def main():
             "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; "
                              + image_note + ")",
             "launches_timed": res["spmv_count"],
+            "image_bytes_per_launch": image_bytes,
+            "image_gbs": image_bytes / spmv_avg_s / 1e9 if image_bytes else None,
+            "image_frac": image_bytes / spmv_avg_s / 1e9 / HBM_PEAK_GBS if image_bytes else None,
         },
     }
     if world == 1 and not args.quick:
         g = run_gmres()
         out["gmres30_it_per_s"] = g["it_per_s"]
         out["gmres"] = g
+        # north_star: GMRES(30) on the same (metric) matrix
+        out["gmres_metric"] = run_gmres(A_host, f"metric 15-point {args.m}^3, GMRES(30) mgs, one cycle")
     if world == 1 and args.configs:
         extra = {}
         extra["cfg2_cg_poisson1000"] = run_cg_config(problems.poisson2d(1000), np.ones(1_000_000), 200, 10)

@@ -1,5 +1,5 @@
 """One secondary BASELINE config on its own, for a kernel trace:
-`python tools/cfg_time.py cfg4|cfg5|cfg2 [steps]` (run under
+`python tools/cfg_time.py cfg4|cfg5|cfg2|gmres_cfg3 [steps]` or `gmres_metric [m]` (run under
 `rocprofv3 --kernel-trace --stats` to split an iteration by kernel)."""
 import os
 import sys
@@ -20,3 +20,8 @@ elif cfg == "cfg2":
     print(cfg, bench.run_cg_config(problems.poisson2d(1000), np.ones(1_000_000), steps, 10), flush=True)
 elif cfg == "cfg5":
     print(cfg, bench.run_minres_cfg5(steps), flush=True)
+elif cfg == "gmres_metric":
+    m = steps if len(sys.argv) > 2 else 216
+    print(cfg, bench.run_gmres(problems.stencil15_3d(m), f"metric {m}^3 GMRES(30)"), flush=True)
+elif cfg == "gmres_cfg3":
+    print(cfg, bench.run_gmres(), flush=True)

@@ -36,9 +36,10 @@ def find(d, *parts):
 def dia_slots(out):
     """dia_slots as printed by tools/dia_bench's first line."""
     with open(os.path.join(out, "micro_FETCH_SIZE.log")) as f:
-        for tok in f.readline().split():
-            if tok.startswith("dia_slots="):
-                return int(tok.split("=")[1])
+        for line in f:
+            for tok in line.split():
+                if tok.startswith("dia_slots="):
+                    return int(tok.split("=")[1])
     raise SystemExit("dia_bench header not found")
 
 
@@ -62,7 +63,7 @@ def main(out):
         "fetch_raw_bytes": fetch,
         "write_bytes": write,
         "read_scale_from_calibration": scale,
-        "calibration": "dia_probe<16,4> (tools/dia_bench 'values only'): the diagonal-offset image's 8 B/lane "
+        "calibration": "dia_probe<16,4> (tools/dia_bench 'values only'): the diagonal-offset image's 16 B/lane (two rows' values) "
                        "nontemporal value stream, 8 B x dia_slots known bytes, FETCH_SIZE x 1024 measured",
         "traffic_bytes_per_launch": fetch * scale + write,
         "algorithmic_bytes_per_launch": alg,
