@@ -66,6 +66,7 @@ struct kry_gmres {
   double *gcrit = nullptr;  // total_k
   int col_offset = 0, total_k = 0;
   int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
+  bool mgsp_large = false;  // gm_mgsl_kernel (basis streamed) rather than gm_mgsp_kernel
   int mgsp_grid = 0;
   int mgsp_fallbacks = 0;  // chunks finished launch per pass after a persistent MGS timeout
   double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
@@ -407,6 +408,212 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
     // prefetch the vector after next only now: the drain in mgs_arrive must
     // not wait for it (vmcnt is in order); it travels during the wait
     if (const V *q2 = next_of(p + 1)) ld(q2, vn);
+    if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
+    reduce_rows<kMgsBlock, true>(slot, G, k, red);
+    if (tid < k) alpha[tid] = red[tid];
+    __syncthreads();
+  }
+}
+
+// ------------------------------- persistent MGS for large n (one launch)
+// As gm_mgsp_kernel (same passes, exchange, abort and partial buffers), for
+// n·k up to 512 · NV · W per block and one block per CU (n = 10 M doubles at
+// NV = 40): only w stays in registers (NV granules of W elements per thread,
+// 160 VGPRs at NV = 40); the pass's two basis vectors are streamed in chunks
+// of U granules, chunk c + 1 loaded while chunk c is used, and chunk 0 of the
+// next pass loaded before the exchange so it travels during the wait. A pass
+// therefore reads V_j (the subtrahend) and V_{j+1} (the next inner product's
+// partner) once each; V_{j+1} is read again as the next pass's subtrahend,
+// with default-policy loads that leave it in the 256 MB MALL between the two
+// uses. The launch-per-pass kernel moves w in and out as well: 4 vectors per
+// pass against 2.
+// Memory access: buffer loads/stores over the block's segment of each vector
+// (descriptor from wave-uniform values; per-lane byte offset tid * 16, the
+// granule's offset u * 8192 as a scalar), so no per-granule address
+// registers; the descriptor's record count ends at N, so the tail's
+// out-of-range granules read as 0 (they add 0 to the partials and stay 0 in
+// w) and their stores are dropped.
+typedef unsigned int mgsl_u4 __attribute__((ext_vector_type(4)));
+template <typename V>
+struct MgslSeg {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ MgslSeg(const V *vec, int64_t e0, int64_t N, int64_t seg) {
+    const int64_t rem = N - e0;
+    const int64_t cnt = rem < seg ? (rem > 0 ? rem : 0) : seg;
+    // wave-uniform by construction; readfirstlane makes it provable, so the
+    // buffer ops take the descriptor from SGPRs without a waterfall loop
+    const uint64_t a = reinterpret_cast<uint64_t>(vec + e0);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(cnt * (int64_t)sizeof(V)));
+    r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  }
+  template <int W>
+  __device__ __forceinline__ void load(int u, V (&o)[W]) const {
+    const mgsl_u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, u * kMgsBlock * 16, 0);
+    if constexpr (W == 2) {
+      const double2 d = __builtin_bit_cast(double2, t);
+      o[0] = d.x;
+      o[1] = d.y;
+    } else {
+      const float4 f = __builtin_bit_cast(float4, t);
+      o[0] = f.x;
+      o[1] = f.y;
+      o[2] = f.z;
+      o[3] = f.w;
+    }
+  }
+  template <int W>
+  __device__ __forceinline__ void store(int u, const V (&o)[W]) const {
+    mgsl_u4 t;
+    if constexpr (W == 2) t = __builtin_bit_cast(mgsl_u4, double2{o[0], o[1]});
+    else t = __builtin_bit_cast(mgsl_u4, float4{o[0], o[1], o[2], o[3]});
+    __builtin_amdgcn_raw_buffer_store_b128(t, r, (int)threadIdx.x * 16, u * kMgsBlock * 16, 0);
+  }
+};
+
+template <typename V, int NV, int U>
+__global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V *__restrict__ w,
+                                                            const V *__restrict__ Vb, size_t stride, int col,
+                                                            int sweeps, const double *__restrict__ part0, int P0,
+                                                            double *__restrict__ pbuf, double *__restrict__ h,
+                                                            unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
+                                                            int step, int fault_step) {
+  static_assert(NV % U == 0, "chunks must tile the thread's granules");
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int NC = NV / U;
+  __shared__ double red[kMgsBlock * W];
+  __shared__ double alpha[kMaxCols];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_MGS_FAULT)
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  auto abort_step = [&]() {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+  };
+  const int64_t seg = (int64_t)NV * kMgsBlock * W;  // elements of the block's segment
+  const int64_t e0 = (int64_t)blockIdx.x * seg;
+  // element v of every granule of this thread belongs to column (tid W + v) & (k - 1)
+  // (the segment and granule strides are multiples of 1024 >= k)
+  int colv[W];
+#pragma unroll
+  for (int v = 0; v < W; ++v) colv[v] = (tid * W + v) & (k - 1);
+  const MgslSeg<V> ws(w, e0, N, seg);
+  V wr[NV][W];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) ws.template load<W>(u, wr[u]);
+  const int np = sweeps * (col + 1);
+  auto sub_of = [&](int p) -> const V * { return Vb + stride * (size_t)(p % (col + 1)); };  // V_j of pass p
+  auto next_of = [&](int p) -> const V * {  // the vector of pass p's inner product (null = w)
+    const int j = p % (col + 1), sw = p / (col + 1);
+    if (j < col) return Vb + stride * (size_t)(j + 1);
+    if (sw + 1 < sweeps) return Vb;
+    return nullptr;
+  };
+  // chunk buffers: [parity][granule of the chunk][element]
+  V cs[2][U][W], cn[2][U][W];
+  auto ld_chunk = [&](const MgslSeg<V> &sg, int c, V(&dst)[U][W]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) sg.template load<W>(c * U + u, dst[u]);
+  };
+  {
+    const MgslSeg<V> s0(sub_of(0), e0, N, seg);
+    ld_chunk(s0, 0, cs[0]);
+    const V *q = next_of(0);
+    ld_chunk(MgslSeg<V>(q ? q : Vb, e0, N, seg), 0, cn[0]);
+  }
+  reduce_rows<kMgsBlock, false>(part0, P0, k, red);  // alpha_0 = <V_0, w> from the SpMV's partials
+  if (tid < k) alpha[tid] = red[tid];
+  __syncthreads();
+  for (int p = 0; p < np; ++p) {
+    const int j = p % (col + 1);
+    const bool first_sweep = p <= col;
+    if (blockIdx.x == 0 && tid < k) {  // h[j] += alpha_j (arnoldi.py:160-161)
+      const V a = (V)alpha[tid];
+      const V prev = first_sweep ? V(0) : (V)h[(int64_t)j * k + tid];
+      h[(int64_t)j * k + tid] = (double)(prev + a);
+    }
+    const MgslSeg<V> sv(sub_of(p), e0, N, seg);
+    const V *qp = next_of(p);
+    const MgslSeg<V> sq(qp ? qp : Vb, e0, N, seg);
+    V al[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) al[v] = (V)alpha[colv[v]];
+    double acc[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc[v] = 0.0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int b = c & 1;
+      // keeps the scheduler from hoisting later chunks' loads (their buffers
+      // would be live all at once: spills)
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < NC) {  // the next chunk travels while this one is used
+        // (the partner is loaded even when the pass pairs w with itself: no
+        // branch, so the chunks stay in one block for the scheduler)
+        ld_chunk(sv, c + 1, cs[b ^ 1]);
+        ld_chunk(sq, c + 1, cn[b ^ 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int g = c * U + u;
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+          const V t = al[v] * cs[b][u][v];
+          wr[g][v] = wr[g][v] - t;  // Av -= alpha * V[j] (arnoldi.py:162)
+          const double a = qp ? (double)cn[b][u][v] : (double)wr[g][v];
+          acc[v] += dterm(a, (double)wr[g][v]);  // out-of-range elements are 0: they add 0
+        }
+      }
+    }
+    double part1 = 0.0;  // k == 1: the block partial, in thread 0
+    if (k == 1) {
+      double t = acc[0];
+#pragma unroll
+      for (int v = 1; v < W; ++v) t += acc[v];
+      part1 = block_sum1_t0(t, red + kMgsBlock);
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < W; ++v) red[tid * W + v] = acc[v];
+      block_tree_reduce(red, kMgsBlock * W, k);
+    }
+    double *slot = pbuf + (size_t)(p < np - 1 ? (p & 1) : 2) * G * k;
+    if (p == np - 1) {  // <w, w> partials for the QR kernel; w back to HBM
+      if (k == 1) {
+        if (tid == 0) slot[blockIdx.x] = part1;
+      } else if (tid < k) {
+        slot[(int64_t)blockIdx.x * k + tid] = red[tid];
+      }
+#pragma unroll
+      for (int u = 0; u < NV; ++u) ws.template store<W>(u, wr[u]);
+      return;
+    }
+    // chunk 0 of the next pass: its loads must not be waited on by the
+    // exchange's drains (vmcnt is in order), so they are issued after the
+    // publish / arrive and travel during the wait
+    const MgslSeg<V> sv2(sub_of(p + 1), e0, N, seg);
+    const V *q2 = next_of(p + 1);
+    if (k == 1) {  // granule all-gather of the block partials
+      unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
+      const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
+      if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
+      ld_chunk(sv2, 0, cs[0]);
+      ld_chunk(MgslSeg<V>(q2 ? q2 : Vb, e0, N, seg), 0, cn[0]);
+      if (tid < 64) {
+        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
+        if (tid == 0) flag = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!__builtin_amdgcn_readfirstlane(flag)) return abort_step();
+      continue;
+    }
+    if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
+    mgs_arrive(bar, (unsigned)(p + 1));
+    ld_chunk(sv2, 0, cs[0]);
+    ld_chunk(MgslSeg<V>(q2 ? q2 : Vb, e0, N, seg), 0, cn[0]);
     if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
     reduce_rows<kMgsBlock, true>(slot, G, k, red);
     if (tid < k) alpha[tid] = red[tid];
@@ -989,11 +1196,21 @@ void hh_run_impl(kry_gmres *s, int max_steps) {
 // Launch the persistent MGS kernel for this Arnoldi step if w fits the
 // registers of one resident 512-thread block per CU; false = not eligible
 // (decided once per solver: s->mgsp_E = 0 no, else elements per thread).
+// Up to 16 doubles per thread w and the two basis vectors stay in registers
+// (gm_mgsp_kernel); up to 80 only w does and the basis is streamed
+// (gm_mgsl_kernel, n = 10 M at one column).
+// granules per streamed chunk: 4 (2 from NV = 32 on, where 4 would spill)
+template <int NV>
+constexpr int mgsl_u() {
+  return NV >= 32 ? 2 : 4;
+}
 template <typename V>
 bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int step) {
   const int64_t N = s->n * (int64_t)s->k;
+  constexpr int W = Vec16<V>::W;
   if (s->mgsp_E < 0) {
     s->mgsp_E = 0;
+    s->mgsp_large = false;
     const char *e = getenv("KRY_MGS_PERSIST");
     if (!(e && atoi(e) == 0)) {
       int dev = 0, ncu = 0;
@@ -1011,6 +1228,15 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       if (fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
       else if (fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
       else if (sizeof(V) == 4 && fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
+      else if (!(e && atoi(e) == 1)) {  // KRY_MGS_PERSIST=1: the register-resident kernel only
+        s->mgsp_large = true;
+        if (fits(gm_mgsl_kernel<V, 12, mgsl_u<12>()>, 12 * W)) s->mgsp_E = 12 * W;
+        else if (fits(gm_mgsl_kernel<V, 16, mgsl_u<16>()>, 16 * W)) s->mgsp_E = 16 * W;
+        else if (fits(gm_mgsl_kernel<V, 24, mgsl_u<24>()>, 24 * W)) s->mgsp_E = 24 * W;
+        else if (fits(gm_mgsl_kernel<V, 32, mgsl_u<32>()>, 32 * W)) s->mgsp_E = 32 * W;
+        else if (fits(gm_mgsl_kernel<V, 40, mgsl_u<40>()>, 40 * W)) s->mgsp_E = 40 * W;
+        else s->mgsp_large = false;
+      }
     }
   }
   if (s->mgsp_E == 0) return false;
@@ -1028,9 +1254,21 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
                        pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step);
   };
-  if (E == 8) go(gm_mgsp_kernel<V, 8>);
-  else if (E == 16) go(gm_mgsp_kernel<V, 16>);
-  else if constexpr (sizeof(V) == 4) go(gm_mgsp_kernel<V, 32>);
+  if (s->mgsp_large) {
+    switch (E / W) {
+      case 12: go(gm_mgsl_kernel<V, 12, mgsl_u<12>()>); break;
+      case 16: go(gm_mgsl_kernel<V, 16, mgsl_u<16>()>); break;
+      case 24: go(gm_mgsl_kernel<V, 24, mgsl_u<24>()>); break;
+      case 32: go(gm_mgsl_kernel<V, 32, mgsl_u<32>()>); break;
+      default: go(gm_mgsl_kernel<V, 40, mgsl_u<40>()>); break;
+    }
+  } else if (E == 8) {
+    go(gm_mgsp_kernel<V, 8>);
+  } else if (E == 16) {
+    go(gm_mgsp_kernel<V, 16>);
+  } else if constexpr (sizeof(V) == 4) {
+    go(gm_mgsp_kernel<V, 32>);
+  }
   KRY_HIP(hipGetLastError());
   s->mgsp_grid = G;
   s->mgsp_out = pbuf + (size_t)2 * G * s->k;
