@@ -67,6 +67,7 @@ struct kry_gmres {
   int col_offset = 0, total_k = 0;
   int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
   bool mgsp_large = false;  // gm_mgsl_kernel (basis streamed) rather than gm_mgsp_kernel
+  bool mgsp_norm = false;   // the last launch also wrote V_{k+1} (no w / hsafe pending)
   int mgsp_grid = 0;
   int mgsp_fallbacks = 0;  // chunks finished launch per pass after a persistent MGS timeout
   double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
                                                             int sweeps, const double *__restrict__ part0, int P0,
                                                             double *__restrict__ pbuf, double *__restrict__ h,
                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
-                                                            int step, int fault_step) {
+                                                            int step, int fault_step, V *__restrict__ vnext) {
   static_assert(NV % U == 0, "chunks must tile the thread's granules");
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
@@ -581,7 +582,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       block_tree_reduce(red, kMgsBlock * W, k);
     }
     double *slot = pbuf + (size_t)(p < np - 1 ? (p & 1) : 2) * G * k;
-    if (p == np - 1) {  // <w, w> partials for the QR kernel; w back to HBM
+    if (p == np - 1 && vnext == nullptr) {  // <w, w> partials for the QR kernel; w back to HBM
       if (k == 1) {
         if (tid == 0) slot[blockIdx.x] = part1;
       } else if (tid < k) {
@@ -589,6 +590,47 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       }
 #pragma unroll
       for (int u = 0; u < NV; ++u) ws.template store<W>(u, wr[u]);
+      return;
+    }
+    if (p == np - 1) {
+      // one more exchange: every block gets <w, w>, forms h[k+1] =
+      // sqrt(<w, w>) and its guard exactly as the QR kernel does (same
+      // value, same operations) and writes the next basis vector
+      // V_{k+1} = w / guard(h[k+1]) (arnoldi.py:185,191-196) straight from
+      // its registers; w itself is not written back. The QR kernel reads
+      // the exchanged sum as a single partial row (slot 2, row 0).
+      double *tot = pbuf + (size_t)2 * G * k;
+      if (k == 1) {
+        unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
+        const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
+        if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
+        if (tid < 64) {
+          const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
+          if (tid == 0) flag = ok ? 1 : 0;
+        }
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(flag)) return abort_step();
+      } else {
+        double *xs = pbuf + (size_t)(p & 1) * G * k;
+        if (tid < k) st_agent(xs + (int64_t)blockIdx.x * k + tid, red[tid]);
+        mgs_arrive(bar, (unsigned)(p + 1));
+        if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
+        reduce_rows<kMgsBlock, true>(xs, G, k, red);
+        if (tid < k) alpha[tid] = red[tid];
+        __syncthreads();
+      }
+      if (blockIdx.x == 0 && tid < k) tot[tid] = alpha[tid];
+      V hs[W];
+#pragma unroll
+      for (int v = 0; v < W; ++v) hs[v] = safe<V>(sqrt((V)alpha[colv[v]]));
+      const MgslSeg<V> vs(vnext, e0, N, seg);
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        V o[W];
+#pragma unroll
+        for (int v = 0; v < W; ++v) o[v] = wr[u][v] / hs[v];
+        vs.template store<W>(u, o);
+      }
       return;
     }
     // chunk 0 of the next pass: its loads must not be waited on by the
@@ -1254,13 +1296,20 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
                        pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step);
   };
+  // the streamed kernel also normalises: V_{col+1} = w / guard(h[col+1])
+  V *vnext = basis<V>(s->V, s->vstride, col + 1);
+  auto gol = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
+                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step, vnext);
+  };
+  s->mgsp_norm = s->mgsp_large;
   if (s->mgsp_large) {
     switch (E / W) {
-      case 12: go(gm_mgsl_kernel<V, 12, mgsl_u<12>()>); break;
-      case 16: go(gm_mgsl_kernel<V, 16, mgsl_u<16>()>); break;
-      case 24: go(gm_mgsl_kernel<V, 24, mgsl_u<24>()>); break;
-      case 32: go(gm_mgsl_kernel<V, 32, mgsl_u<32>()>); break;
-      default: go(gm_mgsl_kernel<V, 40, mgsl_u<40>()>); break;
+      case 12: gol(gm_mgsl_kernel<V, 12, mgsl_u<12>()>); break;
+      case 16: gol(gm_mgsl_kernel<V, 16, mgsl_u<16>()>); break;
+      case 24: gol(gm_mgsl_kernel<V, 24, mgsl_u<24>()>); break;
+      case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>()>); break;
+      default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>()>); break;
     }
   } else if (E == 8) {
     go(gm_mgsp_kernel<V, 8>);
@@ -1270,7 +1319,7 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
     go(gm_mgsp_kernel<V, 32>);
   }
   KRY_HIP(hipGetLastError());
-  s->mgsp_grid = G;
+  s->mgsp_grid = s->mgsp_norm ? 1 : G;  // normalising: the exchanged sum, one row
   s->mgsp_out = pbuf + (size_t)2 * G * s->k;
   return true;
 }
@@ -1326,6 +1375,7 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
     if (fuse_norm && !s->w && mgsp_launch<V>(s, w, s->part, P, col, step)) {
       // the QR kernel reads the persistent kernel's <w, w> partials
       gm_qr_step<V>(s, s->mgsp_out, s->mgsp_grid, col, step);
+      if (s->mgsp_norm) continue;  // V_{col+1} is in the basis already
       if (col + 1 < s->maxiter) {
         s->vpending = true;  // V_{col+1} is formed by the next step's SpMV
         continue;
