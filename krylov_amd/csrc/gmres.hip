@@ -449,9 +449,9 @@ struct MgslSeg {
     const int bytes = __builtin_amdgcn_readfirstlane((int)(cnt * (int64_t)sizeof(V)));
     r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
   }
-  template <int W>
+  template <int W, int AUX = 0>
   __device__ __forceinline__ void load(int u, V (&o)[W]) const {
-    const mgsl_u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, u * kMgsBlock * 16, 0);
+    const mgsl_u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, u * kMgsBlock * 16, AUX);
     if constexpr (W == 2) {
       const double2 d = __builtin_bit_cast(double2, t);
       o[0] = d.x;
@@ -473,7 +473,7 @@ struct MgslSeg {
   }
 };
 
-template <typename V, int NV, int U>
+template <typename V, int NV, int U, bool NT>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V *__restrict__ w,
                                                             const V *__restrict__ Vb, size_t stride, int col,
                                                             int sweeps, const double *__restrict__ part0, int P0,
@@ -484,6 +484,15 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int NC = NV / U;
+  // The partner V_{j+1} of pass j is the subtrahend of pass j + 1. Its first
+  // KU granule rows (KC chunks) are kept in LDS from one pass to the next, as
+  // per-thread storage (each thread reads back only what it wrote: no
+  // barrier), so a pass reads them from HBM once, not twice. The rest of the
+  // 160 KiB holds the reduction scratch.
+  constexpr int KEEP = W == 2 ? 18 : 16;
+  constexpr int KU = (NV < KEEP ? NV : KEEP) / U * U;
+  constexpr int KC = KU / U;
+  __shared__ __attribute__((aligned(16))) V keep[KU > 0 ? KU : 1][kMgsBlock * W];
   __shared__ double red[kMgsBlock * W];
   __shared__ double alpha[kMaxCols];
   __shared__ int flag;
@@ -519,9 +528,34 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
 #pragma unroll
     for (int u = 0; u < U; ++u) sg.template load<W>(c * U + u, dst[u]);
   };
+  // the subtrahend V_j is read for the last time in this step: nontemporal
+  // (NT), so the MALL keeps V_{j+1} for its second read in the next pass
+  auto ld_chunk_sub = [&](const MgslSeg<V> &sg, int c, V(&dst)[U][W]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) sg.template load<W, NT ? 2 : 0>(c * U + u, dst[u]);
+  };
+  auto keep_ld = [&](int g, V(&o)[W]) {
+    typedef V vec_t __attribute__((ext_vector_type(W)));
+    const vec_t t = *reinterpret_cast<const vec_t *>(&keep[g][tid * W]);
+#pragma unroll
+    for (int v = 0; v < W; ++v) o[v] = t[v];
+  };
+  auto keep_st = [&](int g, const V(&o)[W]) {
+    typedef V vec_t __attribute__((ext_vector_type(W)));
+    vec_t t;
+#pragma unroll
+    for (int v = 0; v < W; ++v) t[v] = o[v];
+    *reinterpret_cast<vec_t *>(&keep[g][tid * W]) = t;
+  };
   {
     const MgslSeg<V> s0(sub_of(0), e0, N, seg);
-    ld_chunk(s0, 0, cs[0]);
+#pragma unroll
+    for (int g = 0; g < KU; ++g) {  // V_0's kept rows
+      V t[W];
+      s0.template load<W>(g, t);
+      keep_st(g, t);
+    }
+    if (KC == 0) ld_chunk_sub(s0, 0, cs[0]);
     const V *q = next_of(0);
     ld_chunk(MgslSeg<V>(q ? q : Vb, e0, N, seg), 0, cn[0]);
   }
@@ -554,15 +588,23 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       if (c + 1 < NC) {  // the next chunk travels while this one is used
         // (the partner is loaded even when the pass pairs w with itself: no
         // branch, so the chunks stay in one block for the scheduler)
-        ld_chunk(sv, c + 1, cs[b ^ 1]);
+        if (c + 1 >= KC) ld_chunk_sub(sv, c + 1, cs[b ^ 1]);
         ld_chunk(sq, c + 1, cn[b ^ 1]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int g = c * U + u;
+        V sub[W];
+        if (c < KC) {
+          keep_ld(g, sub);
+          keep_st(g, cn[b][u]);  // the next pass's subtrahend
+        } else {
+#pragma unroll
+          for (int v = 0; v < W; ++v) sub[v] = cs[b][u][v];
+        }
 #pragma unroll
         for (int v = 0; v < W; ++v) {
-          const V t = al[v] * cs[b][u][v];
+          const V t = al[v] * sub[v];
           wr[g][v] = wr[g][v] - t;  // Av -= alpha * V[j] (arnoldi.py:162)
           const double a = qp ? (double)cn[b][u][v] : (double)wr[g][v];
           acc[v] += dterm(a, (double)wr[g][v]);  // out-of-range elements are 0: they add 0
@@ -642,7 +684,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
       const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
       if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
-      ld_chunk(sv2, 0, cs[0]);
+      if (KC == 0) ld_chunk_sub(sv2, 0, cs[0]);
       ld_chunk(MgslSeg<V>(q2 ? q2 : Vb, e0, N, seg), 0, cn[0]);
       if (tid < 64) {
         const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
@@ -654,7 +696,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
     }
     if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
     mgs_arrive(bar, (unsigned)(p + 1));
-    ld_chunk(sv2, 0, cs[0]);
+    if (KC == 0) ld_chunk_sub(sv2, 0, cs[0]);
     ld_chunk(MgslSeg<V>(q2 ? q2 : Vb, e0, N, seg), 0, cn[0]);
     if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
     reduce_rows<kMgsBlock, true>(slot, G, k, red);
@@ -1272,11 +1314,11 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       else if (sizeof(V) == 4 && fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
       else if (!(e && atoi(e) == 1)) {  // KRY_MGS_PERSIST=1: the register-resident kernel only
         s->mgsp_large = true;
-        if (fits(gm_mgsl_kernel<V, 12, mgsl_u<12>()>, 12 * W)) s->mgsp_E = 12 * W;
-        else if (fits(gm_mgsl_kernel<V, 16, mgsl_u<16>()>, 16 * W)) s->mgsp_E = 16 * W;
-        else if (fits(gm_mgsl_kernel<V, 24, mgsl_u<24>()>, 24 * W)) s->mgsp_E = 24 * W;
-        else if (fits(gm_mgsl_kernel<V, 32, mgsl_u<32>()>, 32 * W)) s->mgsp_E = 32 * W;
-        else if (fits(gm_mgsl_kernel<V, 40, mgsl_u<40>()>, 40 * W)) s->mgsp_E = 40 * W;
+        if (fits(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>, 12 * W)) s->mgsp_E = 12 * W;
+        else if (fits(gm_mgsl_kernel<V, 16, mgsl_u<16>(), true>, 16 * W)) s->mgsp_E = 16 * W;
+        else if (fits(gm_mgsl_kernel<V, 24, mgsl_u<24>(), true>, 24 * W)) s->mgsp_E = 24 * W;
+        else if (fits(gm_mgsl_kernel<V, 32, mgsl_u<32>(), true>, 32 * W)) s->mgsp_E = 32 * W;
+        else if (fits(gm_mgsl_kernel<V, 40, mgsl_u<40>(), true>, 40 * W)) s->mgsp_E = 40 * W;
         else s->mgsp_large = false;
       }
     }
@@ -1303,13 +1345,25 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
                        pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step, vnext);
   };
   s->mgsp_norm = s->mgsp_large;
-  if (s->mgsp_large) {
+  static const bool mgsl_nt = [] {
+    const char *e = getenv("KRY_MGSL_NT");  // tuning override: subtrahend loads nontemporal (1) or not (0)
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (s->mgsp_large && mgsl_nt) {
     switch (E / W) {
-      case 12: gol(gm_mgsl_kernel<V, 12, mgsl_u<12>()>); break;
-      case 16: gol(gm_mgsl_kernel<V, 16, mgsl_u<16>()>); break;
-      case 24: gol(gm_mgsl_kernel<V, 24, mgsl_u<24>()>); break;
-      case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>()>); break;
-      default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>()>); break;
+      case 12: gol(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>); break;
+      case 16: gol(gm_mgsl_kernel<V, 16, mgsl_u<16>(), true>); break;
+      case 24: gol(gm_mgsl_kernel<V, 24, mgsl_u<24>(), true>); break;
+      case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>(), true>); break;
+      default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>(), true>); break;
+    }
+  } else if (s->mgsp_large) {
+    switch (E / W) {
+      case 12: gol(gm_mgsl_kernel<V, 12, mgsl_u<12>(), false>); break;
+      case 16: gol(gm_mgsl_kernel<V, 16, mgsl_u<16>(), false>); break;
+      case 24: gol(gm_mgsl_kernel<V, 24, mgsl_u<24>(), false>); break;
+      case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>(), false>); break;
+      default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>(), false>); break;
     }
   } else if (E == 8) {
     go(gm_mgsp_kernel<V, 8>);
