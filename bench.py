@@ -14,8 +14,9 @@ column of the same matrix on its own GPU (RHS sharding) with
 one RCCL allreduce of the residual-norm vector per iteration for the global
 stop rule; value = total RHS-iterations per second (weak scaling).
 
-Also reported (N = 1): the live SpMV roofline (HIP events around every SpMV
-launch of the timed region), GMRES(30) on the cfg3 matrix, the secondary
+Also reported (N = 1): the live SpMV roofline (HIP events around one SpMV
+launch in 4 of the timed region: two event records per timed launch cost the
+stream ~6 us, so timing all of them would slow the measured iteration), GMRES(30) on the cfg3 matrix, the secondary
 BASELINE configs (cfg2 CG Poisson 1000^2, cfg4 block CG 8 RHS on Poisson
 3163^2, cfg5 weighted fp32 MINRES 200^3), and the CPU baseline: the oracle
 (the reference iteration on NumPy/SciPy) on a bounded sample of the metric
@@ -33,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SPMV_TIMED_EVERY = 4  # the live SpMV timing samples one launch in 4 of the timed region
 
 
 def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
@@ -118,7 +120,9 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     chunk = st.preferred_chunk()
     _iterate(st, warmup, ncols, chunk)
     ctx.synchronize()
-    ctx.profile(True)
+    # HIP events around one SpMV launch in 4 (two event records per timed
+    # launch cost ~6 us of stream time; every launch of every kernel, 20 us)
+    ctx.profile(True, kernels=[_lib.PROF_SPMV], every=SPMV_TIMED_EVERY)
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -128,14 +132,12 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     barrier(pg)
     elapsed = allmax(pg, t1 - t0)
     cnt, spmv_ms = ctx.profile_read(_lib.PROF_SPMV)
-    ucnt, upd_ms = ctx.profile_read(_lib.PROF_UPDATE)
     ctx.profile(False)
     del st
     if comm is not None:
         comm.close()
     layout = A.layout()
-    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_ms": spmv_ms, "update_count": ucnt, "update_ms": upd_ms,
-            "n": A.n, "nnz": A.nnz, "layout": layout}
+    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_ms": spmv_ms, "n": A.n, "nnz": A.nnz, "layout": layout}
 
 
 def spmv_kernel_desc(layout):
@@ -351,6 +353,8 @@ def main():
             "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; "
                              + image_note + ")",
             "launches_timed": res["spmv_count"],
+            "timing": f"HIP events on the solver stream around one SpMV launch in {SPMV_TIMED_EVERY} of the timed "
+                      f"region ({args.steps} launches)",
             "image_bytes_per_launch": image_bytes,
             "image_gbs": image_bytes / spmv_avg_s / 1e9 if image_bytes else None,
             "image_frac": image_bytes / spmv_avg_s / 1e9 / HBM_PEAK_GBS if image_bytes else None,

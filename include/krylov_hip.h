@@ -253,9 +253,14 @@ int kry_minres_attach_comm(kry_minres *s, kry_comm *c, int32_t col_offset, int32
 /* ---- timing: HIP events on the context stream --------------------------- */
 int kry_timer_start(kry_ctx *ctx);
 int kry_timer_stop(kry_ctx *ctx, double *ms);
-/* average device time of the most recent SpMV launches made by CG runs,
- * measured with HIP events around each SpMV launch when enabled */
+/* device time of the solvers' launches per kernel id (0 SpMV, 1 update
+ * pass, 2 MGS, 3 other), measured with HIP events around the launches when
+ * enabled; enable != 0 times every launch of every id, kry_profile_select
+ * only the ids whose bit is set in mask and of those one launch in `every`
+ * (each timed launch adds two event records to the stream: ~3 us at the
+ * metric). Both reset the counts. kry_profile_read: timed launches, total ms. */
 int kry_profile_enable(kry_ctx *ctx, int enable);
+int kry_profile_select(kry_ctx *ctx, uint32_t mask, int32_t every);
 int kry_profile_read(kry_ctx *ctx, int kernel_id, int64_t *count, double *total_ms);
 
 #ifdef __cplusplus

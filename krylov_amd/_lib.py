@@ -105,6 +105,7 @@ _SIGNATURES = {
     "kry_timer_start": [_vp],
     "kry_timer_stop": [_vp, _dp],
     "kry_profile_enable": [_vp, _int],
+    "kry_profile_select": [_vp, ctypes.c_uint32, ctypes.c_int32],
     "kry_profile_read": [_vp, _int, _ip64, _dp],
 }
 

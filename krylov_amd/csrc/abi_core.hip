@@ -47,7 +47,8 @@ double *ctx_scratch(kry_ctx *ctx, size_t bytes) {
 }
 
 ProfScope::ProfScope(kry_ctx *c, int kernel_id) : ctx(c), id(kernel_id) {
-  if (!ctx->profile) return;
+  if (!((ctx->profile >> kernel_id) & 1u)) return;
+  if (ctx->prof_calls[kernel_id]++ % ctx->prof_every != 0) return;
   if (ctx->ev_used == ctx->ev_pool.size()) {
     hipEvent_t a, b;
     KRY_HIP(hipEventCreate(&a));
@@ -836,11 +837,15 @@ int kry_timer_stop(kry_ctx *ctx, double *ms) {
   KRY_API_END
 }
 
-int kry_profile_enable(kry_ctx *ctx, int enable) {
+int kry_profile_enable(kry_ctx *ctx, int enable) { return kry_profile_select(ctx, enable ? 0xFu : 0u, 1); }
+
+int kry_profile_select(kry_ctx *ctx, uint32_t mask, int32_t every) {
   KRY_API_BEGIN
-  KRY_REQUIRE(ctx, KRY_EINVAL, "null ctx");
+  KRY_REQUIRE(ctx && every >= 1, KRY_EINVAL, "bad argument");
   KRY_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->profile = enable != 0;
+  ctx->profile = mask & 0xFu;
+  ctx->prof_every = every;
+  for (int i = 0; i < 4; ++i) ctx->prof_calls[i] = 0;
   ctx->ev_used = 0;
   for (int i = 0; i < 4; ++i) {
     ctx->prof_count[i] = 0;

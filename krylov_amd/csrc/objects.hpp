@@ -11,7 +11,9 @@ struct kry_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t t0 = nullptr, t1 = nullptr;
   // per-kernel HIP-event profiling (bench.py's live roofline measurement)
-  bool profile = false;
+  unsigned profile = 0;  // bit id: HIP events around launches of kernel id (PROF_*)
+  int prof_every = 1;    // ... around one launch in prof_every of each id
+  int64_t prof_calls[4] = {0, 0, 0, 0};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   size_t ev_used = 0;
   int ev_kernel_id = 0;  // which kernel family the pool currently records

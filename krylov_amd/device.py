@@ -35,8 +35,16 @@ class Context:
         check(lib.kry_timer_stop(self.handle, ctypes.byref(ms)))
         return ms.value
 
-    def profile(self, enable=True):
-        check(lib.kry_profile_enable(self.handle, 1 if enable else 0))
+    def profile(self, enable=True, kernels=None, every=1):
+        """HIP-event timing of the solvers' launches: every kernel id, or
+        only the ids in ``kernels`` (e.g. ``[_lib.PROF_SPMV]``), one launch
+        in ``every``."""
+        if kernels is None and every == 1:
+            check(lib.kry_profile_enable(self.handle, 1 if enable else 0))
+        else:
+            ids = range(4) if kernels is None else kernels
+            mask = sum(1 << int(i) for i in ids) if enable else 0
+            check(lib.kry_profile_select(self.handle, mask, int(every)))
 
     def profile_read(self, kernel_id=_lib.PROF_SPMV):
         cnt = ctypes.c_int64()
