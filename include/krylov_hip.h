@@ -160,6 +160,14 @@ int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps);
  * uninterrupted solve. Fault injection for tests: KRY_CGP_FAULT=t makes the
  * last block drop out at iteration t of a chunk. */
 int kry_cg_path(kry_cg *s, int32_t *info);
+/* The same for the one-launch update of the launch-per-pass form (large n,
+ * one RHS, no M / Ml, Euclidean inner: alpha, r, rho, omega, y and p of an
+ * iteration in one cooperative launch after the SpMV): info[0] = 1 if the last
+ * kry_cg_run chunk used it; info[1] = chunks whose remaining steps were rerun
+ * with separate passes after its exchange timed out (it writes nothing
+ * before the exchange completes). KRY_CG_UPD=0 disables it; KRY_CGU_FAULT=t
+ * makes the last block drop out at step t of a chunk (tests). */
+int kry_cg_update_path(kry_cg *s, int32_t *info);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
 int kry_cg_scalars(kry_cg *s, double *out);

@@ -63,6 +63,13 @@ class _CGState:
         check(lib.kry_cg_path(self.h, info))
         return bool(info[0]), int(info[1])
 
+    def update_path(self):
+        """(one_launch_update, fallbacks) of the launch-per-pass form
+        (kry_cg_update_path)."""
+        info = (ctypes.c_int32 * 2)()
+        check(lib.kry_cg_update_path(self.h, info))
+        return bool(info[0]), int(info[1])
+
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)
         check(lib.kry_cg_residual(self.h, _lib.dptr(out)))

@@ -65,6 +65,13 @@ struct kry_cg {
   int cgp_spw = -1;
   int cgp_fallbacks = 0;  // chunks rerun on the launch-per-pass path after a timeout
   bool cgp_last = false;  // the last kry_cg_run chunk ran the persistent loop
+  // one-launch update (cg_upd_kernel): upd_nv = -1 undecided, 0 not used,
+  // else granules per thread; its abort word and granule region
+  int upd_nv = -1;
+  unsigned *upd_words = nullptr;
+  int upd_fallbacks = 0;
+  bool upd_used = false;  // an update kernel was launched in the current chunk
+  bool upd_last = false;  // ... in the last kry_cg_run chunk
 };
 
 namespace {
@@ -296,6 +303,144 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
         gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
       }
     } else if (all_le(rn, scal + S_CRIT * k, k, &flag) && tid == 0) {
+      ctrl->stop_at = step + 1;
+    }
+  }
+}
+
+// ------------------------------------- one-launch CG update (large n, k = 1)
+// Replaces the alpha kernel, the r pass and the fused rho / y / p pass of an
+// iteration for one right-hand side, no M / Ml, Euclidean inner and n up to
+// 512 * 40 * 2 per block at one 512-thread block per CU (n = 10.5 M doubles),
+// with the same scalar arithmetic:
+//   alpha = rho / guard(<p, Ap>)  (every block sums the SpMV's partials in
+//                                  the alpha kernel's fixed order)
+//   r' = r - alpha Ap, <r', r'>   (r' kept in registers; block partial)
+//   all-gather of the block partials -> rho' = <r', r'>, omega = rho' / guard(rho)
+//   y += alpha p, p = r' + omega p; y, p and r' stored
+// so an iteration streams Ap, r, y, p in and r, y, p out (7 vectors, the
+// launch-per-pass form moves 8: r twice) with one kernel boundary instead of
+// three. Nothing is stored before the exchange has completed: a timed-out
+// exchange (a block not resident) leaves the iteration's state untouched, the
+// kernel halts the chunk at this step and kry_cg_run reruns it launch per
+// pass. A block that comes late to a finished exchange re-checks the abort
+// word before it writes anything.
+constexpr int kUpdBlock = 512;
+constexpr int kUpdU = 2;  // granules per streamed chunk
+constexpr size_t kUpdWords = 16 + 2 * 2 * 256 * 2;  // abort word area + two parity regions of G <= 256 granule pairs
+template <typename V, typename S, int NV>
+__global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restrict__ y, V *__restrict__ r,
+                                                           V *__restrict__ p, const V *__restrict__ Ap,
+                                                           const double *__restrict__ partA, int PA, double *scal,
+                                                           double *hist, Ctrl *ctrl, int step, double *gbuf,
+                                                           int col_offset, int total_k, unsigned *words,
+                                                           int fault_step) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int U = kUpdU;
+  constexpr int NC = NV / U;
+  static_assert(NV % U == 0, "chunks must tile the thread's granules");
+  __shared__ double red[kUpdBlock];
+  __shared__ double shv[2];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_CGU_FAULT)
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  const int64_t seg = (int64_t)NV * kUpdBlock * W;
+  const int64_t e0 = (int64_t)blockIdx.x * seg;
+  const BufSeg<V, kUpdBlock> sr(r, e0, N, seg), sa(Ap, e0, N, seg), sy(y, e0, N, seg), sp(p, e0, N, seg);
+  V ca[2][U][W], cb[2][U][W];
+  auto ld2 = [&](const BufSeg<V, kUpdBlock> &s1, const BufSeg<V, kUpdBlock> &s2, int c, V(&d1)[U][W],
+                 V(&d2)[U][W]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s1.template load<W>(c * U + u, d1[u]);
+      s2.template load<W, 2>(c * U + u, d2[u]);  // second stream (Ap / p... see callers) nontemporal
+    }
+  };
+  ld2(sr, sa, 0, ca[0], cb[0]);  // chunk 0 of r and Ap travels during the alpha reduction
+  // alpha = rho / guard(<p, Ap>)  (cg.py:183-185), same order as cg_alpha_kernel
+  reduce_partials<kUpdBlock>(partA, PA, 1, red);
+  const S rho = (S)scal[S_RHO];
+  const S alpha = rho / safe<S>((S)red[0]);
+  const V a = (V)alpha;
+  // r' = r - alpha Ap (cg.py:200) and <r', r'>
+  V rr[NV][W];
+  double acc = 0.0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int b = c & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NC) ld2(sr, sa, c + 1, ca[b ^ 1], cb[b ^ 1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = c * U + u;
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V t2 = a * cb[b][u][v];
+        rr[g][v] = ca[b][u][v] - t2;
+        const double rd = (double)rr[g][v];
+        acc += dterm(rd, rd);  // out-of-range elements are 0: they add 0
+      }
+    }
+  }
+  const double bp = block_sum1_t0(acc, red);
+  unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16) + (size_t)(step & 1) * 2 * 256;
+  const unsigned tag = (unsigned)step + 1u;
+  if (tid == 0) publish_partial(gran + 2 * blockIdx.x, tag, bp);
+  ld2(sp, sy, 0, ca[0], cb[0]);  // chunk 0 of p and y travels during the exchange
+  if (tid < 64) {
+    bool ok = sweep_partials(gran, G, tag, words, ctrl, &shv[0], spin_limit);
+    // a late block must not write after the others gave up
+    if (ok && __hip_atomic_load(words + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) ok = false;
+    if (tid == 0) flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  if (!__builtin_amdgcn_readfirstlane(flag)) {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+    return;
+  }
+  const S rrs = (S)shv[0];
+  const S om = rrs / safe<S>(rho);  // omega = rhos[-1] / rhos[-2] (cg.py:177)
+  const V o = (V)om;
+  // y += alpha p (cg.py:196), p = r' + omega p (cg.py:178); y, p, r' stored
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int b = c & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NC) ld2(sp, sy, c + 1, ca[b ^ 1], cb[b ^ 1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = c * U + u;
+      V yv[W], pv[W];
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V t1 = a * ca[b][u][v];
+        yv[v] = cb[b][u][v] + t1;
+        const V t = o * ca[b][u][v];
+        pv[v] = rr[g][v] + t;
+      }
+      sy.template store<W, 2>(g, yv);
+      sp.template store<W>(g, pv);
+      sr.template store<W>(g, rr[g]);
+    }
+  }
+  if (blockIdx.x == 0) {
+    if (tid == 0) {
+      scal[S_ALPHA] = (double)alpha;
+      scal[S_RHO_OLD] = (double)rho;
+      scal[S_RHO_PREV] = (double)rho;
+      scal[S_RHO] = (double)rrs;
+      scal[S_OMEGA] = (double)om;
+      const double nrm = (double)sqrt(rrs);
+      red[0] = nrm;
+      if (!gbuf) hist[step] = nrm;
+    }
+    __syncthreads();
+    if (gbuf) {
+      for (int t = tid; t < total_k; t += kUpdBlock) gbuf[t] = t == col_offset ? red[0] : 0.0;
+    } else if (all_le(red, scal + S_CRIT, 1, &flag) && tid == 0) {
       ctrl->stop_at = step + 1;
     }
   }
@@ -750,6 +895,83 @@ bool cgp_launch(kry_cg *s, int max_steps, bool decide_only = false) {
   return taken;
 }
 
+// One-launch update of step `step` (cg_upd_kernel) if eligible: one RHS, no
+// M / Ml, Euclidean inner, n larger than the persistent loop serves and at
+// most 512 * 40 granules per block at one block per CU (decided once per
+// solver; KRY_CG_UPD=0 disables). Cooperative launch: the runtime refuses a
+// grid it cannot make co-resident, and then this step and the rest of the
+// solve take the launch-per-pass form. Returns false when not launched.
+template <typename V, typename S, int NV>
+void *cgu_kern() {
+  return reinterpret_cast<void *>(cg_upd_kernel<V, S, NV>);
+}
+template <typename V>
+bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) {
+  constexpr int W = Vec16<V>::W;
+  using S = V;
+  const int64_t N = s->n;
+  auto kern = [&](int nv) -> void * {
+    switch (nv) {
+      case 8: return cgu_kern<V, S, 8>();
+      case 16: return cgu_kern<V, S, 16>();
+      case 24: return cgu_kern<V, S, 24>();
+      case 32: return cgu_kern<V, S, 32>();
+      default: return cgu_kern<V, S, 40>();
+    }
+  };
+  if (s->upd_nv < 0) {
+    s->upd_nv = 0;
+    const char *e = getenv("KRY_CG_UPD");
+    const bool scalars_match = (sizeof(V) == 8) != s->scalar_f32;
+    if (!(e && atoi(e) == 0) && s->k == 1 && !s->M && !s->Ml && !s->w && scalars_match) {
+      int dev = 0, ncu = 0, coop = 0;
+      KRY_HIP(hipGetDevice(&dev));
+      KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      KRY_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+      const int gmax = ncu < 256 ? ncu : 256;
+      for (int nv : {8, 16, 24, 32, 40}) {
+        if (!coop) break;
+        const int64_t G = (N + (int64_t)kUpdBlock * nv * W - 1) / ((int64_t)kUpdBlock * nv * W);
+        if (G > gmax) continue;
+        int per_cu = 0;
+        KRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern(nv)),
+                                                             kUpdBlock, 0));
+        if (per_cu >= 1) s->upd_nv = nv;
+        break;
+      }
+      if (s->upd_nv > 0) s->upd_words = static_cast<unsigned *>(dev_alloc(kUpdWords * 4));
+    }
+  }
+  if (s->upd_nv == 0) return false;
+  const int nv = s->upd_nv;
+  const int G = (int)((N + (int64_t)kUpdBlock * nv * W - 1) / ((int64_t)kUpdBlock * nv * W));
+  hipStream_t st = s->ctx->stream;
+  if (step == 0) KRY_HIP(hipMemsetAsync(s->upd_words, 0, kUpdWords * 4, st));
+  const char *fe = getenv("KRY_CGU_FAULT");  // fault injection (tests): step at which a block drops out
+  int fault_step = fe ? atoi(fe) : -1;
+  V *y = static_cast<V *>(s->y), *r = static_cast<V *>(s->r), *p = static_cast<V *>(s->p);
+  const V *Ap = static_cast<const V *>(s->Ap);
+  double *scal = s->scal, *hist = s->hist;
+  Ctrl *ctrl = s->ctrl;
+  int col_offset = s->col_offset, total_k = s->total_k;
+  unsigned *words = s->upd_words;
+  int64_t n = N;
+  void *args[] = {&n, &y, &r, &p, &Ap, &partA, &PA, &scal, &hist, &ctrl, &step, &gbuf, &col_offset, &total_k,
+                  &words, &fault_step};
+  hipError_t le;
+  {
+    ProfScope ps(s->ctx, PROF_UPDATE);
+    le = hipLaunchCooperativeKernel(kern(nv), dim3(G), dim3(kUpdBlock), args, 0, st);
+  }
+  if (le != hipSuccess) {
+    (void)hipGetLastError();  // clear the refusal; the launch-per-pass form takes over
+    s->upd_nv = 0;
+    return false;
+  }
+  s->upd_used = true;
+  return true;
+}
+
 // Returns true when the chunk ran as one persistent launch.
 template <typename V, typename MV, typename I>
 bool cg_run_impl(kry_cg *s, int max_steps) {
@@ -773,12 +995,16 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
                               s->ctrl, step, st);
       }
     }
-    if (s->scalar_f32)
-      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
-    else
-      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
     double *gb = s->comm ? s->gbuf : nullptr;
-    if (!s->M && k <= 8) {  // r pass, then the fused rho / y / p pass
+    if (!s->M && !s->Ml && k == 1 && cgu_launch<V>(s, partA, PA, step, gb)) {
+      // alpha, r, rho, omega, y and p in one launch (cg_upd_kernel)
+    } else if (!s->M && k <= 8) {  // alpha kernel, r pass, then the fused rho / y / p pass
+      if (s->scalar_f32)
+        hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                           step);
+      else
+        hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                           step);
       {
         ProfScope ps(s->ctx, PROF_UPDATE);
         PB = launch_elementwise<V>(N, k,
@@ -798,7 +1024,13 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
                            static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
                            s->col_offset, s->total_k);
       KRY_HIP(hipGetLastError());
-    } else {  // update pass, [z = M r], one-block rho kernel, p pass
+    } else {  // alpha kernel, update pass, [z = M r], one-block rho kernel, p pass
+      if (s->scalar_f32)
+        hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                           step);
+      else
+        hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                           step);
       {
         ProfScope ps(s->ctx, PROF_UPDATE);
         PB = launch_elementwise<V>(N, k,
@@ -872,7 +1104,7 @@ static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
                   s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
                   s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
-                  s->cgp_scal, s->cgp_words};
+                  s->cgp_scal, s->cgp_words, s->upd_words};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -988,27 +1220,42 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * hk * 8));
     s->chunk_cap = max_steps;
   }
-  auto run_chunk = [&](Ctrl *c) -> std::pair<int, bool> {
+  auto run_steps = [&](int steps, double *rows, Ctrl *c) -> std::pair<int, bool> {
     reset_ctrl(s->ctrl, st);
     bool persistent = false;
+    s->upd_used = false;
     dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) {
-      persistent = cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps);
+      persistent = cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, steps);
     });
-    return {read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, hk, resnorms, c), persistent};
+    return {read_chunk(s->ctx, st, s->ctrl, s->hist, steps, hk, rows, c), persistent};
   };
+  auto run_chunk = [&](Ctrl *c) { return run_steps(max_steps, resnorms, c); };
   Ctrl c;
   auto [done, persistent] = run_chunk(&c);
+  bool upd = s->upd_used;
   if (persistent && c.status == KRY_EDEVICE) {
     // an in-launch exchange timed out (a block was not resident): the kernel
     // left the chunk-start state untouched; rerun the chunk launch per pass
     s->cgp_spw = 0;
     ++s->cgp_fallbacks;
     std::tie(done, persistent) = run_chunk(&c);
+    upd = s->upd_used;
   } else if (persistent) {
     cgp_commit(s, done);
+  } else if (upd && c.status == KRY_EDEVICE) {
+    // a one-launch update timed out at step `done` and wrote nothing: the
+    // steps before it stand; rerun the rest of the chunk launch per pass,
+    // from that step's SpMV (p is unchanged, so it recomputes the same Ap)
+    s->upd_nv = 0;
+    ++s->upd_fallbacks;
+    const int first = done;
+    auto [more, pers2] = run_steps(max_steps - first, resnorms + (size_t)first * hk, &c);
+    (void)pers2;
+    done = first + more;
   }
   KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: device error status " + std::to_string(c.status));
   s->cgp_last = persistent;
+  s->upd_last = upd;
   s->it += done;
   *steps_done = done;
   KRY_API_END
@@ -1034,6 +1281,14 @@ int kry_cg_path(kry_cg *s, int32_t *info) {
   KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
   info[0] = s->cgp_last ? 1 : 0;
   info[1] = s->cgp_fallbacks;
+  KRY_API_END
+}
+
+int kry_cg_update_path(kry_cg *s, int32_t *info) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
+  info[0] = s->upd_last ? 1 : 0;
+  info[1] = s->upd_fallbacks;
   KRY_API_END
 }
 

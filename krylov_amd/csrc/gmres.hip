@@ -434,44 +434,8 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
 // registers; the descriptor's record count ends at N, so the tail's
 // out-of-range granules read as 0 (they add 0 to the partials and stay 0 in
 // w) and their stores are dropped.
-typedef unsigned int mgsl_u4 __attribute__((ext_vector_type(4)));
 template <typename V>
-struct MgslSeg {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ MgslSeg(const V *vec, int64_t e0, int64_t N, int64_t seg) {
-    const int64_t rem = N - e0;
-    const int64_t cnt = rem < seg ? (rem > 0 ? rem : 0) : seg;
-    // wave-uniform by construction; readfirstlane makes it provable, so the
-    // buffer ops take the descriptor from SGPRs without a waterfall loop
-    const uint64_t a = reinterpret_cast<uint64_t>(vec + e0);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    const int bytes = __builtin_amdgcn_readfirstlane((int)(cnt * (int64_t)sizeof(V)));
-    r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
-  }
-  template <int W, int AUX = 0>
-  __device__ __forceinline__ void load(int u, V (&o)[W]) const {
-    const mgsl_u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, u * kMgsBlock * 16, AUX);
-    if constexpr (W == 2) {
-      const double2 d = __builtin_bit_cast(double2, t);
-      o[0] = d.x;
-      o[1] = d.y;
-    } else {
-      const float4 f = __builtin_bit_cast(float4, t);
-      o[0] = f.x;
-      o[1] = f.y;
-      o[2] = f.z;
-      o[3] = f.w;
-    }
-  }
-  template <int W>
-  __device__ __forceinline__ void store(int u, const V (&o)[W]) const {
-    mgsl_u4 t;
-    if constexpr (W == 2) t = __builtin_bit_cast(mgsl_u4, double2{o[0], o[1]});
-    else t = __builtin_bit_cast(mgsl_u4, float4{o[0], o[1], o[2], o[3]});
-    __builtin_amdgcn_raw_buffer_store_b128(t, r, (int)threadIdx.x * 16, u * kMgsBlock * 16, 0);
-  }
-};
+using MgslSeg = BufSeg<V, kMgsBlock>;
 
 template <typename V, int NV, int U, bool NT>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V *__restrict__ w,

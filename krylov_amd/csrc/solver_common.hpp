@@ -132,6 +132,71 @@ __device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) 
   __syncthreads();
 }
 
+// ------------------------------------------ block-segment buffer access
+// The persistent kernels that hold a vector segment per thread in registers
+// (streamed MGS, one-launch CG update) address it with buffer loads/stores
+// over the block's segment of each vector: a descriptor from wave-uniform
+// values, the per-lane byte offset tid * 16 and the granule's offset
+// u * BLOCK * 16 as a scalar, so no per-granule address registers; the
+// descriptor's record count ends at N, so out-of-range granules read as 0
+// and their stores are dropped.
+typedef unsigned int bufseg_u4 __attribute__((ext_vector_type(4)));
+template <typename V, int BLOCK>
+struct BufSeg {
+  __amdgpu_buffer_rsrc_t r;
+  V *base;      // the segment's first element (wave-uniform)
+  int64_t cnt;  // its elements inside [0, N)
+  __device__ __forceinline__ BufSeg(const V *vec, int64_t e0, int64_t N, int64_t seg) {
+    const int64_t rem = N - e0;
+    cnt = rem < seg ? (rem > 0 ? rem : 0) : seg;
+    // wave-uniform by construction; readfirstlane makes it provable, so the
+    // buffer ops take the descriptor from SGPRs without a waterfall loop
+    const uint64_t a = reinterpret_cast<uint64_t>(vec + e0);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(cnt * (int64_t)sizeof(V)));
+    base = reinterpret_cast<V *>(((uint64_t)hi << 32) | lo);
+    r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+  }
+  template <int W, int AUX = 0>
+  __device__ __forceinline__ void load(int u, V (&o)[W]) const {
+    const bufseg_u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, u * BLOCK * 16, AUX);
+    if constexpr (W == 2) {
+      const double2 d = __builtin_bit_cast(double2, t);
+      o[0] = d.x;
+      o[1] = d.y;
+    } else {
+      const float4 f = __builtin_bit_cast(float4, t);
+      o[0] = f.x;
+      o[1] = f.y;
+      o[2] = f.z;
+      o[3] = f.w;
+    }
+  }
+  // Stores are plain global stores, guarded at the segment's end: with
+  // __builtin_amdgcn_raw_buffer_store_b128 hipcc (ROCm 7.2, gfx950) may let a
+  // VALU overwrite the store's data VGPRs in the very next instruction, before
+  // the 16-byte store has read them (seen as corrupted lanes 12-15 of every 16
+  // in one element: tools/cgu_debug.py); for global stores it keeps the wait
+  // states.
+  template <int W, int AUX = 0>
+  __device__ __forceinline__ void store(int u, const V (&o)[W]) const {
+    typedef V vec_t __attribute__((ext_vector_type(W)));
+    const int64_t e = ((int64_t)u * BLOCK + threadIdx.x) * W;
+    if (e + W <= cnt) {
+      vec_t t;
+#pragma unroll
+      for (int v = 0; v < W; ++v) t[v] = o[v];
+      if (AUX & 2) __builtin_nontemporal_store(t, reinterpret_cast<vec_t *>(base + e));
+      else *reinterpret_cast<vec_t *>(base + e) = t;
+    } else {
+#pragma unroll
+      for (int v = 0; v < W; ++v)
+        if (e + v < cnt) base[e + v] = o[v];
+    }
+  }
+};
+
 // guarded divisor, np.where(d != 0, d, 1.0)
 template <typename S>
 __device__ __forceinline__ S safe(S d) {

@@ -103,3 +103,67 @@ def test_gmres_persistent_mgs_timeout_falls_back(monkeypatch, ortho):
     hist, _ = st.run(6)
     assert len(hist) == 6
     assert st.path() == (False, 1)
+
+
+@pytest.mark.parametrize("fault_step", [0, 4])
+def test_cg_update_kernel_timeout_falls_back(monkeypatch, fault_step):
+    """The one-launch update of the launch-per-pass form (cg_upd_kernel,
+    n beyond the persistent loop; forced here with KRY_CG_PERSIST=0): a block
+    that never joins the exchange at step `fault_step` of the first chunk.
+    Nothing was written, the rest of the chunk is rerun with separate passes
+    from that step's SpMV, and the solve keeps the reference's iteration."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+    from oracle import krylov_ref
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    R = problems.poisson2d(300)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(13).standard_normal(R.shape[0])
+    _, clean = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.setenv("KRY_CGU_FAULT", str(fault_step))
+    _, faulted = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    assert faulted.numsteps == clean.numsteps
+    f, c = np.asarray(faulted.resnorms), np.asarray(clean.resnorms)
+    np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-10)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-10, atol=1e-12 * np.abs(clean.xk).max())
+    _, ref = krylov_ref.cg(R, b, tol=1e-9, maxiter=500)
+    assert ref.numsteps == faulted.numsteps
+    np.testing.assert_allclose(f[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+    # the state reports the switch: used in the faulted chunk, then off
+    st = _CGState(_helpers.Problem(A, b, None, None))
+    st.start()
+    st.set_criterion(np.zeros(1))
+    assert len(st.run(8)) == 8
+    assert st.update_path() == (True, 1)
+    assert len(st.run(8)) == 8
+    assert st.update_path() == (False, 1)
+
+
+def test_cg_update_kernel_matches_separate_passes(monkeypatch):
+    """n = 2.0 M (Poisson 1414^2, above the persistent loop's 1 M): the
+    one-launch update against the alpha / r / yp passes (KRY_CG_UPD=0) and
+    the oracle's first 40 steps."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+    from oracle import krylov_ref
+
+    P = problems.poisson2d(1414)
+    A = krylov_amd.CsrOperator(P)
+    b = np.random.default_rng(14).standard_normal(P.shape[0])
+    st = _CGState(_helpers.Problem(A, b, None, None))
+    st.start()
+    st.set_criterion(np.zeros(1))
+    h1 = st.run(40)[:, 0]
+    assert st.update_path() == (True, 0)
+    monkeypatch.setenv("KRY_CG_UPD", "0")
+    st0 = _CGState(_helpers.Problem(A, b, None, None))
+    st0.start()
+    st0.set_criterion(np.zeros(1))
+    h0 = st0.run(40)[:, 0]
+    assert st0.update_path() == (False, 0)
+    np.testing.assert_allclose(h1, h0, rtol=1e-12)
+    _, ref = krylov_ref.cg(P, b, tol=0.0, atol=0.0, maxiter=40)
+    np.testing.assert_allclose(h1, np.asarray(ref.resnorms)[1:41], rtol=1e-10)
