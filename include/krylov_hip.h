@@ -162,7 +162,7 @@ int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps);
 int kry_cg_path(kry_cg *s, int32_t *info);
 /* The same for the one-launch update of the launch-per-pass form (large n,
  * one RHS, no M / Ml, Euclidean inner: alpha, r, rho, omega, y and p of an
- * iteration in one cooperative launch after the SpMV): info[0] = 1 if the last
+ * iteration in one launch after the SpMV): info[0] = 1 if the last
  * kry_cg_run chunk used it; info[1] = chunks whose remaining steps were rerun
  * with separate passes after its exchange timed out (it writes nothing
  * before the exchange completes). KRY_CG_UPD=0 disables it; KRY_CGU_FAULT=t

@@ -312,7 +312,8 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 // Replaces the alpha kernel, the r pass and the fused rho / y / p pass of an
 // iteration for one right-hand side, no M / Ml, Euclidean inner and n up to
 // 512 * 40 * 2 per block at one 512-thread block per CU (n = 10.5 M doubles),
-// with the same scalar arithmetic:
+// with the same scalar arithmetic (one launch of at most one block per CU,
+// all resident):
 //   alpha = rho / guard(<p, Ap>)  (every block sums the SpMV's partials in
 //                                  the alpha kernel's fixed order)
 //   r' = r - alpha Ap, <r', r'>   (r' kept in registers; block partial)
@@ -898,9 +899,7 @@ bool cgp_launch(kry_cg *s, int max_steps, bool decide_only = false) {
 // One-launch update of step `step` (cg_upd_kernel) if eligible: one RHS, no
 // M / Ml, Euclidean inner, n larger than the persistent loop serves and at
 // most 512 * 40 granules per block at one block per CU (decided once per
-// solver; KRY_CG_UPD=0 disables). Cooperative launch: the runtime refuses a
-// grid it cannot make co-resident, and then this step and the rest of the
-// solve take the launch-per-pass form. Returns false when not launched.
+// solver; KRY_CG_UPD=0 disables). Returns false when not launched.
 template <typename V, typename S, int NV>
 void *cgu_kern() {
   return reinterpret_cast<void *>(cg_upd_kernel<V, S, NV>);
@@ -924,13 +923,11 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
     const char *e = getenv("KRY_CG_UPD");
     const bool scalars_match = (sizeof(V) == 8) != s->scalar_f32;
     if (!(e && atoi(e) == 0) && s->k == 1 && !s->M && !s->Ml && !s->w && scalars_match) {
-      int dev = 0, ncu = 0, coop = 0;
+      int dev = 0, ncu = 0;
       KRY_HIP(hipGetDevice(&dev));
       KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      KRY_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
       const int gmax = ncu < 256 ? ncu : 256;
       for (int nv : {8, 16, 24, 32, 40}) {
-        if (!coop) break;
         const int64_t G = (N + (int64_t)kUpdBlock * nv * W - 1) / ((int64_t)kUpdBlock * nv * W);
         if (G > gmax) continue;
         int per_cu = 0;
@@ -960,11 +957,16 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
                   &words, &fault_step};
   hipError_t le;
   {
+    // A plain launch: a cooperative one costs ~8 us more stream time on each
+    // side of the kernel, which is most of what the fusion saves. Residency
+    // is the occupancy check above (one block per CU, G <= CUs) and the
+    // exchange's bounded spin with rollback covers a block that still does
+    // not become resident.
     ProfScope ps(s->ctx, PROF_UPDATE);
-    le = hipLaunchCooperativeKernel(kern(nv), dim3(G), dim3(kUpdBlock), args, 0, st);
+    le = hipLaunchKernel(kern(nv), dim3(G), dim3(kUpdBlock), args, 0, st);
   }
   if (le != hipSuccess) {
-    (void)hipGetLastError();  // clear the refusal; the launch-per-pass form takes over
+    (void)hipGetLastError();
     s->upd_nv = 0;
     return false;
   }
