@@ -739,6 +739,97 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
   }
 }
 
+// ------------------------------ diagonal-offset SpMV, block RHS (k = 2..8)
+// The same SELL-128/DIA image for k right-hand sides stored row-major
+// (n x k): for a slot column of offset o the x rows of the slice's rows are
+// the contiguous block x[128 s + o, +128) x k. A lane owns CPL consecutive
+// columns (16 bytes) of one row per row group; a wave covers 64 / (k / CPL)
+// rows per group, so one x load per slot column is a contiguous 1 KB run
+// (for k = 8: 16 rows x 64 B), and the value of the row is one 8-byte load
+// (shared by the k / CPL lanes of the row). Each (row, column) is summed from
+// 0 over the slot columns in ascending offset order, holes skipped: bitwise
+// csr_matvecs. The epilogue is the lane-group kernel's row<CPL>.
+template <typename V, typename MV, int CPL, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__restrict__ sptr,
+                                                              const int *__restrict__ swidth,
+                                                              const int *__restrict__ doff,
+                                                              const uint64_t *__restrict__ dmask,
+                                                              const MV *__restrict__ val, int64_t nslices, int64_t n,
+                                                              int k, Src src, Epi epi, double *__restrict__ part,
+                                                              const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock * CPL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int lpr = k / CPL;         // lanes per row
+  const int rpg = 64 / lpr;        // rows per group
+  const int rl0 = lane / lpr, c0 = (lane % lpr) * CPL;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  const auto bs = src.template bind<CPL>(c0);
+  double dacc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t cb = base / kDiaSlice;
+    const int *mo = doff + cb;  // wave-uniform: scalar loads
+    const uint64_t *mk = dmask + 2 * cb;
+    for (int rl = rl0; rl < kDiaSlice; rl += rpg) {
+      const int64_t row = s * kDiaSlice + rl;
+      const int q = rl & 1;             // mask word of this row
+      const uint64_t bit = uint64_t(1) << (rl >> 1);
+      const MV *cv = val + base + rl;
+      V acc[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[c] = V(0);
+      for (int j0 = 0; j0 < w; j0 += UNR) {
+        int off[UNR];
+        uint64_t m0[UNR], m1[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          off[u] = mo[j0 + u];
+          m0[u] = mk[2 * (j0 + u)];
+          m1[u] = mk[2 * (j0 + u) + 1];
+        }
+        V a[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) a[u] = j0 + u < w ? (V)cv[(int64_t)(j0 + u) * kDiaSlice] : V(0);
+        bool on[UNR];
+        V xv[UNR][CPL];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          on[u] = j0 + u < w && ((q ? m1[u] : m0[u]) & bit) != 0;
+          bs.row(on[u] ? row + off[u] : 0, xv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const V p = a[u] * xv[u][c];
+            const V t = acc[c] + p;
+            acc[c] = on[u] ? t : acc[c];
+          }
+      }
+      if (row < n) {
+        V xi[CPL];
+        bs.row(row, xi);
+        epi.template row<CPL>(row, c0, acc, xi, dacc);
+      }
+    }
+  }
+  if (part != nullptr) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];  // slot tid * CPL + c holds column (c0 + c)
+    block_tree_reduce(red, kBlock * CPL, k);
+    if (tid < k) part[(int64_t)g * k + tid] = red[tid];
+  }
+}
+
 // ---------------------------------------------------- elementwise passes
 // Op(e, N, acc) handles the W = 16/sizeof(V) consecutive elements at flat
 // index e (a multiple of W) and adds its dot terms to acc[0..W). Each block
@@ -1187,6 +1278,16 @@ int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const C
   return launch_sell_img<V, MV, I, KT, UNR, false>(A, k, src, epi, part, ctrl, step, st);
 }
 
+// KRY_SPMV_DIA_BLK=0: block right-hand sides on the lane-group SELL kernel
+// instead of the diagonal-offset image (A/B and tests)
+inline bool dia_blk_off() {
+  static const bool off = [] {
+    const char *e = getenv("KRY_SPMV_DIA_BLK");
+    return e && atoi(e) == 0;
+  }();
+  return off;
+}
+
 // y-side epilogue Epi / x-side source Src composition of one SpMV launch;
 // returns the number of block partials written to `part` (if non-null).
 template <typename V, typename MV, typename I, class Src, class Epi>
@@ -1205,6 +1306,21 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
       };
       if (A->dia_max_width <= 8) go(spmv_dia_kernel<V, MV, 8, Src, Epi>);
       else go(spmv_dia_kernel<V, MV, 16, Src, Epi>);
+      KRY_HIP(hipGetLastError());
+      if (grid_out) *grid_out = grid;
+      return;
+    }
+    constexpr int CPLB = 16 / (int)sizeof(V);  // columns per lane of the block DIA kernel
+    if (k >= CPLB && k <= 8 && A->dia && !dia_blk_off()) {
+      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->dia_nslices + 3) / 4));
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->dia_sptr),
+                           static_cast<const int *>(A->dia_width), static_cast<const int *>(A->dia_off),
+                           static_cast<const uint64_t *>(A->dia_mask), static_cast<const MV *>(A->dia_val),
+                           A->dia_nslices, A->n, k, src, epi, part, ctrl, step);
+      };
+      if (A->dia_max_width <= 8) go(spmv_dia_blk_kernel<V, MV, CPLB, 8, Src, Epi>);
+      else go(spmv_dia_blk_kernel<V, MV, CPLB, 16, Src, Epi>);
       KRY_HIP(hipGetLastError());
       if (grid_out) *grid_out = grid;
       return;
