@@ -674,6 +674,21 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
   const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
   const auto bs = src.template bind<1>(0);
   double dacc = 0.0;
+  // The epilogue (result store, dot term) of slice s - 1 runs after slice s's
+  // first round of loads is issued: on gfx9's in-order vmcnt a wait on those
+  // loads then never waits for the store's acknowledgement
+  // (tools/dia_bench "deferred store": -3.5 % on the metric SpMV).
+  V pend[2] = {V(0), V(0)};
+  int64_t prow = -1;
+  auto flush = [&]() {
+    if (prow + 1 < n) {
+      V xi[2];
+      bs.pair(prow, xi);
+      dacc += epi.rows2(prow, pend, xi);
+    } else if (prow < n) {
+      dacc += epi(prow, 0, pend[0], bs(prow, 0));
+    }
+  };
   for (int64_t s = s_begin; s < s_end; ++s) {
     const int w = swidth[s];
     const int64_t base = sptr[s];
@@ -713,6 +728,11 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
         on1[u] = j0 + u < w && ((md[u] >> lane) & 1u) != 0;
         bs.pair((on0[u] || on1[u]) ? row + off[u] : 0, xv[u]);
       }
+      if (j0 == 0 && prow >= 0) {  // the previous slice's epilogue, behind this round's loads
+        __builtin_amdgcn_sched_barrier(0);
+        flush();
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const V p0 = (V)a[u][0] * xv[u][0];
@@ -723,15 +743,12 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
         acc1 = on1[u] ? t1 : acc1;
       }
     }
-    if (row + 1 < n) {
-      const V sv[2] = {acc0, acc1};
-      V xi[2];
-      bs.pair(row, xi);
-      dacc += epi.rows2(row, sv, xi);
-    } else if (row < n) {
-      dacc += epi(row, 0, acc0, bs(row, 0));
-    }
+    if (w == 0 && prow >= 0) flush();
+    pend[0] = acc0;
+    pend[1] = acc1;
+    prow = row;
   }
+  if (prow >= 0) flush();
   if (part != nullptr) {
     red[tid] = dacc;
     block_tree_reduce(red, kBlock, 1);

@@ -176,6 +176,84 @@ __global__ __launch_bounds__(256) void dia_probe(const int64_t *__restrict__ spt
   if (tid == 0) part[g] = red[0];
 }
 
+// Deferred store: slice s's result is stored after slice s + 1's loads have
+// been issued (sched_barrier keeps the order), so a wait on those loads never
+// waits for the store's acknowledgement. One round of UNR >= width.
+template <int UNR>
+__global__ __launch_bounds__(256) void dia_defer(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                 const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                 const double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ part) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  double dacc = 0.0;
+  double pend[2] = {0.0, 0.0};
+  int64_t prow = -1;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * 128 + 2 * lane;
+    const int64_t c0 = base / 128;
+    const double *cv = val + base + 2 * lane;
+    int off[UNR];
+    uint64_t me[UNR], md[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      off[u] = doff[c0 + u];
+      me[u] = dmask[2 * (c0 + u)];
+      md[u] = dmask[2 * (c0 + u) + 1];
+    }
+    double a[UNR][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (u < w) pload_nt<double>(cv + (int64_t)u * 128, a[u]);
+      else a[u][0] = a[u][1] = 0.0;
+    }
+    bool on0[UNR], on1[UNR];
+    double xv[UNR][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      on0[u] = u < w && ((me[u] >> lane) & 1u) != 0;
+      on1[u] = u < w && ((md[u] >> lane) & 1u) != 0;
+      pload<double>(x + ((on0[u] || on1[u]) ? row + off[u] : 0), xv[u]);
+    }
+    double xr[2];
+    pload<double>(x + (row < n ? row : 0), xr);
+    __builtin_amdgcn_sched_barrier(0);
+    if (prow >= 0) {
+      if (prow + 1 < n) pstore<double, true>(y + prow, pend);
+      else if (prow < n) y[prow] = pend[0];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const double p0 = a[u][0] * xv[u][0], p1 = a[u][1] * xv[u][1];
+      const double t0 = acc0 + p0, t1 = acc1 + p1;
+      acc0 = on0[u] ? t0 : acc0;
+      acc1 = on1[u] ? t1 : acc1;
+    }
+    if (row + 1 < n) dacc += xr[0] * acc0 + xr[1] * acc1;
+    else if (row < n) dacc += xr[0] * acc0;
+    pend[0] = acc0;
+    pend[1] = acc1;
+    prow = row;
+  }
+  if (prow >= 0) {
+    if (prow + 1 < n) pstore<double, true>(y + prow, pend);
+    else if (prow < n) y[prow] = pend[0];
+  }
+  red[tid] = dacc;
+  block_tree_reduce(red, 256, 1);
+  if (tid == 0) part[g] = red[0];
+}
+
 int main(int argc, char **argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 216;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -285,6 +363,16 @@ int main(int argc, char **argv) {
   PROBE(8, 0, "probe: UNR 8", true);
   PROBE(16, 16, "probe: interleaved slices", true);
   PROBE(16, 32, "probe: plain (not nt) store", true);
+  for (int gr : {grid, 4096, 16384 < kMaxGrid ? 16384 : kMaxGrid}) {
+    char nm[80];
+    snprintf(nm, sizeof nm, "probe: deferred store, grid %d", gr);
+    timeit(nm, [&] {
+      hipLaunchKernelGGL(dia_defer<16>, dim3(gr), dim3(256), 0, st, (const int64_t *)A->dia_sptr,
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);
+    });
+    check(nm);
+  }
   KC(kry_vec_destroy(xv));
   KC(kry_vec_destroy(yv));
   KC(kry_vec_destroy(yrefv));

@@ -40,7 +40,7 @@ def scan(asm):
 
 def main(srcs):
     bad = 0
-    for src in srcs:
+    for src in map(os.path.abspath, srcs):
         with tempfile.NamedTemporaryFile(suffix=".s") as f:
             subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                                    "-ffp-contract=off", "--cuda-device-only", "-S", src, "-o", f.name],
