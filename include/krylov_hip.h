@@ -232,6 +232,14 @@ int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double 
 int kry_minres_set_criterion(kry_minres *s, const double *criterion);
 int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done,
                    double *resnorms, int32_t *invariant);
+/* Whether the last kry_minres_run chunk ran the one-launch step tail (alpha,
+ * Lanczos orthogonalisation, QR update and the z / W / yk / p update in one
+ * launch after the SpMV: one RHS, no M / Ml / Mr, float64 vectors): info[0];
+ * info[1] = chunks whose remaining steps were rerun with the separate kernels
+ * after its exchange timed out (it writes nothing before the exchange
+ * completes). KRY_MR_UPD=0 disables it; KRY_MRU_FAULT=t drops the last block
+ * out at step t of a chunk (tests). */
+int kry_minres_update_path(kry_minres *s, int32_t *info);
 int kry_minres_residual(kry_minres *s, double *resnorm);
 /* get: which = 0: xk; 1: the current Lanczos vector p; 2: v = M p; 3: the last
  * step's [h0, h1, h2] (3 x k; ArnoldiLanczos state, arnoldi.py:203-281). */

@@ -71,6 +71,7 @@ _SIGNATURES = {
     "kry_cg_preferred_chunk": [_vp, _ip32],
     "kry_cg_path": [_vp, _ip32],
     "kry_cg_update_path": [_vp, _ip32],
+    "kry_minres_update_path": [_vp, _ip32],
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
     "kry_cg_scalars": [_vp, _dp],

@@ -50,6 +50,13 @@ struct kry_minres {
   int wflip = 0;
   bool invariant = false;
   bool started = false;
+  // one-launch update (mr_upd_kernel): upd_nv = -1 undecided, 0 not used,
+  // else granules per thread; its abort word and granule region
+  int upd_nv = -1;
+  unsigned *upd_words = nullptr;
+  int upd_fallbacks = 0;
+  bool upd_used = false;
+  bool upd_last = false;
 };
 
 namespace {
@@ -255,6 +262,204 @@ __global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int
   }
 }
 
+// ------------------------------ one-launch MINRES step tail (large n, k = 1)
+// Replaces mr_alpha_kernel, the Lanczos ortho pass, mr_qr_kernel and the
+// update pass of a step for one right-hand side without preconditioners
+// (float64 vectors, Euclidean or weighted inner), at one 512-thread block per
+// CU, all resident, with the same arithmetic:
+//   alpha = <v, w> (every block sums the SpMV's partials in one fixed order)
+//   w' = w - alpha p kept in registers, <w', w'>_W block partial
+//   all-gather -> h2 = sqrt(<w', w'>); every block then runs the scalar
+//   recurrence of mr_qr_kernel (old rotations, lartg, y) from the same
+//   values, so the update needs no second exchange
+//   z = (v - R0 W0 - R1 W1) / guard(R2) into W0's buffer, yk += y0 z,
+//   p_new = w' / guard(h2)
+// so a step streams w, p, [weights,] v (= p), W0, W1, yk in and z, yk, p_new
+// out in one launch instead of four. Nothing is stored before the exchange has
+// completed: a timed-out exchange leaves the step's state untouched, halts
+// the chunk at this step, and kry_minres_run reruns the rest with the
+// separate kernels. Block 0 writes the scalar slots and the history.
+constexpr int kMrBlock = 512;
+constexpr int kMrU = 2;
+constexpr size_t kMrWords = 16 + 2 * 2 * 256 * 2;
+template <bool WT, int NV>
+__global__ __launch_bounds__(kMrBlock) void mr_upd_kernel(int64_t N, const double *__restrict__ w,
+                                                          const double *__restrict__ p, const double *__restrict__ wt,
+                                                          double *__restrict__ W0z, const double *__restrict__ W1,
+                                                          double *__restrict__ yk, double *__restrict__ pnew,
+                                                          const double *__restrict__ partA, int PA, double *scal,
+                                                          int have_g0, int have_g1, double *hist, Ctrl *ctrl, int step,
+                                                          double *gbuf, int col_offset, int total_k, unsigned *words,
+                                                          int fault_step) {
+  using V = double;
+  if (halted(ctrl, step)) return;
+  constexpr int W = 2;
+  constexpr int U = kMrU;
+  constexpr int NC = NV / U;
+  static_assert(NV % U == 0, "chunks must tile the thread's granules");
+  __shared__ double red[kMrBlock];
+  __shared__ double shv[2];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_MRU_FAULT)
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  const int64_t seg = (int64_t)NV * kMrBlock * W;
+  const int64_t e0 = (int64_t)blockIdx.x * seg;
+  using Seg = BufSeg<V, kMrBlock>;
+  const Seg sw(w, e0, N, seg), sp(p, e0, N, seg), swt(WT ? wt : p, e0, N, seg), sW0(W0z, e0, N, seg),
+      sW1(W1, e0, N, seg), sy(yk, e0, N, seg), spn(pnew, e0, N, seg);
+  // phase A buffers: w, p, weights; phase B: v (= p), W0, W1, yk
+  V c1[2][U][W], c2[2][U][W], c3[2][U][W], c4[2][U][W];
+  auto ldA = [&](int c, int b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      sw.template load<W, 2>(c * U + u, c1[b][u]);
+      sp.template load<W>(c * U + u, c2[b][u]);
+      if (WT) swt.template load<W>(c * U + u, c3[b][u]);
+    }
+  };
+  auto ldB = [&](int c, int b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      sp.template load<W>(c * U + u, c1[b][u]);
+      sW0.template load<W, 2>(c * U + u, c2[b][u]);
+      sW1.template load<W, 2>(c * U + u, c3[b][u]);
+      sy.template load<W, 2>(c * U + u, c4[b][u]);
+    }
+  };
+  ldA(0, 0);
+  // alpha = <v, w> (arnoldi.py:252), h[1] = alpha in the Lanczos dtype
+  reduce_partials<kMrBlock>(partA, PA, 1, red);
+  const double alpha = red[0];
+  // the old scalars, read before this block publishes (block 0 rewrites them
+  // only after every block has published)
+  const double h0 = scal[M_H0], g0c = scal[M_G0C], g0s = scal[M_G0S], g1c = scal[M_G1C], g1s = scal[M_G1S];
+  const double y0o = scal[M_Y0], y1o = scal[M_Y1];
+  // w' = w - alpha p (arnoldi.py:264) and <w', w'>_W
+  V wr[NV][W];
+  double acc = 0.0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int b = c & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NC) ldA(c + 1, b ^ 1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = c * U + u;
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V t = alpha * c2[b][u][v];
+        wr[g][v] = c1[b][u][v] - t;
+        const double d = wr[g][v];
+        acc += WT ? dterm_w(d, c3[b][u][v], d) : dterm(d, d);  // out-of-range elements are 0
+      }
+    }
+  }
+  const double bp = block_sum1_t0(acc, red);
+  unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16) + (size_t)(step & 1) * 2 * 256;
+  const unsigned tag = (unsigned)step + 1u;
+  if (tid == 0) publish_partial(gran + 2 * blockIdx.x, tag, bp);
+  ldB(0, 0);  // phase B's first chunk travels during the exchange
+  if (tid < 64) {
+    bool ok = sweep_partials(gran, G, tag, words, ctrl, &shv[0], spin_limit);
+    if (ok && __hip_atomic_load(words + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) ok = false;
+    if (tid == 0) flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  if (!__builtin_amdgcn_readfirstlane(flag)) {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+    return;
+  }
+  // mr_qr_kernel's scalar recurrence (minres.py:193-228), same in every block
+  const V h2 = (V)sqrt(shv[0]);
+  const bool inv = h2 <= 1.0e-14;  // np.all(h[2] <= 1e-14)
+  const V hsafe = h2 != V(0) ? h2 : V(1);
+  double R0 = 0.0, R1 = h0, R2, R3;
+  if (have_g1) {
+    const double a0 = g1c * R0, a1 = g1s * R1, b0 = -g1s * R0, b1 = g1c * R1;
+    R0 = a0 + a1;
+    R1 = b0 + b1;
+  }
+  R2 = (double)(V)alpha;
+  R3 = (double)h2;
+  if (have_g0) {
+    const double a0 = g0c * R1, a1 = g0s * R2, b0 = -g0s * R1, b1 = g0c * R2;
+    R1 = a0 + a1;
+    R2 = b0 + b1;
+  }
+  double cs, sn, rr;
+  lartg<double>(R2, R3, cs, sn, rr);
+  R2 = rr;
+  const double a0 = cs * y0o, a1 = sn * y1o, b0 = -sn * y0o, b1 = cs * y1o;
+  const double ny0 = a0 + a1, ny1 = b0 + b1;
+  const double z2 = R2 != 0.0 ? R2 : 1.0;
+  // z = (v - R0 W0 - R1 W1) / R2 (minres.py:219), yk += y0 z (221), p_new = w' / guard(h2) (arnoldi.py:274-277)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int b = c & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NC) ldB(c + 1, b ^ 1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = c * U + u;
+      V zv[W], yv[W], pv[W];
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const double t0 = R0 * c2[b][u][v];
+        const double t1 = R1 * c3[b][u][v];
+        const double z = ((c1[b][u][v] - t0) - t1) / z2;
+        zv[v] = z;
+        const double dy = ny0 * z;
+        yv[v] = c4[b][u][v] + dy;
+        pv[v] = wr[g][v] / hsafe;
+      }
+      sW0.template store<W, 2>(g, zv);
+      sy.template store<W, 2>(g, yv);
+      spn.template store<W>(g, pv);
+    }
+  }
+  if (blockIdx.x == 0) {
+    if (tid == 0) {
+      scal[M_ALPHA] = alpha;
+      scal[M_H1] = (double)(V)alpha;
+      scal[M_H2] = (double)h2;
+      scal[M_HSAFE] = (double)hsafe;
+      if (have_g0) {
+        scal[M_G1C] = g0c;
+        scal[M_G1S] = g0s;
+      }
+      scal[M_G0C] = cs;
+      scal[M_G0S] = sn;
+      scal[M_Z0] = R0;
+      scal[M_Z1] = R1;
+      scal[M_Z2] = z2;
+      scal[M_ZY] = ny0;
+      scal[M_Y0] = ny1;
+      scal[M_Y1] = 0.0;
+      scal[M_H0] = (double)h2;
+      red[0] = fabs(ny1);
+      if (!gbuf) hist[step] = red[0];
+    }
+    __syncthreads();
+    if (gbuf) {
+      for (int t = tid; t < total_k; t += kMrBlock) gbuf[t] = t == col_offset ? red[0] : 0.0;
+      if (tid == 0) gbuf[total_k] = inv ? 0.0 : 1.0;
+    } else {
+      const bool conv = all_le(red, scal + M_CRIT, 1, &flag);
+      if (tid == 0) {
+        if (inv) ctrl->invariant = 1;
+        if (inv || conv) ctrl->stop_at = step + 1;
+      }
+    }
+  }
+}
+
+template <bool WT, int NV>
+void *mru_kern() {
+  return reinterpret_cast<void *>(mr_upd_kernel<WT, NV>);
+}
+
 // Sharded global step decision (Lanczos invariance over all columns,
 // arnoldi.py:270-272; stop rule over all columns, minres.py:162).
 __global__ void mr_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
@@ -349,6 +554,74 @@ void mr_start_impl(kry_minres *s) {
                           nullptr, nullptr, 0, st);
 }
 
+// One launch for the step tail (mr_upd_kernel) if eligible: one RHS, no
+// preconditioners, float64 vectors, at most 512 * 40 granules per block at
+// one block per CU (decided once per solver; KRY_MR_UPD=0 disables).
+inline bool mru_launch(kry_minres *s, const double *w, const double *p, double *W0z, const double *W1, double *pnew,
+                       const double *partA, int PA, int step, int64_t i) {
+  const int64_t N = s->n;
+  auto kern = [&](bool wt, int nv) -> void * {
+    switch (nv) {
+      case 8: return wt ? mru_kern<true, 8>() : mru_kern<false, 8>();
+      case 16: return wt ? mru_kern<true, 16>() : mru_kern<false, 16>();
+      case 24: return wt ? mru_kern<true, 24>() : mru_kern<false, 24>();
+      case 32: return wt ? mru_kern<true, 32>() : mru_kern<false, 32>();
+      default: return wt ? mru_kern<true, 40>() : mru_kern<false, 40>();
+    }
+  };
+  const bool wt = s->w != nullptr;
+  if (s->upd_nv < 0) {
+    s->upd_nv = 0;
+    const char *e = getenv("KRY_MR_UPD");
+    if (!(e && atoi(e) == 0) && s->k == 1 && !s->M && !s->Ml && !s->Mr && s->dtype == KRY_F64) {
+      int dev = 0, ncu = 0;
+      KRY_HIP(hipGetDevice(&dev));
+      KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      const int gmax = ncu < 256 ? ncu : 256;
+      for (int nv : {8, 16, 24, 32, 40}) {
+        const int64_t G = (N + (int64_t)kMrBlock * nv * 2 - 1) / ((int64_t)kMrBlock * nv * 2);
+        if (G > gmax) continue;
+        int per_cu = 0;
+        KRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern(wt, nv)),
+                                                             kMrBlock, 0));
+        if (per_cu >= 1) s->upd_nv = nv;
+        break;
+      }
+      if (s->upd_nv > 0) s->upd_words = static_cast<unsigned *>(dev_alloc(kMrWords * 4));
+    }
+  }
+  if (s->upd_nv == 0) return false;
+  const int nv = s->upd_nv;
+  const int G = (int)((N + (int64_t)kMrBlock * nv * 2 - 1) / ((int64_t)kMrBlock * nv * 2));
+  hipStream_t st = s->ctx->stream;
+  if (step == 0) KRY_HIP(hipMemsetAsync(s->upd_words, 0, kMrWords * 4, st));
+  const char *fe = getenv("KRY_MRU_FAULT");  // fault injection (tests): step at which a block drops out
+  int fault_step = fe ? atoi(fe) : -1;
+  int64_t n = N;
+  const double *wtp = s->w;
+  double *yk = static_cast<double *>(s->yk), *scal = s->scal, *hist = s->hist;
+  int have_g0 = i >= 1 ? 1 : 0, have_g1 = i >= 2 ? 1 : 0;
+  Ctrl *ctrl = s->ctrl;
+  double *gbuf = s->comm ? s->gbuf : nullptr;
+  int col_offset = s->col_offset, total_k = s->total_k;
+  unsigned *words = s->upd_words;
+  void *args[] = {&n,       &w,   &p,       &wtp,        &W0z,     &W1,    &yk,    &pnew,  &partA, &PA,
+                  &scal,    &have_g0, &have_g1, &hist,  &ctrl,   &step,   &gbuf, &col_offset, &total_k,
+                  &words,   &fault_step};
+  hipError_t le;
+  {
+    ProfScope ps(s->ctx, PROF_UPDATE);
+    le = hipLaunchKernel(kern(wt, nv), dim3(G), dim3(kMrBlock), args, 0, st);
+  }
+  if (le != hipSuccess) {
+    (void)hipGetLastError();
+    s->upd_nv = 0;
+    return false;
+  }
+  s->upd_used = true;
+  return true;
+}
+
 template <typename V, typename S, typename MV, typename I>
 void mr_run_typed(kry_minres *s, int max_steps) {
   hipStream_t st = s->ctx->stream;
@@ -367,6 +640,19 @@ void mr_run_typed(kry_minres *s, int max_steps) {
       ProfScope ps(s->ctx, PROF_SPMV);
       mr_apply_op<V, MV, I>(s, v, EpiLanczos<V>{w, v, pold, s->scal + M_H0 * k, s->w, k}, partA, &PA, s->ctrl, step);
     }
+    const int f = (s->wflip + step) & 1;
+    if constexpr (std::is_same<V, double>::value) {
+      if (mru_launch(s, w, p, s->W[f], s->W[f ^ 1], pnew, partA, PA, step, i)) {
+        if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
+          ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+          KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+          hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
+                             (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
+          KRY_HIP(hipGetLastError());
+        }
+        continue;
+      }
+    }
     hipLaunchKernelGGL((mr_alpha_kernel<V, S>), dim3(1), dim3(kBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
     PB = launch_elementwise<V>(N, k, OpLanczosOrtho<V, S>{w, p, s->scal + M_ALPHA * k, s->w, k, s->M ? 1 : 0},
                                s->M ? nullptr : partB, s->ctrl, step, st);
@@ -384,7 +670,6 @@ void mr_run_typed(kry_minres *s, int max_steps) {
                          (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
       KRY_HIP(hipGetLastError());
     }
-    const int f = (s->wflip + step) & 1;
     {
       ProfScope ps(s->ctx, PROF_UPDATE);
       launch_elementwise<V>(N, k,
@@ -424,7 +709,7 @@ void mr_residual_impl(kry_minres *s, double *norm2) {
 void mr_free(kry_minres *s) {
   void *bufs[] = {s->b,  s->x0,   s->yk,   s->wv,   s->xk,    s->rt,  s->P[0], s->P[1], s->P[2], s->W[0],
                   s->W[1], s->w, s->part, s->scal, s->hist, s->ctrl, s->Vr[0], s->Vr[1], s->mw, s->t1, s->t2,
-                  s->gbuf, s->gcrit};
+                  s->gbuf, s->gcrit, s->upd_words};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -591,15 +876,44 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
     s->hist = static_cast<double *>(dev_alloc((size_t)max_steps * (s->comm ? s->total_k : s->k) * 8));
     s->chunk_cap = max_steps;
   }
-  reset_ctrl(s->ctrl, st);
-  dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, max_steps); });
+  const int hk = s->comm ? s->total_k : s->k;
+  auto run_steps = [&](int steps, double *rows, Ctrl *c) {
+    reset_ctrl(s->ctrl, st);
+    s->upd_used = false;
+    dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { mr_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, steps); });
+    return read_chunk(s->ctx, st, s->ctrl, s->hist, steps, hk, rows, c);
+  };
   Ctrl c;
-  const int done = read_chunk(s->ctx, st, s->ctrl, s->hist, max_steps, s->comm ? s->total_k : s->k, resnorms, &c);
+  int done = run_steps(max_steps, resnorms, &c);
+  const bool upd = s->upd_used;
+  if (upd && c.status == KRY_EDEVICE) {
+    // the one-launch step tail timed out at step `done` and wrote nothing:
+    // keep the steps before it and rerun the rest with the separate kernels,
+    // from that step's SpMV (its inputs are unchanged)
+    s->it += done;
+    s->wflip = (s->wflip + done) & 1;
+    s->upd_nv = 0;
+    ++s->upd_fallbacks;
+    const int more = run_steps(max_steps - done, resnorms + (size_t)done * hk, &c);
+    s->it -= done;
+    s->wflip = (s->wflip + 2 - (done & 1)) & 1;
+    done += more;
+  }
+  KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "MINRES: device error status " + std::to_string(c.status));
+  s->upd_last = upd;
   s->it += done;
   s->wflip = (s->wflip + done) & 1;
   s->invariant = c.invariant != 0;
   *steps_done = done;
   *invariant = s->invariant ? 1 : 0;
+  KRY_API_END
+}
+
+int kry_minres_update_path(kry_minres *s, int32_t *info) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
+  info[0] = s->upd_last ? 1 : 0;
+  info[1] = s->upd_fallbacks;
   KRY_API_END
 }
 

@@ -42,6 +42,13 @@ class _MinresState:
         check(lib.kry_minres_run(self.h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
         return out[: done.value], bool(inv.value)
 
+    def update_path(self):
+        """(one_launch_tail, fallbacks) of the last run chunk
+        (kry_minres_update_path)."""
+        info = (ctypes.c_int32 * 2)()
+        check(lib.kry_minres_update_path(self.h, info))
+        return bool(info[0]), int(info[1])
+
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)
         check(lib.kry_minres_residual(self.h, _lib.dptr(out)))
