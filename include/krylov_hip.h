@@ -81,6 +81,14 @@ int kry_csr_destroy(kry_csr *A);
  * kernel walks in CSR form instead. */
 int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
                    int64_t *nslots, int64_t *nirregular);
+/* Host-only: the diagonal-offset (SELL-128/DIA) plan kry_csr_create would
+ * build for these CSR arrays (no device needed). info[0..3] = built (0/1),
+ * slices, slots, widest slice; when built and the arrays are non-null:
+ * widths[slices], offsets[slots / 128] (each slice's sorted offsets col - row),
+ * masks[2 * slots / 128] (word q, bit l: row 128 s + 2 l + q has an entry at
+ * that offset). Call once with null arrays to size them. */
+int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                 int32_t *widths, int32_t *offsets, uint64_t *masks);
 /* The device image kry_csr_create built: info[0..6] = slices, slots,
  * irregular slices, compact (1 when the column indices are stored as uint16
  * deltas over per-slot-column int32 bases: every slot column spans <= 65534

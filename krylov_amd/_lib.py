@@ -54,6 +54,7 @@ _SIGNATURES = {
     "kry_csr_create": [_vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
     "kry_csr_destroy": [_vp],
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
+    "kry_dia_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
     "kry_csr_info": [_vp, _ip64],
     "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
     "kry_vec_destroy": [_vp],
@@ -163,6 +164,28 @@ def device_count():
     c = _int(0)
     check(lib.kry_device_count(ctypes.byref(c)))
     return c.value
+
+
+def dia_plan(indptr, indices):
+    """Host-only diagonal-offset plan (kry_dia_plan): None if the image would
+    not be built, else {"slices", "slots", "max_width", "widths", "offsets",
+    "masks"}."""
+    indptr = np.ascontiguousarray(indptr)
+    indices = np.ascontiguousarray(indices, dtype=indptr.dtype)
+    n, nnz = indptr.shape[0] - 1, indices.shape[0]
+    info = np.zeros(4, dtype=np.int64)
+    ip64 = info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    check(lib.kry_dia_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, None, None, None))
+    if not info[0]:
+        return None
+    cols = int(info[2]) // 128
+    widths = np.zeros(int(info[1]), dtype=np.int32)
+    offsets = np.zeros(cols, dtype=np.int32)
+    masks = np.zeros(2 * cols, dtype=np.uint64)
+    check(lib.kry_dia_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, ptr(widths),
+                           ptr(offsets), ptr(masks)))
+    return {"slices": int(info[1]), "slots": int(info[2]), "max_width": int(info[3]), "widths": widths,
+            "offsets": offsets, "masks": masks}
 
 
 def csr_layout(indptr):

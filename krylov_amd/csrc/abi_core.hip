@@ -411,6 +411,27 @@ static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t
   return true;
 }
 
+// Host-only view of the diagonal-offset plan (kry_dia_plan): the image
+// kry_csr_create would build for these CSR arrays, without a device.
+template <typename I>
+static void dia_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
+                          int32_t *offsets, uint64_t *masks) {
+  int64_t ns = 0, sell_slots = 0, irr = 0;
+  sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
+  std::vector<double> zeros((size_t)std::max<int64_t>(nnz, 1), 0.0);
+  DiaHost<double> d;
+  const bool built = dia_build(n, ip, ix, zeros.data(), sell_slots, d);
+  info[0] = built ? 1 : 0;
+  info[1] = built ? (int64_t)d.width.size() : 0;
+  info[2] = built ? d.sptr.back() : 0;
+  info[3] = built ? d.max_width : 0;
+  if (!built) return;
+  if (widths) std::copy(d.width.begin(), d.width.end(), widths);
+  const int64_t cols = d.sptr.back() / kDiaSlice;
+  if (offsets) std::copy(d.off.begin(), d.off.begin() + cols, offsets);
+  if (masks) std::copy(d.mask.begin(), d.mask.begin() + 2 * cols, masks);
+}
+
 // Column-blocked image (see kry_csr::cb_*). Returns false when not useful or
 // not possible: rows not sorted, x small enough to stay cache-resident, the
 // columns not scattered (most entries within half a block of the diagonal),
@@ -610,6 +631,21 @@ static void csr_free(kry_csr *A) {
 }
 
 extern "C" {
+
+int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                 int32_t *widths, int32_t *offsets, uint64_t *masks) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
+  if (itype == KRY_I32)
+    dia_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, widths,
+                  offsets, masks);
+  else if (itype == KRY_I64)
+    dia_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
+                  offsets, masks);
+  else
+    throw Error{KRY_EINVAL, "bad itype"};
+  KRY_API_END
+}
 
 int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
                    const void *data, int dtype, int itype, kry_csr **out) {

@@ -7,6 +7,7 @@ import re
 
 import numpy as np
 import pytest
+import scipy.sparse
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -152,3 +153,95 @@ def test_unsupported_inputs_are_rejected_before_any_device_work():
         krylov_amd.gmres(np.eye(3), np.ones((3, 2)), ortho="householder")
     with pytest.raises(ValueError):
         krylov_amd.gmres(np.eye(3), np.ones(3), ortho="cgs")
+
+
+def _dia_plan_py(indptr, indices):
+    """Restatement of the SELL-128/DIA plan (kry_dia_plan): slices of 128
+    rows; each slice's sorted distinct offsets col - row; a row's entries must
+    be strictly increasing (so offset order is stored order); the slice is
+    refused when 128 * width > 2 * nnz_slice + 2048, and the whole image when
+    it holds more than 1.25x the SELL-64 slots plus one slice of padding."""
+    n = indptr.shape[0] - 1
+    if n == 0:
+        return None
+    ns = (n + 127) // 128
+    widths, offs, masks = [], [], []
+    maxw = 0
+    for s in range(ns):
+        r0, r1 = 128 * s, min(n, 128 * s + 128)
+        rows = np.repeat(np.arange(r0, r1), np.diff(indptr[r0:r1 + 1]))
+        cols = indptr.dtype.type(0) + indices[indptr[r0]:indptr[r1]].astype(np.int64)
+        seg = np.split(cols, np.cumsum(np.diff(indptr[r0:r1 + 1]))[:-1])
+        if any(np.any(np.diff(c) <= 0) for c in seg):
+            return None
+        o = np.unique(cols - rows)
+        if 128 * len(o) > 2 * int(indptr[r1] - indptr[r0]) + 2048:
+            return None
+        m = np.zeros((len(o), 2), dtype=np.uint64)
+        for r, c in zip(rows, cols):
+            j = np.searchsorted(o, c - r)
+            rl = r - r0
+            m[j, rl & 1] |= np.uint64(1) << np.uint64(rl >> 1)
+        widths.append(len(o))
+        offs.extend(o.tolist())
+        masks.extend(m.ravel().tolist())
+        maxw = max(maxw, len(o))
+    slots = 128 * sum(widths)
+    sell_slots = _layout_py(indptr)[1]
+    if slots * 4 > sell_slots * 5 + 4 * 128 * maxw:
+        return None
+    return {"slices": ns, "slots": slots, "max_width": maxw, "widths": np.array(widths, dtype=np.int32),
+            "offsets": np.array(offs, dtype=np.int32), "masks": np.array(masks, dtype=np.uint64)}
+
+
+def _banded(n, offsets, seed, drop=0.1):
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    for o in offsets:
+        r = np.arange(max(0, -o), min(n, n - o))
+        keep = rng.random(r.size) >= drop
+        rows.append(r[keep])
+        cols.append(r[keep] + o)
+    A = scipy.sparse.coo_matrix((np.ones(sum(x.size for x in rows)), (np.concatenate(rows), np.concatenate(cols))),
+                                shape=(n, n)).tocsr()
+    A.sort_indices()
+    return A
+
+
+@pytest.mark.parametrize("case", ["poisson2d_61", "stencil15_12", "banded_holes", "ragged_129", "one_row",
+                                  "unsorted", "scattered"])
+def test_dia_plan_matches_restatement(case):
+    """The host side of the diagonal-offset image (offsets, lane masks,
+    widths, and when it is refused) against a NumPy restatement, without a
+    device (kry_dia_plan)."""
+    from krylov_amd import _lib, problems
+
+    if case == "poisson2d_61":
+        A = problems.poisson2d(61)
+    elif case == "stencil15_12":
+        A = problems.stencil15_3d(12)
+    elif case == "banded_holes":
+        A = _banded(3000, [-70, -3, -1, 0, 2, 9, 70], 1, drop=0.2)
+    elif case == "ragged_129":
+        A = _banded(129, [-1, 0, 1], 2, drop=0.0)
+    elif case == "one_row":
+        A = scipy.sparse.csr_matrix(np.array([[2.0]]))
+    elif case == "unsorted":
+        A = problems.poisson2d(20).tocsr()
+        a = A.indptr[37]
+        A.indices[a], A.indices[a + 1] = A.indices[a + 1], A.indices[a]
+    else:
+        A = problems.random_nonsym(4000, seed=3)
+    ip = A.indptr.astype(np.int32)
+    ix = A.indices.astype(np.int32)
+    got = _lib.dia_plan(ip, ix)
+    want = _dia_plan_py(ip, ix)
+    if want is None:
+        assert got is None
+        return
+    assert got is not None
+    for key in ("slices", "slots", "max_width"):
+        assert got[key] == want[key], key
+    for key in ("widths", "offsets", "masks"):
+        np.testing.assert_array_equal(got[key], want[key])
+    assert case not in ("unsorted", "scattered")

@@ -254,6 +254,127 @@ __global__ __launch_bounds__(256) void dia_defer(const int64_t *__restrict__ spt
   if (tid == 0) part[g] = red[0];
 }
 
+// x-run reuse: a slot column whose offset is 1 or 2 above an earlier loaded
+// column's (the base) takes its x pair from the neighbouring lane's base pair
+// (DPP wave_shl:1) instead of a load; lane 63 takes the element(s) past the
+// base run from one extra 16-byte load. src[j] = 0: load; else (j - b) << 2 | d.
+// Base runs are loaded for every lane (address clamped to [-1, n - 1]: a lane
+// that consumes a shifted value has its source in range).
+__device__ __forceinline__ double shl1(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int UNR>
+__global__ __launch_bounds__(256) void dia_reuse(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                 const signed char *__restrict__ dsrc,
+                                                 const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                 const double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ part) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t m = (int64_t)g * 4 + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  double dacc = 0.0;
+  double pend[2] = {0.0, 0.0};
+  int64_t prow = -1;
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * 128 + 2 * lane;
+    const int64_t c0 = base / 128;
+    const double *cv = val + base + 2 * lane;
+    int off[UNR], src[UNR];
+    uint64_t me[UNR], md[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      off[u] = doff[c0 + u];
+      me[u] = dmask[2 * (c0 + u)];
+      md[u] = dmask[2 * (c0 + u) + 1];
+      src[u] = dsrc[c0 + u];
+    }
+    double a[UNR][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (u < w) pload_nt<double>(cv + (int64_t)u * 128, a[u]);
+      else a[u][0] = a[u][1] = 0.0;
+    }
+    bool on0[UNR], on1[UNR];
+    double xv[UNR][2];
+    double ex[UNR][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      on0[u] = u < w && ((me[u] >> lane) & 1u) != 0;
+      on1[u] = u < w && ((md[u] >> lane) & 1u) != 0;
+      if (u < w && src[u] == 0) {
+        int64_t ix = row + off[u];
+        ix = ix < -1 ? -1 : (ix > n - 1 ? n - 1 : ix);
+        pload<double>(x + ix, xv[u]);
+        int64_t ie = s * 128 + 128 + off[u];  // the pair past the run (lane 63's shifted source)
+        ie = ie < -1 ? -1 : (ie > n - 1 ? n - 1 : ie);
+        pload<double>(x + ie, ex[u]);
+      } else {
+        xv[u][0] = xv[u][1] = 0.0;
+        ex[u][0] = ex[u][1] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (u < w && src[u] != 0) {
+        const int b = u - (src[u] >> 2), d = src[u] & 3;
+#pragma unroll
+        for (int bb = 0; bb < UNR; ++bb)
+          if (bb == b) {
+            const double s0 = shl1(xv[bb][0]);
+            if (d == 2) {
+              const double s1 = shl1(xv[bb][1]);
+              xv[u][0] = lane < 63 ? s0 : ex[bb][0];
+              xv[u][1] = lane < 63 ? s1 : ex[bb][1];
+            } else {
+              xv[u][0] = xv[bb][1];
+              xv[u][1] = lane < 63 ? s0 : ex[bb][0];
+            }
+          }
+      }
+    }
+    double xr[2];
+    pload<double>(x + (row < n ? row : 0), xr);
+    __builtin_amdgcn_sched_barrier(0);
+    if (prow >= 0) {
+      if (prow + 1 < n) pstore<double, true>(y + prow, pend);
+      else if (prow < n) y[prow] = pend[0];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const double p0 = a[u][0] * xv[u][0], p1 = a[u][1] * xv[u][1];
+      const double t0 = acc0 + p0, t1 = acc1 + p1;
+      acc0 = on0[u] ? t0 : acc0;
+      acc1 = on1[u] ? t1 : acc1;
+    }
+    if (row + 1 < n) dacc += xr[0] * acc0 + xr[1] * acc1;
+    else if (row < n) dacc += xr[0] * acc0;
+    pend[0] = acc0;
+    pend[1] = acc1;
+    prow = row;
+  }
+  if (prow >= 0) {
+    if (prow + 1 < n) pstore<double, true>(y + prow, pend);
+    else if (prow < n) y[prow] = pend[0];
+  }
+  red[tid] = dacc;
+  block_tree_reduce(red, 256, 1);
+  if (tid == 0) part[g] = red[0];
+}
+
+__global__ void dpp_direction(int *o) { o[threadIdx.x] = __builtin_amdgcn_update_dpp(-7, (int)threadIdx.x, 0x130, 0xf, 0xf, false); }
+
 int main(int argc, char **argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 216;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -372,6 +493,56 @@ int main(int argc, char **argv) {
                          (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);
     });
     check(nm);
+  }
+  {
+    int *od;
+    CK(hipMalloc(&od, 64 * 4));
+    hipLaunchKernelGGL(dpp_direction, dim3(1), dim3(64), 0, st, od);
+    int oh[64];
+    CK(hipMemcpy(oh, od, 256, hipMemcpyDeviceToHost));
+    printf("dpp wave_shl:1 -> lane 0 gets %d, lane 62 gets %d, lane 63 gets %d\n", oh[0], oh[62], oh[63]);
+    CK(hipFree(od));
+    // x-run reuse codes from the image's offsets
+    const int64_t cols = A->dia_nslots / 128;
+    std::vector<int> offh(cols), wh(A->dia_nslices);
+    std::vector<int64_t> sp(A->dia_nslices + 1);
+    CK(hipMemcpy(offh.data(), A->dia_off, cols * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(wh.data(), A->dia_width, wh.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sp.data(), A->dia_sptr, sp.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<signed char> srch(cols + 64, 0);
+    int64_t derived = 0;
+    for (int64_t s = 0; s < A->dia_nslices; ++s) {
+      const int64_t c0 = sp[s] / 128;
+      int lastb = -1;
+      for (int j = 0; j < wh[s]; ++j) {
+        const int o = offh[c0 + j];
+        if (lastb >= 0 && o - offh[c0 + lastb] >= 1 && o - offh[c0 + lastb] <= 2 && j - lastb < 32) {
+          srch[c0 + j] = (signed char)(((j - lastb) << 2) | (o - offh[c0 + lastb]));
+          ++derived;
+        } else {
+          lastb = j;
+        }
+      }
+    }
+    printf("x-run reuse: %ld of %ld slot columns derived\n", (long)derived, (long)cols);
+    signed char *srcd;
+    CK(hipMalloc(&srcd, srch.size()));
+    CK(hipMemcpy(srcd, srch.data(), srch.size(), hipMemcpyHostToDevice));
+    for (int rep = 0; rep < 2; ++rep) {
+      timeit("probe: deferred store + x-run reuse", [&] {
+        hipLaunchKernelGGL(dia_reuse<16>, dim3(grid), dim3(256), 0, st, (const int64_t *)A->dia_sptr,
+                           (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,
+                           (const signed char *)srcd, (const double *)A->dia_val, A->dia_nslices, n,
+                           (const double *)x, y, part);
+      });
+      check("probe: deferred store + x-run reuse");
+      timeit("probe: deferred store", [&] {
+        hipLaunchKernelGGL(dia_defer<16>, dim3(grid), dim3(256), 0, st, (const int64_t *)A->dia_sptr,
+                           (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,
+                           (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);
+      });
+    }
+    CK(hipFree(srcd));
   }
   KC(kry_vec_destroy(xv));
   KC(kry_vec_destroy(yv));
