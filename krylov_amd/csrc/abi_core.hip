@@ -775,7 +775,7 @@ int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out) {
   KRY_HIP(hipSetDevice(ctx->device));
   const int k = x->k;
   const int64_t N = x->n * (int64_t)k;
-  double *part = ctx_scratch(ctx, (kMaxGrid + 1) * (size_t)k * 8);
+  double *part = ctx_scratch(ctx, (part_rows(k) + 1) * (size_t)k * 8);
   {
     int P;
     const double *wd = w ? static_cast<const double *>(w->d) : nullptr;
@@ -785,7 +785,7 @@ int kry_dot(kry_ctx *ctx, kry_vec *x, kry_vec *y, kry_vec *w, double *out) {
     else
       P = launch_elementwise<float>(N, k, OpDot<float>{static_cast<const float *>(x->d), static_cast<const float *>(y->d), wd, k},
                                     part, nullptr, 0, ctx->stream);
-    double *res = part + (size_t)kMaxGrid * k;
+    double *res = part + part_rows(k) * k;
     hipLaunchKernelGGL(reduce_to_kernel<0>, dim3(1), dim3(kBlock), 0, ctx->stream, part, P, k, res);
     KRY_HIP(hipGetLastError());
     KRY_HIP(hipMemcpyAsync(out, res, k * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -41,7 +41,7 @@ struct kry_cg {
   void *z = nullptr;                    // M Ml_r (with M)
   void *t = nullptr;                    // A p / scratch (with Ml)
   double *w = nullptr;
-  double *part = nullptr;  // 2 * kMaxGrid * k
+  double *part = nullptr;  // 2 * part_rows(k) * k
   double *scal = nullptr;  // scalar slots, see S_* below
   double *hist = nullptr;  // chunk_cap * hist_k
   Ctrl *ctrl = nullptr;
@@ -177,7 +177,7 @@ __global__ void cg_start_finalize(const double *part, int P, int k, double *scal
 }
 
 // alpha = rhos[-1] / np.where(pAp != 0, pAp, 1.0)  (cg.py:183-185)
-// 1024 threads: the SpMV's partials (up to 8192 blocks x k) in 32-load rounds
+// 1024 threads: the SpMV's partials (up to part_rows(k) blocks x k) in 32-load rounds
 constexpr int kAlphaBlock = 1024;
 template <typename S>
 __global__ __launch_bounds__(kAlphaBlock) void cg_alpha_kernel(const double *part, int P, int k, double *scal,
@@ -981,7 +981,7 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   if (cgp_launch<V, MV, I>(s, max_steps)) return true;
-  double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
+  double *partA = s->part, *partB = s->part + part_rows(k) * k;
   for (int step = 0; step < max_steps; ++step) {
     V *p = static_cast<V *>(s->p);
     int PA, PB;
@@ -1132,7 +1132,7 @@ int kry_cg_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_cg **out) 
       *v = dev_alloc(vb);
       KRY_HIP(hipMemsetAsync(*v, 0, vb, ctx->stream));
     }
-    s->part = static_cast<double *>(dev_alloc(2 * (size_t)kMaxGrid * k * 8));
+    s->part = static_cast<double *>(dev_alloc(2 * part_rows(k) * k * 8));
     s->scal = static_cast<double *>(dev_alloc(S_COUNT * (size_t)k * 8));
     KRY_HIP(hipMemsetAsync(s->scal, 0, S_COUNT * (size_t)k * 8, ctx->stream));
     s->chunk_cap = 64;

@@ -16,6 +16,10 @@ namespace kry {
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kWave = 64;            // CDNA wavefront
 constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
+// The block right-hand-side SpMV (k <= 8) runs one slice per wave, up to
+// kMaxGridBlk blocks, so partial buffers for k <= 8 hold that many rows.
+constexpr int kMaxGridBlk = 32768;
+inline size_t part_rows(int k) { return k <= 8 ? (size_t)kMaxGridBlk : (size_t)kMaxGrid; }
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
 constexpr int kSlice = 64;           // SELL slice height = one wavefront
 // diagonal-offset image (kry_csr::dia_*): slices of kDiaSlice rows, lane l

@@ -760,13 +760,19 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
 // The same SELL-128/DIA image for k right-hand sides stored row-major
 // (n x k): for a slot column of offset o the x rows of the slice's rows are
 // the contiguous block x[128 s + o, +128) x k. A lane owns CPL consecutive
-// columns (16 bytes) of one row per row group; a wave covers 64 / (k / CPL)
-// rows per group, so one x load per slot column is a contiguous 1 KB run
-// (for k = 8: 16 rows x 64 B), and the value of the row is one 8-byte load
-// (shared by the k / CPL lanes of the row). Each (row, column) is summed from
-// 0 over the slot columns in ascending offset order, holes skipped: bitwise
-// csr_matvecs. The epilogue is the lane-group kernel's row<CPL>.
-template <typename V, typename MV, int CPL, int UNR, class Src, class Epi>
+// columns (16 bytes) of one row per row group; a wave covers RPG = 64 / (k /
+// CPL) rows per group and NG = 128 / RPG groups per slice. Slot-major: for
+// each slot column the wave loads every group's value and x run at once (NG
+// contiguous runs of RPG x k elements, 1 KB each for k = 8) and accumulates;
+// each (row, column) is summed from 0 over the slot columns in ascending
+// offset order, holes skipped: bitwise csr_matvecs. One slice per wave (the
+// grid covers the slices, kMaxGridBlk blocks at most): the waves resident on
+// an XCD then work on neighbouring slices together, so the x rows a slot
+// column at offset +-o reads again were fetched by a neighbouring wave
+// moments before and are L2 hits (tools/dia_blk_bench: x fetched ~1x from
+// HBM, against ~3x with 2.4 contiguous slices per wave at 8192 blocks).
+// The epilogue is the lane-group kernel's row<CPL>.
+template <typename V, typename MV, int CPL, int NG, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__restrict__ sptr,
                                                               const int *__restrict__ swidth,
                                                               const int *__restrict__ doff,
@@ -774,68 +780,60 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__r
                                                               const MV *__restrict__ val, int64_t nslices, int64_t n,
                                                               int k, Src src, Epi epi, double *__restrict__ part,
                                                               const Ctrl *ctrl, int step) {
+  constexpr int RPG = kDiaSlice / NG;  // rows per group
+  constexpr int LPR = 64 / RPG;        // lanes per row (k / CPL)
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock * CPL];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int lpr = k / CPL;         // lanes per row
-  const int rpg = 64 / lpr;        // rows per group
-  const int rl0 = lane / lpr, c0 = (lane % lpr) * CPL;
+  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
   const int64_t W = (int64_t)gridDim.x * 4;
-  const int64_t m = (int64_t)g * 4 + wid;
-  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
   const auto bs = src.template bind<CPL>(c0);
   double dacc[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
-  for (int64_t s = s_begin; s < s_end; ++s) {
+  for (int64_t s = (int64_t)g * 4 + wid; s < nslices; s += W) {
     const int w = swidth[s];
     const int64_t base = sptr[s];
     const int64_t cb = base / kDiaSlice;
-    const int *mo = doff + cb;  // wave-uniform: scalar loads
-    const uint64_t *mk = dmask + 2 * cb;
-    for (int rl = rl0; rl < kDiaSlice; rl += rpg) {
-      const int64_t row = s * kDiaSlice + rl;
-      const int q = rl & 1;             // mask word of this row
-      const uint64_t bit = uint64_t(1) << (rl >> 1);
-      const MV *cv = val + base + rl;
-      V acc[CPL];
+    V acc[NG][CPL];
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) acc[c] = V(0);
-      for (int j0 = 0; j0 < w; j0 += UNR) {
-        int off[UNR];
-        uint64_t m0[UNR], m1[UNR];
+    for (int r = 0; r < NG; ++r)
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          off[u] = mo[j0 + u];
-          m0[u] = mk[2 * (j0 + u)];
-          m1[u] = mk[2 * (j0 + u) + 1];
-        }
-        V a[UNR];
+      for (int c = 0; c < CPL; ++c) acc[r][c] = V(0);
+    for (int j = 0; j < w; ++j) {
+      const int off = doff[cb + j];  // wave-uniform: scalar loads
+      const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+      const MV *cv = val + base + (int64_t)j * kDiaSlice;
+      V a[NG];
+      bool on[NG];
+      V xv[NG][CPL];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) a[u] = j0 + u < w ? (V)cv[(int64_t)(j0 + u) * kDiaSlice] : V(0);
-        bool on[UNR];
-        V xv[UNR][CPL];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          on[u] = j0 + u < w && ((q ? m1[u] : m0[u]) & bit) != 0;
-          bs.row(on[u] ? row + off[u] : 0, xv[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const V p = a[u] * xv[u][c];
-            const V t = acc[c] + p;
-            acc[c] = on[u] ? t : acc[c];
-          }
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        a[r] = (V)cv[rl];
+        on[r] = ((((rl & 1) ? m1 : m0) >> (rl >> 1)) & 1u) != 0;  // mask word (rl & 1), bit (rl >> 1)
+        const int64_t row = s * kDiaSlice + rl;
+        bs.row(on[r] ? row + off : 0, xv[r]);
       }
+#pragma unroll
+      for (int r = 0; r < NG; ++r)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const V p = a[r] * xv[r][c];
+          const V t = acc[r][c] + p;
+          acc[r][c] = on[r] ? t : acc[r][c];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NG; ++r) {
+      const int64_t row = s * kDiaSlice + r * RPG + rl0;
       if (row < n) {
         V xi[CPL];
         bs.row(row, xi);
-        epi.template row<CPL>(row, c0, acc, xi, dacc);
+        epi.template row<CPL>(row, c0, acc[r], xi, dacc);
       }
     }
   }
@@ -1329,15 +1327,20 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
     }
     constexpr int CPLB = 16 / (int)sizeof(V);  // columns per lane of the block DIA kernel
     if (k >= CPLB && k <= 8 && A->dia && !dia_blk_off()) {
-      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->dia_nslices + 3) / 4));
+      // one slice per wave (partial buffers hold part_rows(k) = kMaxGridBlk rows for k <= 8)
+      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGridBlk, (A->dia_nslices + 3) / 4));
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->dia_sptr),
                            static_cast<const int *>(A->dia_width), static_cast<const int *>(A->dia_off),
                            static_cast<const uint64_t *>(A->dia_mask), static_cast<const MV *>(A->dia_val),
                            A->dia_nslices, A->n, k, src, epi, part, ctrl, step);
       };
-      if (A->dia_max_width <= 8) go(spmv_dia_blk_kernel<V, MV, CPLB, 8, Src, Epi>);
-      else go(spmv_dia_blk_kernel<V, MV, CPLB, 16, Src, Epi>);
+      // NG = 128 / (64 / (k / CPLB)) = 2 k / CPLB row groups per slice
+      switch (k / CPLB) {
+        case 1: go(spmv_dia_blk_kernel<V, MV, CPLB, 2, Src, Epi>); break;
+        case 2: go(spmv_dia_blk_kernel<V, MV, CPLB, 4, Src, Epi>); break;
+        default: go(spmv_dia_blk_kernel<V, MV, CPLB, 8, Src, Epi>); break;
+      }
       KRY_HIP(hipGetLastError());
       if (grid_out) *grid_out = grid;
       return;

@@ -1558,9 +1558,9 @@ int kry_gmres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, int32_t max
     KRY_HIP(hipMemsetAsync(s->xk, 0, vb, ctx->stream));
     KRY_HIP(hipMemsetAsync(s->wv, 0, vb, ctx->stream));
     KRY_HIP(hipMemsetAsync(s->wv2, 0, vb, ctx->stream));
-    s->part = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
+    s->part = static_cast<double *>(dev_alloc(part_rows(k) * k * 8));
     s->part1 = static_cast<double *>(dev_alloc((size_t)k * 8));
-    s->part2 = static_cast<double *>(dev_alloc((size_t)kMaxGrid * k * 8));
+    s->part2 = static_cast<double *>(dev_alloc(part_rows(k) * k * 8));
     s->scal = static_cast<double *>(dev_alloc(G_COUNT * (size_t)k * 8));
     s->h = static_cast<double *>(dev_alloc(((size_t)maxiter + 2) * k * 8));
     s->R = static_cast<double *>(dev_alloc(((size_t)maxiter + 1) * (maxiter > 0 ? maxiter : 1) * k * 8));

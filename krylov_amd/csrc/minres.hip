@@ -628,7 +628,7 @@ void mr_run_typed(kry_minres *s, int max_steps) {
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   V *w = static_cast<V *>(s->wv);
-  double *partA = s->part, *partB = s->part + (size_t)kMaxGrid * k;
+  double *partA = s->part, *partB = s->part + part_rows(k) * k;
   for (int step = 0; step < max_steps; ++step) {
     const int64_t i = s->it + step;
     const V *p = static_cast<const V *>(s->P[i % 3]);
@@ -755,7 +755,7 @@ int kry_minres_create(kry_ctx *ctx, kry_csr *A, int32_t k, int dtype, kry_minres
       s->W[i] = static_cast<double *>(dev_alloc(elems * 8));
       KRY_HIP(hipMemsetAsync(s->W[i], 0, elems * 8, ctx->stream));
     }
-    s->part = static_cast<double *>(dev_alloc(2 * (size_t)kMaxGrid * k * 8));
+    s->part = static_cast<double *>(dev_alloc(2 * part_rows(k) * k * 8));
     s->scal = static_cast<double *>(dev_alloc(M_COUNT * (size_t)k * 8));
     KRY_HIP(hipMemsetAsync(s->scal, 0, M_COUNT * (size_t)k * 8, ctx->stream));
     s->chunk_cap = 64;

@@ -1,0 +1,374 @@
+// Microbenchmark of the block right-hand-side DIA SpMV (k = 8, cfg4's 5-point
+// Poisson N^2) on gfx950 (development tool, not product). Uploads the matrix
+// through the library's C-ABI, times the library's block CG SpMV (Ap stored +
+// <p, Ap> partials) and probe variants on the same image: no store, a pure
+// p-read + Ap-write stream (the traffic floor), and slot-major kernels in
+// which a wave loads one slot column for ALL row groups of its slice at once
+// (CPL = 2, 4 or 8 columns per lane). Every full variant is checked bitwise
+// against the library kernel.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     tools/dia_blk_bench.hip -o tools/dia_blk_bench -Lkrylov_amd -lkrylov_hip -Wl,-rpath,'$ORIGIN/../krylov_amd'
+//   ./tools/dia_blk_bench [N=3163] [reps=20]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/krylov_hip.h"
+#include "../krylov_amd/csrc/device.hpp"
+
+using namespace kry;
+
+#define CK(x)                                                                         \
+  do {                                                                                \
+    hipError_t e = (x);                                                               \
+    if (e != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                        \
+    }                                                                                 \
+  } while (0)
+#define KC(x)                                                                             \
+  do {                                                                                    \
+    int r = (x);                                                                          \
+    if (r != KRY_OK) {                                                                    \
+      fprintf(stderr, "%s:%d %s: %d %s\n", __FILE__, __LINE__, #x, r, kry_last_error()); \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+constexpr int K = 8;
+
+static void build_poisson(int N, std::vector<int> &ip, std::vector<int> &ix, std::vector<double> &dv) {
+  const int64_t n = (int64_t)N * N;
+  ip.assign(n + 1, 0);
+  ix.clear();
+  dv.clear();
+  for (int64_t r = 0; r < n; ++r) {
+    const int i = r % N, j = r / N;
+    if (j > 0) ix.push_back((int)(r - N)), dv.push_back(-1.0);
+    if (i > 0) ix.push_back((int)(r - 1)), dv.push_back(-1.0);
+    ix.push_back((int)r), dv.push_back(4.0);
+    if (i < N - 1) ix.push_back((int)(r + 1)), dv.push_back(-1.0);
+    if (j < N - 1) ix.push_back((int)(r + N)), dv.push_back(-1.0);
+    ip[r + 1] = (int)ix.size();
+  }
+}
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+// p read + Ap write, 16 B per lane: the SpMV's vector traffic alone
+__global__ __launch_bounds__(256) void copy_floor(const d2v *__restrict__ a, d2v *__restrict__ b, int64_t nb) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride)
+    __builtin_nontemporal_store(a[i], b + i);
+}
+
+template <int C>
+__device__ __forceinline__ void ldx(const double *p, double (&o)[C]) {
+#pragma unroll
+  for (int c = 0; c < C; c += 2) {
+    const d2v v = *reinterpret_cast<const d2v *>(p + c);
+    o[c] = v.x;
+    o[c + 1] = v.y;
+  }
+}
+
+// Slot-major: per slot column j of the slice, every row group's value and x
+// run are loaded together (NG = 128 / rows-per-group loads of each), then
+// accumulated; each (row, column) still sums its slot columns in ascending
+// order from 0. MODE bits: 1 no store (dot terms only); 2 nontemporal value
+// loads; 4 the slice's epilogue deferred behind the next slice's first slot
+// column loads; 8 the epilogue's p values taken from the offset-0 slot
+// column's x run (reloaded only where that slot is a hole); 16 the slot
+// column's 128 values loaded once (16 B per lane) and handed to the row
+// groups by lane shuffles; 32 every x run read at offset 0 (locality probe,
+// wrong results); 64 no x loads; 256 no XCD remap of the block index; 512
+// wave m takes slices m, m + W, m + 2W, ... (W waves) instead of a contiguous run.
+template <int CPL, int MODE, int BS = 256>
+__global__ __launch_bounds__(BS) void dia_slot_major(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                      const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                      const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                      const double *__restrict__ x, double *__restrict__ y,
+                                                      double *__restrict__ part) {
+  constexpr int LPR = K / CPL, RPG = 64 / LPR, NG = kDiaSlice / RPG;
+  constexpr bool DEFER = (MODE & 4) != 0, CAPT = (MODE & 8) != 0, SHUF = (MODE & 16) != 0;
+  __shared__ double red[BS * CPL];
+  constexpr int WPB = BS / 64;  // waves per block
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = (MODE & 256) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
+  const int64_t W = (int64_t)gridDim.x * WPB, m = (int64_t)g * WPB + wid;
+  const int64_t s_begin = nslices * m / W, s_end = nslices * (m + 1) / W;
+  double dacc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
+  double pend[DEFER ? NG : 1][CPL];
+  double xi[CAPT ? NG : 1][CPL];
+  bool have[CAPT ? NG : 1];
+  int64_t prow0 = -1;  // first row (group 0, lane's rl0) of the pending slice
+  auto finish = [&](int64_t row0, auto &&accs) {
+#pragma unroll
+    for (int r = 0; r < NG; ++r) {
+      const int64_t row = row0 + r * RPG;
+      if (row < n) {
+        double q[CPL];
+        if (CAPT) {
+          if (have[r]) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) q[c] = xi[CAPT ? r : 0][c];
+          } else {
+            ldx<CPL>(x + row * K + c0, q);
+          }
+        } else {
+          ldx<CPL>(x + row * K + c0, q);
+        }
+        if (!(MODE & 1)) {
+#pragma unroll
+          for (int c = 0; c < CPL; c += 2) {
+            d2v v;
+            v.x = accs(r, c);
+            v.y = accs(r, c + 1);
+            __builtin_nontemporal_store(v, reinterpret_cast<d2v *>(y + row * K + c0 + c));
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) dacc[c] += dterm(q[c], accs(r, c));
+      }
+    }
+  };
+  const bool strided = (MODE & 512) != 0;
+  for (int64_t s = strided ? m : s_begin; s < (strided ? nslices : s_end); s += strided ? W : 1) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s], cb = base / kDiaSlice;
+    double acc[NG][CPL];
+#pragma unroll
+    for (int r = 0; r < NG; ++r)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[r][c] = 0.0;
+    for (int j = 0; j < w; ++j) {
+      const int off = doff[cb + j];
+      const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+      double a[NG], xv[NG][CPL];
+      bool on[NG];
+      d2v vv;
+      if (SHUF) {
+        const d2v *vp = reinterpret_cast<const d2v *>(val + base + (int64_t)j * kDiaSlice) + lane;
+        vv = (MODE & 2) ? __builtin_nontemporal_load(vp) : *vp;
+      }
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        if (!SHUF) {
+          const double *vp = val + base + (int64_t)j * kDiaSlice + rl;
+          a[r] = (MODE & 2) ? __builtin_nontemporal_load(vp) : *vp;
+        }
+        on[r] = (((rl & 1) ? m1 : m0) >> (rl >> 1) & 1u) != 0;
+        const int64_t row = s * kDiaSlice + rl;
+        if (MODE & 64) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) xv[r][c] = 1.0;
+        } else {
+          ldx<CPL>(x + (on[r] ? row + ((MODE & 32) ? 0 : off) : 0) * K + c0, xv[r]);
+        }
+      }
+      if (DEFER && j == 0 && prow0 >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        finish(prow0, [&](int r, int c) { return pend[DEFER ? r : 0][c]; });
+        __builtin_amdgcn_sched_barrier(0);
+        prow0 = -1;
+      }
+      if (SHUF) {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) {
+          const int rl = r * RPG + rl0;
+          const double lo = __shfl(vv.x, rl >> 1), hi = __shfl(vv.y, rl >> 1);
+          a[r] = (rl & 1) ? hi : lo;
+        }
+      }
+      if (CAPT && off == 0) {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) {
+          have[CAPT ? r : 0] = on[r];
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) xi[CAPT ? r : 0][c] = xv[r][c];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NG; ++r)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const double p = a[r] * xv[r][c];
+          const double t = acc[r][c] + p;
+          acc[r][c] = on[r] ? t : acc[r][c];
+        }
+    }
+    if (CAPT) {
+      bool any0 = false;
+      for (int j = 0; j < w; ++j) any0 = any0 || doff[cb + j] == 0;
+      if (!any0)
+#pragma unroll
+        for (int r = 0; r < NG; ++r) have[CAPT ? r : 0] = false;
+    }
+    if (DEFER) {
+      if (w == 0 && prow0 >= 0) finish(prow0, [&](int r, int c) { return pend[DEFER ? r : 0][c]; });
+#pragma unroll
+      for (int r = 0; r < NG; ++r)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) pend[DEFER ? r : 0][c] = acc[r][c];
+      prow0 = s * kDiaSlice + rl0;
+    } else {
+      finish(s * kDiaSlice + rl0, [&](int r, int c) { return acc[r][c]; });
+    }
+  }
+  if (DEFER && prow0 >= 0) finish(prow0, [&](int r, int c) { return pend[DEFER ? r : 0][c]; });
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];
+  block_tree_reduce(red, BS * CPL, K);
+  if (tid < K) part[(int64_t)g * K + tid] = red[tid];
+}
+
+int main(int argc, char **argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 3163;
+  const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  std::vector<int> ip, ix;
+  std::vector<double> dv;
+  build_poisson(N, ip, ix, dv);
+  const int64_t n = (int64_t)ip.size() - 1, nnz = ix.size();
+  kry_ctx *ctx;
+  KC(kry_ctx_create(0, &ctx));
+  kry_csr *A;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
+  if (!A->dia) {
+    fprintf(stderr, "no DIA image\n");
+    return 1;
+  }
+  printf("N=%d n=%ld nnz=%ld k=%d dia_slices=%ld dia_slots=%ld max_width=%d\n", N, (long)n, (long)nnz, K,
+         (long)A->dia_nslices, (long)A->dia_nslots, A->dia_max_width);
+  std::vector<double> xh(n * K);
+  for (int64_t i = 0; i < n * K; ++i) xh[i] = 1.0 + (double)((i * 7919) % 1000) * 1e-3;
+  kry_vec *xv, *yv, *yrefv;
+  KC(kry_vec_create(ctx, n, K, KRY_F64, &xv));
+  KC(kry_vec_create(ctx, n, K, KRY_F64, &yv));
+  KC(kry_vec_create(ctx, n, K, KRY_F64, &yrefv));
+  KC(kry_vec_upload(xv, xh.data()));
+  double *x = (double *)xv->d, *y = (double *)yv->d, *yref = (double *)yrefv->d, *part;
+  CK(hipMalloc(&part, (size_t)65536 * K * 8));  // grids up to 65536 blocks (the sweep goes past kMaxGrid)
+  hipStream_t st = ctx->stream;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double S = (double)nnz * 12 + (double)(n + 1) * 4 + 2.0 * n * K * 8;
+  const double phys = (double)A->dia_nslots * 8 + (double)A->dia_nslots / 128 * 20 + 2.0 * n * K * 8;
+  auto timeit = [&](const char *name, auto launch) {
+    launch();
+    CK(hipStreamSynchronize(st));
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, st));
+      launch();
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ts.push_back(t);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double ms = ts[ts.size() / 2];
+    printf("%-46s %.4f ms  S-rate %.0f GB/s  image-rate %.0f GB/s\n", name, ms, S / ms / 1e6, phys / ms / 1e6);
+    return ms;
+  };
+  timeit("library spmv_dia_blk (EpiApDot)", [&] {
+    int P;
+    launch_spmv<double, double, int>(A, K, SrcPlain<double>{x, K}, EpiApDot<double>{yref, nullptr, K}, part, &P,
+                                     nullptr, 0, st);
+  });
+  std::vector<double> ref(n * K), got(n * K);
+  CK(hipMemcpy(ref.data(), yref, n * K * 8, hipMemcpyDeviceToHost));
+  {
+    int64_t bad = 0;
+    for (int64_t r = 0; r < n; ++r)
+      for (int c = 0; c < K; ++c) {
+        double acc = 0.0;
+        for (int e = ip[r]; e < ip[r + 1]; ++e) {
+          volatile double p = dv[e] * xh[(int64_t)ix[e] * K + c];
+          acc = acc + p;
+        }
+        bad += memcmp(&acc, &ref[r * K + c], 8) != 0;
+      }
+    printf("library vs host csr_matvecs: %ld entries differ\n", (long)bad);
+  }
+  auto check = [&](const char *name) {
+    CK(hipMemcpy(got.data(), y, n * K * 8, hipMemcpyDeviceToHost));
+    if (memcmp(got.data(), ref.data(), n * K * 8) != 0) printf("  !! %s differs from the library kernel\n", name);
+  };
+  timeit("floor: p read + Ap write (16 B/lane copy)", [&] {
+    hipLaunchKernelGGL(copy_floor, dim3(8192), dim3(256), 0, st, (const d2v *)x, (d2v *)y, n * K / 2);
+  });
+  const int grid = (int)std::min<int64_t>(kMaxGrid, (A->dia_nslices + 3) / 4);
+  int gr = 0;
+#define SM(CPL, MODE, NAME, CHECK)                                                                                \
+  {                                                                                                               \
+    char nm[96];                                                                                                  \
+    snprintf(nm, sizeof nm, "%s, grid %d", NAME, gr);                                                             \
+    timeit(nm, [&] {                                                                                              \
+      hipLaunchKernelGGL((dia_slot_major<CPL, MODE>), dim3(gr), dim3(256), 0, st, (const int64_t *)A->dia_sptr,   \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,       \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);              \
+    });                                                                                                           \
+    if (CHECK) check(nm);                                                                                         \
+  }
+  if (getenv("DIA_BLK_GRIDS")) {  // block size / grid sweep of the slot-major kernel
+    const int full = (int)((A->dia_nslices + 3) / 4);
+    if (full > 65536) return 1;
+    for (int rep = 0; rep < 2; ++rep) {
+      gr = full;
+      SM(2, 0, "slot-major CPL 2, 256 threads, 1 slice/wave", true);
+      gr = (int)((A->dia_nslices + 15) / 16);
+#define SMB(CPL, MODE, BS, NAME)                                                                                  \
+  {                                                                                                               \
+    char nm[96];                                                                                                  \
+    snprintf(nm, sizeof nm, "%s, grid %d", NAME, gr);                                                             \
+    timeit(nm, [&] {                                                                                              \
+      hipLaunchKernelGGL((dia_slot_major<CPL, MODE, BS>), dim3(gr), dim3(BS), 0, st, (const int64_t *)A->dia_sptr, \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,       \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);              \
+    });                                                                                                           \
+    check(nm);                                                                                                    \
+  }
+      SMB(2, 0, 1024, "slot-major CPL 2, 1024 threads, 1 slice/wave");
+      SMB(2, 16, 1024, "slot-major CPL 2, 1024 thr, shuffled values");
+      gr = (int)((A->dia_nslices + 7) / 8);
+      SMB(2, 0, 512, "slot-major CPL 2, 512 threads, 1 slice/wave");
+      gr = (int)((A->dia_nslices + 31) / 32);
+      SMB(2, 0, 1024, "slot-major CPL 2, 1024 threads, 2 slices/wave");
+      SMB(2, 512, 1024, "slot-major CPL 2, 1024 thr, 2 slices/wave strided");
+    }
+  } else
+  for (int gr2 : {grid, 4096}) {
+    gr = gr2;
+    SM(2, 0, "slot-major CPL 2", true);
+    SM(2, 1, "slot-major CPL 2, no store", false);
+    SM(2, 2, "slot-major CPL 2, nt values", true);
+    SM(2, 4, "slot-major CPL 2, deferred epilogue", true);
+    SM(2, 8, "slot-major CPL 2, p from the diagonal", true);
+    SM(2, 16, "slot-major CPL 2, shuffled values", true);
+    SM(2, 18, "slot-major CPL 2, shuffled nt values", true);
+    SM(2, 24, "slot-major CPL 2, shuffled values + diagonal p", true);
+    SM(2, 28, "slot-major CPL 2, shuffled + diag p + deferred", true);
+    SM(2, 32, "slot-major CPL 2, x at offset 0 only", false);
+    SM(2, 64, "slot-major CPL 2, no x loads", false);
+    if (getenv("DIA_BLK_SHORT")) break;
+    SM(4, 16, "slot-major CPL 4, shuffled values", true);
+  }
+  KC(kry_vec_destroy(xv));
+  KC(kry_vec_destroy(yv));
+  KC(kry_vec_destroy(yrefv));
+  KC(kry_csr_destroy(A));
+  KC(kry_ctx_destroy(ctx));
+  return 0;
+}
