@@ -1312,7 +1312,18 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   int grid;
   if constexpr (sizeof(I) == 4) {
     if (k == 1 && A->dia) {
-      grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A->dia_nslices + 3) / 4));
+      // Wide images (more than 8 slot columns, the metric's 15): one slice
+      // per wave (tools/dia_bench "deferred store, grid": 0.227 ms on the
+      // metric against 0.252 ms at 8192 blocks of 2.4 slices per wave; CG
+      // 2896 -> 3040 it/s). Narrow ones keep 8192 blocks: on cfg5 (7 slot
+      // columns, fp32 values) the larger grid measured 1.8 % slower per
+      // MINRES iteration, its consumers summing twice the partials.
+      static const int dia_cap_env = [] {
+        const char *e = getenv("KRY_DIA_GRID");  // tuning override: grid cap
+        return e ? std::max(1, std::min(atoi(e), kMaxGridBlk)) : 0;
+      }();
+      const int dia_cap = dia_cap_env ? dia_cap_env : (A->dia_max_width > 8 ? kMaxGridBlk : kMaxGrid);
+      grid = (int)std::max<int64_t>(1, std::min<int64_t>(dia_cap, (A->dia_nslices + 3) / 4));
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->dia_sptr),
                            static_cast<const int *>(A->dia_width), static_cast<const int *>(A->dia_off),

@@ -1,5 +1,5 @@
 """One secondary BASELINE config on its own, for a kernel trace:
-`python tools/cfg_time.py cfg4|cfg5|cfg2|gmres_cfg3 [steps]` or `gmres_metric [m]` (run under
+`python tools/cfg_time.py metric|cfg4|cfg5|cfg2|gmres_cfg3 [steps]` or `gmres_metric [m]` (run under
 `rocprofv3 --kernel-trace --stats` to split an iteration by kernel)."""
 import os
 import sys
@@ -23,5 +23,9 @@ elif cfg == "cfg5":
 elif cfg == "gmres_metric":
     m = steps if len(sys.argv) > 2 else 216
     print(cfg, bench.run_gmres(problems.stencil15_3d(m), f"metric {m}^3 GMRES(30)"), flush=True)
+elif cfg == "metric":
+    r = bench.run_metric(problems.stencil15_3d(216), 200, 20, 1, 0, 0, None)
+    spmv_ms = r["spmv_ms"] / max(r["spmv_count"], 1)
+    print(cfg, {"it_per_s": 200 / r["elapsed"], "spmv_ms": spmv_ms}, flush=True)
 elif cfg == "gmres_cfg3":
     print(cfg, bench.run_gmres(), flush=True)

@@ -400,7 +400,7 @@ int main(int argc, char **argv) {
   KC(kry_vec_create(ctx, n, 1, KRY_F64, &yrefv));
   KC(kry_vec_upload(xv, xh.data()));
   double *x = (double *)xv->d, *y = (double *)yv->d, *yref = (double *)yrefv->d, *part, *dummy;
-  CK(hipMalloc(&part, kMaxGrid * 8));
+  CK(hipMalloc(&part, (size_t)65536 * 8));  // grids up to 65536 blocks (the sweep goes past kMaxGrid)
   CK(hipMalloc(&dummy, 64));
   hipStream_t st = ctx->stream;
   hipEvent_t e0, e1;
@@ -484,7 +484,8 @@ int main(int argc, char **argv) {
   PROBE(8, 0, "probe: UNR 8", true);
   PROBE(16, 16, "probe: interleaved slices", true);
   PROBE(16, 32, "probe: plain (not nt) store", true);
-  for (int gr : {grid, 4096, 16384 < kMaxGrid ? 16384 : kMaxGrid}) {
+  const int full = (int)std::min<int64_t>(65536, (A->dia_nslices + 3) / 4);  // one slice per wave
+  for (int gr : {grid, 4096, full}) {
     char nm[80];
     snprintf(nm, sizeof nm, "probe: deferred store, grid %d", gr);
     timeit(nm, [&] {
