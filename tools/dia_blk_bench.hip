@@ -232,6 +232,78 @@ __global__ __launch_bounds__(BS) void dia_slot_major(const int64_t *__restrict__
   if (tid < K) part[(int64_t)g * K + tid] = red[tid];
 }
 
+// Split slices: wave (s, part) handles GPW of the slice's 8 row groups (CPL 2,
+// k = 8), one (slice, part) per wave; SPR slot columns per round (all their
+// loads issued together). Fewer registers per wave (more resident waves) or
+// more loads in flight per wave than the whole-slice kernel.
+template <int GPW, int SPR>
+__global__ __launch_bounds__(256) void dia_split(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                 const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                 const double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ part) {
+  constexpr int CPL = 2, LPR = K / CPL, RPG = 64 / LPR, NG = kDiaSlice / RPG, PARTS = NG / GPW;
+  __shared__ double red[256 * CPL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  double dacc[CPL] = {0.0, 0.0};
+  for (int64_t t = (int64_t)g * 4 + wid; t < nslices * PARTS; t += W) {
+    const int64_t s = t / PARTS;
+    const int pt = (int)(t % PARTS);
+    const int w = swidth[s];
+    const int64_t base = sptr[s], cb = base / kDiaSlice;
+    double acc[GPW][CPL];
+#pragma unroll
+    for (int r = 0; r < GPW; ++r) acc[r][0] = acc[r][1] = 0.0;
+    for (int j0 = 0; j0 < w; j0 += SPR) {
+      double a[SPR][GPW], xv[SPR][GPW][CPL];
+      bool on[SPR][GPW];
+#pragma unroll
+      for (int q = 0; q < SPR; ++q) {
+        const int j = j0 + q < w ? j0 + q : w - 1;  // a slot past the width repeats the last (dropped below)
+        const int off = doff[cb + j];
+        const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+#pragma unroll
+        for (int r = 0; r < GPW; ++r) {
+          const int rl = (pt * GPW + r) * RPG + rl0;
+          a[q][r] = val[base + (int64_t)j * kDiaSlice + rl];
+          on[q][r] = j0 + q < w && ((((rl & 1) ? m1 : m0) >> (rl >> 1)) & 1u) != 0;
+          ldx<CPL>(x + (on[q][r] ? s * kDiaSlice + rl + off : 0) * K + c0, xv[q][r]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < SPR; ++q)
+#pragma unroll
+        for (int r = 0; r < GPW; ++r)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const double p = a[q][r] * xv[q][r][c];
+            const double tt = acc[r][c] + p;
+            acc[r][c] = on[q][r] ? tt : acc[r][c];
+          }
+    }
+#pragma unroll
+    for (int r = 0; r < GPW; ++r) {
+      const int64_t row = s * kDiaSlice + (pt * GPW + r) * RPG + rl0;
+      if (row < n) {
+        double q[CPL];
+        ldx<CPL>(x + row * K + c0, q);
+        d2v v;
+        v.x = acc[r][0];
+        v.y = acc[r][1];
+        __builtin_nontemporal_store(v, reinterpret_cast<d2v *>(y + row * K + c0));
+        for (int c = 0; c < CPL; ++c) dacc[c] += dterm(q[c], acc[r][c]);
+      }
+    }
+  }
+  for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];
+  block_tree_reduce(red, 256 * CPL, K);
+  if (tid < K) part[(int64_t)g * K + tid] = red[tid];
+}
+
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 3163;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -322,6 +394,31 @@ int main(int argc, char **argv) {
     });                                                                                                           \
     if (CHECK) check(nm);                                                                                         \
   }
+  if (getenv("DIA_BLK_SPLIT")) {
+#define SPL(GPW, SPR)                                                                                              \
+  {                                                                                                                \
+    const int64_t waves = A->dia_nslices * (8 / GPW);                                                              \
+    const int gsp = (int)std::min<int64_t>(65536, (waves + 3) / 4);                                                \
+    char nm[96];                                                                                                   \
+    snprintf(nm, sizeof nm, "split: %d groups/wave, %d slots/round, grid %d", GPW, SPR, gsp);                      \
+    timeit(nm, [&] {                                                                                               \
+      hipLaunchKernelGGL((dia_split<GPW, SPR>), dim3(gsp), dim3(256), 0, st, (const int64_t *)A->dia_sptr,         \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,        \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);               \
+    });                                                                                                            \
+    check(nm);                                                                                                     \
+  }
+    for (int rep = 0; rep < 2; ++rep) {
+      SPL(8, 1);
+      SPL(8, 2);
+      SPL(4, 1);
+      SPL(4, 2);
+      SPL(4, 3);
+      SPL(2, 1);
+      SPL(2, 3);
+      SPL(2, 5);
+    }
+  } else
   if (getenv("DIA_BLK_GRIDS")) {  // block size / grid sweep of the slot-major kernel
     const int full = (int)((A->dia_nslices + 3) / 4);
     if (full > 65536) return 1;
