@@ -63,6 +63,19 @@ int kry_ctx_create(int device, kry_ctx **out);
 int kry_ctx_destroy(kry_ctx *ctx);
 int kry_ctx_synchronize(kry_ctx *ctx);
 
+/* ---- device memory -------------------------------------------------------
+ * The library's device buffers come from a caching allocator: blocks freed by
+ * a destroyed solver / operator / vector are reused by the next allocation of
+ * the same rounded size (after one device synchronisation), instead of a
+ * hipMalloc + hipFree pair per reference-API call (the reference allocates
+ * its NumPy work arrays per call, cg.py:116-131, arnoldi.py:129-131).
+ * KRYLOV_ALLOC_CACHE=0 disables it; KRYLOV_ALLOC_CACHE_MAX_GB caps it (64).
+ * stats: out[0..5] = bytes in use, bytes cached, reuses, hipMallocs, device
+ * syncs taken to retire freed blocks, enabled (0/1). release: hipFree every
+ * cached block (in use blocks are untouched). */
+int kry_mem_stats(int64_t *out);
+int kry_mem_release(void);
+
 /* ---- CSR operator ------------------------------------------------------
  * Replaces the scipy.sparse matrix the reference multiplies with `A @ x`
  * (_helpers.py:44-48 Product.__matmul__, cg.py:86, gmres.py:106,

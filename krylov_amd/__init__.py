@@ -16,6 +16,7 @@ from .givens import givens, lartg
 from .householder import Householder
 from .gmres import arnoldi, gmres, gmres_restarted, multi_solve_triangular
 from .minres import lanczos, minres
+from ._lib import empty_cache, memory_stats
 from .sparse import CsrOperator, as_device_operator, clear_operator_cache
 
 __version__ = "0.1.0"
@@ -38,6 +39,8 @@ __all__ = [
     "CsrOperator",
     "as_device_operator",
     "clear_operator_cache",
+    "memory_stats",
+    "empty_cache",
     "WeightedInner",
     "Identity",
     "Info",

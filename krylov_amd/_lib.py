@@ -110,6 +110,8 @@ _SIGNATURES = {
     "kry_profile_enable": [_vp, _int],
     "kry_profile_select": [_vp, ctypes.c_uint32, ctypes.c_int32],
     "kry_profile_read": [_vp, _int, _ip64, _dp],
+    "kry_mem_stats": [_ip64],
+    "kry_mem_release": [],
 }
 
 for _name, _args in _SIGNATURES.items():
@@ -164,6 +166,19 @@ def device_count():
     c = _int(0)
     check(lib.kry_device_count(ctypes.byref(c)))
     return c.value
+
+
+def memory_stats():
+    """The caching device allocator's counters (kry_mem_stats)."""
+    out = np.zeros(6, dtype=np.int64)
+    check(lib.kry_mem_stats(out.ctypes.data_as(_ip64)))
+    keys = ("bytes_in_use", "bytes_cached", "reuses", "device_mallocs", "retire_syncs", "enabled")
+    return {k: int(v) for k, v in zip(keys, out)}
+
+
+def empty_cache():
+    """Return every cached (freed) device block to the runtime (kry_mem_release)."""
+    check(lib.kry_mem_release())
 
 
 def dia_plan(indptr, indices):

@@ -104,14 +104,13 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter
-    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
 
     st = _CGState(prob)
     rho0 = st.start()
     chunk = st.preferred_chunk()
     rn0 = _norm_from_sq(prob, rho0)
     if callback is not None:
-        callback(x0_host, prob.unpad_vec(st.get(1), prob.r0_dtype))
+        callback(prob.x0_or_zeros(), prob.unpad_vec(st.get(1), prob.r0_dtype))
     resnorms = [prob.colvals(rn0)]
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))

@@ -3,7 +3,10 @@
 #include <atomic>
 #include <climits>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <thread>
+#include <unordered_map>
 
 #include "device.hpp"
 
@@ -20,18 +23,184 @@ void set_error(const std::string &msg) { g_last_error = msg; }
 // never used, the address only has to be mapped).
 constexpr size_t kAllocSlack = 256;
 
+// ------------------------------------------------ caching device allocator
+// A solve allocates its vectors (and GMRES its m + 1 basis vectors: 2.5 GB
+// at the metric) when the solver state is created and frees them when it is
+// destroyed, once per reference-API call. hipMalloc / hipFree of buffers
+// that size cost milliseconds each and hipFree synchronises the device, so
+// freed blocks are kept per (device, rounded size) and handed out again.
+// A freed block first goes to a pending list: it may still be read by work
+// queued on any stream. It is reused only after one hipDeviceSynchronize
+// retires the whole pending list (in practice the device is idle by then:
+// the solve's results have been downloaded). On hipMalloc failure every
+// cached block is released and the allocation retried once.
+// KRYLOV_ALLOC_CACHE=0 restores plain hipMalloc / hipFree.
+namespace {
+
+struct BlockKey {
+  int device;
+  size_t bytes;
+  bool operator<(const BlockKey &o) const { return device != o.device ? device < o.device : bytes < o.bytes; }
+};
+
+struct DevicePool {
+  std::mutex mu;
+  std::multimap<BlockKey, char *> free_blocks;           // reusable now
+  std::vector<std::pair<BlockKey, char *>> pending;      // freed, maybe still in use by queued work
+  std::unordered_map<char *, BlockKey> live;             // handed out (allocation base -> key)
+  size_t cached_bytes = 0, live_bytes = 0;
+  int64_t hits = 0, misses = 0, syncs = 0;
+};
+
+DevicePool &pool() {
+  static DevicePool *p = new DevicePool;  // never destroyed: frees may run from static destructors
+  return *p;
+}
+
+bool cache_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("KRYLOV_ALLOC_CACHE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// Bytes the cache may hold (KRYLOV_ALLOC_CACHE_MAX_GB, default 64 of the
+// 288 GB): a larger free goes straight back to the runtime.
+size_t cache_cap() {
+  static const size_t cap = [] {
+    const char *e = getenv("KRYLOV_ALLOC_CACHE_MAX_GB");
+    const double gb = e ? atof(e) : 64.0;
+    return (size_t)(gb > 0 ? gb * 1e9 : 0);
+  }();
+  return cap;
+}
+
+// 64 KiB granules below 2 MiB, 2 MiB granules above (the HBM page size the
+// runtime maps large buffers with): a reused block wastes < 2 MiB.
+size_t round_alloc(size_t total) {
+  const size_t g = total < ((size_t)2 << 20) ? ((size_t)64 << 10) : ((size_t)2 << 20);
+  return (total + g - 1) / g * g;
+}
+
+// Caller holds the lock. Moves every pending block to the free list after
+// the device has finished all queued work.
+void retire_pending(DevicePool &P) {
+  if (P.pending.empty()) return;
+  (void)hipDeviceSynchronize();
+  ++P.syncs;
+  for (auto &b : P.pending) P.free_blocks.emplace(b.first, b.second);
+  P.pending.clear();
+}
+
+// Caller holds the lock. hipFree of every cached (free or pending) block.
+void release_cached(DevicePool &P) {
+  (void)hipDeviceSynchronize();
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto &b : P.pending) P.free_blocks.emplace(b.first, b.second);
+  P.pending.clear();
+  for (auto &b : P.free_blocks) {
+    (void)hipSetDevice(b.first.device);
+    (void)hipFree(b.second);
+  }
+  (void)hipSetDevice(cur);
+  P.free_blocks.clear();
+  P.cached_bytes = 0;
+}
+
+}  // namespace
+
 void *dev_alloc(size_t bytes) {
-  void *p = nullptr;
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc(&p, bytes + 2 * kAllocSlack);
+  void *p = nullptr;
+  if (!cache_enabled()) {
+    hipError_t e = hipMalloc(&p, bytes + 2 * kAllocSlack);
+    if (e != hipSuccess)
+      throw Error{e == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE,
+                  std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e)};
+    return static_cast<char *>(p) + kAllocSlack;
+  }
+  int dev = 0;
+  KRY_HIP(hipGetDevice(&dev));
+  const BlockKey key{dev, round_alloc(bytes + 2 * kAllocSlack)};
+  DevicePool &P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  auto take = [&](std::multimap<BlockKey, char *>::iterator it) {
+    char *b = it->second;
+    P.free_blocks.erase(it);
+    P.cached_bytes -= key.bytes;
+    P.live.emplace(b, key);
+    P.live_bytes += key.bytes;
+    ++P.hits;
+    return b + kAllocSlack;
+  };
+  auto it = P.free_blocks.find(key);
+  if (it != P.free_blocks.end()) return take(it);
+  bool in_pending = false;
+  for (auto &b : P.pending) in_pending = in_pending || (b.first.device == dev && b.first.bytes == key.bytes);
+  if (in_pending) {
+    retire_pending(P);
+    it = P.free_blocks.find(key);
+    if (it != P.free_blocks.end()) return take(it);
+  }
+  hipError_t e = hipMalloc(&p, key.bytes);
+  if (e == hipErrorOutOfMemory && (P.cached_bytes > 0 || !P.pending.empty())) {
+    (void)hipGetLastError();
+    release_cached(P);
+    e = hipMalloc(&p, key.bytes);
+  }
   if (e != hipSuccess)
     throw Error{e == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE,
                 std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e)};
-  return static_cast<char *>(p) + kAllocSlack;
+  char *b = static_cast<char *>(p);
+  P.live.emplace(b, key);
+  P.live_bytes += key.bytes;
+  ++P.misses;
+  return b + kAllocSlack;
 }
 
-void dev_free(void *p) {
-  if (p) (void)hipFree(static_cast<char *>(p) - kAllocSlack);
+void dev_free(void *ptr) {
+  if (!ptr) return;
+  char *b = static_cast<char *>(ptr) - kAllocSlack;
+  if (!cache_enabled()) {
+    (void)hipFree(b);
+    return;
+  }
+  DevicePool &P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  auto it = P.live.find(b);
+  if (it == P.live.end()) {  // not ours (cannot happen through dev_alloc): plain free
+    (void)hipFree(b);
+    return;
+  }
+  const BlockKey key = it->second;
+  P.live.erase(it);
+  P.live_bytes -= key.bytes;
+  if (P.cached_bytes + key.bytes > cache_cap()) {  // over the cap: back to the runtime
+    (void)hipFree(b);
+    return;
+  }
+  P.pending.emplace_back(key, b);
+  P.cached_bytes += key.bytes;
+}
+
+// kry_mem_stats / kry_mem_release (C-ABI below)
+void mem_stats(int64_t *out) {
+  DevicePool &P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  out[0] = (int64_t)P.live_bytes;
+  out[1] = (int64_t)P.cached_bytes;
+  out[2] = P.hits;
+  out[3] = P.misses;
+  out[4] = P.syncs;
+  out[5] = cache_enabled() ? 1 : 0;
+}
+
+void mem_release() {
+  DevicePool &P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  release_cached(P);
 }
 
 double *ctx_scratch(kry_ctx *ctx, size_t bytes) {
@@ -194,6 +363,19 @@ int kry_device_count(int *count) {
   int c = 0;
   hipError_t e = hipGetDeviceCount(&c);
   *count = (e == hipSuccess) ? c : 0;
+  KRY_API_END
+}
+
+int kry_mem_stats(int64_t *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(out, KRY_EINVAL, "null out");
+  kry::mem_stats(out);
+  KRY_API_END
+}
+
+int kry_mem_release(void) {
+  KRY_API_BEGIN
+  kry::mem_release();
   KRY_API_END
 }
 

@@ -100,7 +100,9 @@ inline size_t dsize(int dtype) { return dtype == KRY_F64 ? 8 : 4; }
 inline size_t isize(int itype) { return itype == KRY_I64 ? 8 : 4; }
 
 void *dev_alloc(size_t bytes);
-void dev_free(void *p);
+void dev_free(void *p);  // to the caching pool (abi_core.hip)
+void mem_stats(int64_t *out);
+void mem_release();
 double *ctx_scratch(kry_ctx *ctx, size_t bytes);  // grown on demand, owned by the context
 
 // Event-timed launch bracket used by the solvers around their SpMV launches.

@@ -175,14 +175,13 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
         raise ValueError(f"unknown ortho {ortho!r}")
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
 
     st = _GmresState(prob, maxiter, sweeps)
     rn0 = st.start()
     resnorms = [prob.colvals(rn0)]
     if callback is not None:
         # the reference passes Ml_r0 = Ml (b - A x0) here (gmres.py:143-144)
-        callback(x0_host, prob.apply_host("Ml", prob.b - prob.A @ x0_host))
+        callback(prob.x0_or_zeros(), prob.apply_host("Ml", prob.b - prob.A @ prob.x0_or_zeros()))
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))
 
@@ -193,7 +192,7 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
 
     def current_x():
         if steps_done == 0:
-            return x0_host  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
+            return prob.x0_or_zeros()  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
         st.solution()
         return st.xk()
 

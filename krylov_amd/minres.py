@@ -113,13 +113,12 @@ def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter
-    x0_host = prob.zeros_like_b() if prob.x0 is None else prob.x0
 
     st = _MinresState(prob)
     rn0 = st.start()
     first = prob.colvals(rn0)
     if callback is not None:
-        callback(x0_host, np.array(first))
+        callback(prob.x0_or_zeros(), np.array(first))
     resnorms = [first]
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))

@@ -139,8 +139,10 @@ def _fingerprint(A):
 
 
 def clear_operator_cache():
-    """Release every cached device copy of a host matrix."""
+    """Release every cached device copy of a host matrix, and return the
+    device blocks freed so far to the runtime (kry_mem_release)."""
     _cache.clear()
+    _lib.empty_cache()
 
 
 def as_device_operator(A, device=None):

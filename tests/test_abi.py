@@ -47,6 +47,16 @@ def test_version_and_device_count_without_gpu():
     assert n >= 0
 
 
+def test_memory_stats_without_gpu():
+    import krylov_amd
+
+    s = krylov_amd.memory_stats()
+    assert set(s) == {"bytes_in_use", "bytes_cached", "reuses", "device_mallocs", "retire_syncs", "enabled"}
+    assert s["bytes_in_use"] >= 0 and s["bytes_cached"] >= 0
+    krylov_amd.empty_cache()  # nothing cached: a no-op, no device needed
+    assert krylov_amd.memory_stats()["bytes_cached"] == 0
+
+
 def test_no_device_fails_loudly():
     from krylov_amd import _lib
 

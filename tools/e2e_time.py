@@ -1,0 +1,93 @@
+"""End-to-end (host-array boundary) timing of the user-facing solvers on the
+metric matrix: krylov_amd.cg / gmres called with numpy b, returning numpy x,
+against the device-resident iteration rate the bench reports. Splits out the
+per-call pieces: Problem (b upload), the solve, the x download.
+
+    python3 tools/e2e_time.py [steps]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(steps=200):
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+
+    M = problems.stencil15_3d(216)
+    t0 = time.perf_counter()
+    A = krylov_amd.CsrOperator(M)
+    A.ctx.synchronize()
+    print(f"upload+image {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
+    b = np.ones(M.shape[0])
+    krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=8)  # warm-up
+    for _ in range(3):
+        t0 = time.perf_counter()
+        _, info = krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
+        t = time.perf_counter() - t0
+        print(f"cg maxiter={steps}: {1e3 * t:.1f} ms, {info.numsteps / t:.0f} it/s end to end", flush=True)
+    for _ in range(3):
+        t0 = time.perf_counter()
+        prob = _helpers.Problem(A, b, None, None)
+        t1 = time.perf_counter()
+        st = _CGState(prob)
+        st.start()
+        A.ctx.synchronize()
+        t2 = time.perf_counter()
+        x = st.get(0)
+        t3 = time.perf_counter()
+        print(f"  Problem (b upload) {1e3 * (t1 - t0):.1f} ms, state+start {1e3 * (t2 - t1):.1f} ms, "
+              f"x download {1e3 * (t3 - t2):.1f} ms", flush=True)
+        del st, prob, x
+    krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30)
+    for _ in range(3):
+        t0 = time.perf_counter()
+        krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30)
+        t = time.perf_counter() - t0
+        print(f"gmres(30): {1e3 * t:.1f} ms, {30 / t:.0f} it/s end to end", flush=True)
+    # per-phase host time of both drivers (each state method wrapped in a timer)
+    cgmod, gmmod = sys.modules["krylov_amd.cg"], sys.modules["krylov_amd.gmres"]
+
+    acc = {}
+
+    def wrap(cls, name):
+        f = getattr(cls, name)
+
+        def g(*a, **k):
+            t = time.perf_counter()
+            try:
+                return f(*a, **k)
+            finally:
+                acc[cls.__name__ + "." + name] = acc.get(cls.__name__ + "." + name, 0.0) + time.perf_counter() - t
+
+        setattr(cls, name, g)
+
+    for cls in (cgmod._CGState, gmmod._GmresState):
+        for name in ("__init__", "start", "set_criterion", "run", "get", "solution", "xk", "residual_norm2"):
+            if hasattr(cls, name):
+                wrap(cls, name)
+    ohelp = _helpers.Problem.__init__
+
+    def pinit(self, *a, **k):
+        t = time.perf_counter()
+        ohelp(self, *a, **k)
+        acc["Problem.__init__"] = acc.get("Problem.__init__", 0.0) + time.perf_counter() - t
+
+    _helpers.Problem.__init__ = pinit
+    for label, fn in (("cg", lambda: krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)),
+                      ("gmres", lambda: krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30))):
+        acc.clear()
+        t0 = time.perf_counter()
+        fn()
+        t = time.perf_counter() - t0
+        print(f"{label} phases (total {1e3 * t:.1f} ms): " +
+              ", ".join(f"{k} {1e3 * v:.1f}" for k, v in sorted(acc.items(), key=lambda kv: -kv[1])), flush=True)
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 200)
