@@ -211,6 +211,36 @@ def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"
             "n": R.shape[0], "nnz": int(R.nnz), "config": label}
 
 
+def run_end_to_end(A_host, steps):
+    """The reference API at the host-array boundary: krylov_amd.cg(A, b) and
+    gmres(A, b, maxiter=30) with numpy b in and numpy x out, on an operator
+    uploaded beforehand (CsrOperator). Includes the b upload (H2D), solver
+    setup, the per-chunk host syncs and the x download (D2H): the
+    PCIe-inclusive rate DESIGN.md (d) quotes. Median of 3 after a warm-up."""
+    import krylov_amd
+
+    A = krylov_amd.CsrOperator(A_host)
+    b = np.ones(A.n)
+    out = {}
+    for label, run, iters in (
+        ("cg", lambda: krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps), steps),
+        ("gmres30", lambda: krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30), 30),
+    ):
+        run()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, info = run()
+            ts.append(time.perf_counter() - t0)
+            assert info.numsteps == iters
+        t = float(np.median(ts))
+        out[f"{label}_it_per_s"] = iters / t
+        out[f"{label}_call_ms"] = 1e3 * t
+    out["includes"] = ("b upload (H2D), solver state setup, per-chunk host syncs, x download (D2H); the operator "
+                       "is uploaded once before (CsrOperator)")
+    return out
+
+
 def run_minres_cfg5(steps=100):
     import krylov_amd
     from krylov_amd import _helpers, problems
@@ -366,6 +396,7 @@ def main():
         out["gmres"] = g
         # north_star: GMRES(30) on the same (metric) matrix
         out["gmres_metric"] = run_gmres(A_host, f"metric 15-point {args.m}^3, GMRES(30) mgs, one cycle")
+        out["end_to_end"] = run_end_to_end(A_host, args.steps)
     if world == 1 and args.configs:
         extra = {}
         extra["cfg2_cg_poisson1000"] = run_cg_config(problems.poisson2d(1000), np.ones(1_000_000), 200, 10)
