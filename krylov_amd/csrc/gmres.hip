@@ -751,6 +751,8 @@ __global__ void gm_coef_kernel(const double *part, int P, int k, double *scal, d
   }
 }
 
+constexpr int kQrTile = 2048;  // doubles per LDS-staged array of gm_qr_kernel (3 x 16 KB)
+
 // h[k+1] = sqrt(<w, w>); invariance; Givens update of column `col`
 // (gmres.py:206-221); resnorm |y[col+1]|; stop test.
 template <typename S>
@@ -758,21 +760,40 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
                              double *Gc, double *Gs, int col, int maxiter, double *hist, Ctrl *ctrl, int step,
                              int hgiven = 0, double *gbuf = nullptr, int col_offset = 0, int total_k = 0,
                              double *Hs = nullptr) {
-  if (halted(ctrl, step)) return;
   __shared__ double red[kBlock];
   __shared__ double rn[kMaxCols];
+  __shared__ double qGc[kQrTile], qGs[kQrTile], qH[kQrTile];
   __shared__ int flag;
-  if (!hgiven) reduce_partials(part, P, k, red);  // else h[k+1] is already in h (Householder)
   const int c = threadIdx.x;
   const int64_t ld = (int64_t)maxiter * k;  // R row stride
+  const int T = kQrTile / k > 0 ? kQrTile / k : 1;  // rotations per LDS tile (below)
+  const int nt0 = col < T ? col : T;
+  // The step's independent loads go out together, before the first wait
+  // (each is a miss to data an earlier kernel wrote, ~1 us when chained):
+  // this thread's item of rotation tile 0, y[col], y[col + 1] and h[0].
+  const bool own0 = c < nt0 * k;
+  double pg0 = 0.0, ps0 = 0.0, ph0 = 0.0, py0 = 0.0, py1 = 0.0, pc0 = 0.0;
+  if (own0) {
+    pg0 = Gc[c];
+    ps0 = Gs[c];
+    ph0 = h[c + k];
+  }
+  if (c < k) {
+    py0 = y[(int64_t)col * k + c];
+    py1 = y[(int64_t)(col + 1) * k + c];
+    pc0 = h[c];
+  }
+  if (halted(ctrl, step)) return;
+  if (!hgiven) reduce_partials(part, P, k, red);  // else h[k+1] is already in h (Householder)
   if (c < k) {
     const S hk1 = hgiven ? (S)h[(int64_t)(col + 1) * k + c] : sqrt((S)red[c]);
     h[(int64_t)(col + 1) * k + c] = (double)hk1;
     red[c] = (double)hk1;
-    if (Hs)  // the Arnoldi relation's H[:col+2, col] (the reference's h column)
-      for (int i = 0; i <= col + 1; ++i) Hs[i * ld + (int64_t)col * k + c] = h[(int64_t)i * k + c];
   }
   __syncthreads();
+  if (Hs)  // the Arnoldi relation's H[:col+2, col] (the reference's h column)
+    for (int t = threadIdx.x; t < (col + 2) * k; t += blockDim.x)
+      Hs[(t / k) * ld + (int64_t)col * k + t % k] = h[t];
   // np.all(h[k+1] <= 1e-14) over the columns (arnoldi.py:187)
   if (threadIdx.x == 0) flag = 1;
   __syncthreads();
@@ -780,28 +801,56 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
   __syncthreads();
   const bool inv = flag != 0;
   __syncthreads();
+  // R[:col+2, col] = h[:col+2], then the previous rotations (gmres.py:208-210).
+  // Rotation i finalises R[i] and hands R[i+1] on: carry it in a register
+  // so the chain is arithmetic only (same operations, same bits). The
+  // rotations and the h column are first staged through LDS by the whole
+  // block, a tile at a time: the chain then waits on LDS, not on one global
+  // round trip per rotation (the R store of rotation i kept the loads of
+  // rotation i + 1 behind it: ~0.35 us per rotation, 10 us per step at j = 30).
+  S carry = c < k ? (S)pc0 : S(0);
+  {
+    for (int i0 = 0; i0 < col; i0 += T) {
+      const int nt = col - i0 < T ? col - i0 : T;
+      __syncthreads();
+      int t0 = threadIdx.x;
+      if (i0 == 0) {  // the prefetched item
+        if (own0) {
+          qGc[c] = pg0;
+          qGs[c] = ps0;
+          qH[c] = ph0;
+        }
+        t0 += blockDim.x;
+      }
+      for (int t = t0; t < nt * k; t += blockDim.x) {
+        const int64_t g = (int64_t)i0 * k + t;  // rotation i0 + t / k, column t % k
+        qGc[t] = Gc[g];
+        qGs[t] = Gs[g];
+        qH[t] = h[g + k];
+      }
+      __syncthreads();
+      if (c < k) {
+        for (int i = 0; i < nt; ++i) {
+          const S cc = (S)qGc[i * k + c], ss = (S)qGs[i * k + c];
+          const S r0 = carry, r1 = (S)qH[i * k + c];
+          const S a0 = cc * r0, a1 = ss * r1;
+          const S b0 = -ss * r0, b1 = cc * r1;
+          R[(int64_t)(i0 + i) * ld + (int64_t)col * k + c] = (double)(a0 + a1);
+          carry = b0 + b1;
+        }
+      }
+    }
+  }
   if (c < k) {
     const S hk1 = (S)red[c];
     scal[G_HSAFE * k + c] = (double)safe<S>(hk1);
-    // R[:col+2, col] = h[:col+2], then the previous rotations (gmres.py:208-210).
-    // Rotation i finalises R[i] and hands R[i+1] on: carry it in a register
-    // so the chain is arithmetic only (same operations, same bits).
-    S carry = (S)h[c];
-    for (int i = 0; i < col; ++i) {
-      const S cc = (S)Gc[(int64_t)i * k + c], ss = (S)Gs[(int64_t)i * k + c];
-      const S r0 = carry, r1 = (S)h[(int64_t)(i + 1) * k + c];
-      const S a0 = cc * r0, a1 = ss * r1;
-      const S b0 = -ss * r0, b1 = cc * r1;
-      R[i * ld + (int64_t)col * k + c] = (double)(a0 + a1);
-      carry = b0 + b1;
-    }
     S cs, sn, rr;
     lartg<S>(carry, (S)h[(int64_t)(col + 1) * k + c], cs, sn, rr);
     Gc[(int64_t)col * k + c] = (double)cs;
     Gs[(int64_t)col * k + c] = (double)sn;
     R[col * ld + (int64_t)col * k + c] = (double)rr;
     R[(col + 1) * ld + (int64_t)col * k + c] = 0.0;
-    const S y0 = (S)y[(int64_t)col * k + c], y1 = (S)y[(int64_t)(col + 1) * k + c];
+    const S y0 = (S)py0, y1 = (S)py1;
     const S a0 = cs * y0, a1 = sn * y1;
     const S b0 = -sn * y0, b1 = cs * y1;
     const S ny1 = b0 + b1;
