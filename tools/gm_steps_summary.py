@@ -28,12 +28,13 @@ def main(path, cycles=2):
     if spmv:
         s = np.array([dur(r) for r in spmv[-30 * cycles:]])
         print(f"spmv mean {s.mean():.1f} us ({spmv[-1]['Kernel_Name'][:60]})")
+    # every kernel of the trace, per cycle: tools/gm_steps.py runs one warm-up
+    # cycle before the timed ones, so the trace holds cycles + 1 of them
     other = {}
-    t0 = int(rows[-1]["End_Timestamp"])
     for r in rows:
         other.setdefault(r["Kernel_Name"][:50], []).append(dur(r))
     for k, v in sorted(other.items(), key=lambda kv: -sum(kv[1]))[:10]:
-        print(f"{sum(v) / cycles / 1e3:8.3f} ms/cycle  {len(v):5d} calls  {k}")
+        print(f"{sum(v) / (cycles + 1) / 1e3:8.3f} ms/cycle  {len(v):5d} calls  {k}")
 
 
 if __name__ == "__main__":
