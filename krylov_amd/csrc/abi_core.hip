@@ -83,19 +83,23 @@ size_t round_alloc(size_t total) {
   return (total + g - 1) / g * g;
 }
 
-// Caller holds the lock. Moves every pending block to the free list after
-// the device has finished all queued work.
-void retire_pending(DevicePool &P) {
-  if (P.pending.empty()) return;
+// Caller holds the lock, with `dev` the current device. Moves the device's
+// pending blocks to the free list after it has finished all queued work
+// (other devices' pending blocks stay: this sync says nothing about them).
+void retire_pending(DevicePool &P, int dev) {
   (void)hipDeviceSynchronize();
   ++P.syncs;
-  for (auto &b : P.pending) P.free_blocks.emplace(b.first, b.second);
-  P.pending.clear();
+  size_t keep = 0;
+  for (size_t i = 0; i < P.pending.size(); ++i) {
+    if (P.pending[i].first.device == dev) P.free_blocks.emplace(P.pending[i].first, P.pending[i].second);
+    else P.pending[keep++] = P.pending[i];
+  }
+  P.pending.resize(keep);
 }
 
-// Caller holds the lock. hipFree of every cached (free or pending) block.
+// Caller holds the lock. hipFree of every cached (free or pending) block
+// (hipFree waits for the block's device to finish its queued work).
 void release_cached(DevicePool &P) {
-  (void)hipDeviceSynchronize();
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (auto &b : P.pending) P.free_blocks.emplace(b.first, b.second);
@@ -140,7 +144,7 @@ void *dev_alloc(size_t bytes) {
   bool in_pending = false;
   for (auto &b : P.pending) in_pending = in_pending || (b.first.device == dev && b.first.bytes == key.bytes);
   if (in_pending) {
-    retire_pending(P);
+    retire_pending(P, dev);
     it = P.free_blocks.find(key);
     if (it != P.free_blocks.end()) return take(it);
   }
