@@ -179,10 +179,18 @@ struct BufSeg {
   // the 16-byte store has read them (seen as corrupted lanes 12-15 of every 16
   // in one element: tools/cgu_debug.py); for global stores it keeps the wait
   // states.
+  // The element offset is built from an opaque zero (a volatile s_mov):
+  // otherwise LLVM hoists the NV per-granule offsets of an epilogue that
+  // sits inside the pass loop out of it and spills them (the streamed MGS
+  // kernel at NV = 40 spilled 148 VGPRs: ~150 MB of scratch traffic per
+  // launch); recomputed here they cost two VALU ops per store.
   template <int W, int AUX = 0>
   __device__ __forceinline__ void store(int u, const V (&o)[W]) const {
     typedef V vec_t __attribute__((ext_vector_type(W)));
-    const int64_t e = ((int64_t)u * BLOCK + threadIdx.x) * W;
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const int tz = (int)threadIdx.x ^ z;  // everything per-thread below depends on z
+    const int64_t e = ((int64_t)u * BLOCK + tz) * W;
     if (e + W <= cnt) {
       vec_t t;
 #pragma unroll
