@@ -17,9 +17,14 @@ def main(which="metric", reps=2):
     import krylov_amd
     from krylov_amd import problems
 
-    M = problems.stencil15_3d(216) if which == "metric" else problems.random_nonsym(2_000_000)
+    if which.startswith("metric"):
+        M = problems.stencil15_3d(216)
+    else:
+        M = problems.random_nonsym(2_000_000)
+    dt = np.float32 if which.endswith("32") else np.float64  # metric32: the same matrix in fp32
+    M = M.astype(dt)
     A = krylov_amd.CsrOperator(M)
-    b = np.ones(M.shape[0])
+    b = np.ones(M.shape[0], dtype=dt)
     krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30)  # warm-up
     for _ in range(reps):
         t0 = time.perf_counter()
