@@ -1362,7 +1362,18 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
     const char *e = getenv("KRY_MGSL_NT");  // tuning override: subtrahend loads nontemporal (1) or not (0)
     return e ? atoi(e) != 0 : true;
   }();
-  if (s->mgsp_large && mgsl_nt) {
+  static const int mgsl_u_env = [] {
+    const char *e = getenv("KRY_MGSL_U");  // tuning override: granules per streamed chunk at NV >= 32 (2 or 4)
+    return e ? atoi(e) : 0;
+  }();
+  bool u4 = false;
+  if constexpr (sizeof(V) == 8) u4 = s->mgsp_large && mgsl_nt && mgsl_u_env == 4 && E / W >= 32;
+  if (u4) {
+    if constexpr (sizeof(V) == 8) {
+      if (E / W == 32) gol(gm_mgsl_kernel<V, 32, 4, true>);
+      else gol(gm_mgsl_kernel<V, 40, 4, true>);
+    }
+  } else if (s->mgsp_large && mgsl_nt) {
     switch (E / W) {
       case 12: gol(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>); break;
       case 16: gol(gm_mgsl_kernel<V, 16, mgsl_u<16>(), true>); break;
