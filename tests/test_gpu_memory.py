@@ -74,3 +74,35 @@ def test_empty_cache_releases_blocks():
     # and the library keeps working after a release
     _, info = krylov_amd.cg(A, np.ones(M.shape[0]), tol=1e-6)
     assert info.success
+
+
+def test_block_freed_with_work_in_flight_is_not_reused_early():
+    """A vector freed while SpMVs that read it are still queued on one stream,
+    and a block of the same size then taken on another context's stream: the
+    allocator retires the freed block only after a device sync, so the queued
+    SpMVs still read the old bytes (bitwise csr_matvec of the old x)."""
+    import krylov_amd
+    from krylov_amd import problems
+    from krylov_amd.device import Context, DeviceVector, get_context
+
+    M = problems.poisson2d(300)
+    n = M.shape[0]
+    ctx = get_context(0)
+    A = krylov_amd.CsrOperator(M)
+    x_host = np.linspace(1.0, 2.0, n).reshape(n, 1)
+    ctx.synchronize()
+    krylov_amd.empty_cache()  # no free block of x's size: z below can only take x's
+    x = DeviceVector.from_host(ctx, x_host)
+    y = DeviceVector(ctx, n, 1, np.float64)
+    for _ in range(64):
+        A.matvec_device(x, y)
+    before = krylov_amd.memory_stats()
+    x.close()  # the SpMVs above may still be queued
+    other = Context(0)  # a second stream on the same device
+    z = DeviceVector(other, n, 1, np.float64)
+    z.upload(np.full((n, 1), -7.0))
+    after = krylov_amd.memory_stats()
+    assert after["reuses"] > before["reuses"]
+    assert after["retire_syncs"] > before["retire_syncs"]
+    assert np.array_equal(y.to_host()[:, 0], M @ x_host[:, 0])
+    assert np.array_equal(z.to_host(), np.full((n, 1), -7.0))
