@@ -3,24 +3,36 @@
 Workload (BASELINE.json metric): CG on the 3-D 15-point stencil
 216^3 (n = 10,077,696, nnz = 149,770,936, fp64, int32 indices), b = ones,
 tol = 0 (fixed iteration count). One step = one CG iteration: the SpMV
-(+ <p,Ap>) launch, the one-block alpha kernel, the r pass (+ <r,r>) and the
-fused rho / y / p pass; no host sync inside a chunk (kry_cg_preferred_chunk:
-32 iterations here, 256 on the persistent small-n loop of cfg2).
+(+ <p,Ap>) launch and the one-launch update (alpha, r, rho, omega, y, p); no
+host sync inside a chunk (kry_cg_preferred_chunk: 32 iterations here, 256 on
+the persistent small-n loop of cfg2).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--quick]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--quick] [--configs]
+                  [--workload metric|cfg4] [--no-cpu]
 
 N > 1 (launched by torch.distributed.run): each rank solves its own RHS
-column of the same matrix on its own GPU (RHS sharding) with
+columns of the same matrix on its own GPU (RHS sharding) with
 one RCCL allreduce of the residual-norm vector per iteration for the global
-stop rule; value = total RHS-iterations per second (weak scaling).
+stop rule; value = total RHS-iterations per second (weak scaling). Unless
+--quick, every N also times cfg4 (Poisson 3163^2, 8 RHS per GPU, the
+BASELINE multi-GPU configuration) the same way ("cfg4_sharded");
+--workload cfg4 makes it the headline.
 
-Also reported (N = 1): the live SpMV roofline (HIP events around one SpMV
-launch in 4 of the timed region: two event records per timed launch cost the
-stream ~6 us, so timing all of them would slow the measured iteration), GMRES(30) on the cfg3 matrix, the secondary
-BASELINE configs (cfg2 CG Poisson 1000^2, cfg4 block CG 8 RHS on Poisson
-3163^2, cfg5 weighted fp32 MINRES 200^3), and the CPU baseline: the oracle
-(the reference iteration on NumPy/SciPy) on a bounded sample of the metric
-workload, rank 0 only.
+roofline: the CG SpMV kernel's bytes per launch are the bytes its image must
+move (the DIA image has no index stream; the compact SELL image 2 B of index
+per slot), divided by its average launch time from HIP events on the solver
+stream in a dedicated pass after the timed region (every launch of >= 64
+iterations); SURVEY's int32-CSR bytes S over the same time is reported
+beside it as effective_gbs / frac_vs_csr_S. spmv_general repeats the
+measurement on the same matrix with the DIA image disabled (KRY_SPMV_DIA=0):
+the compact SELL kernel that arbitrary sorted CSR takes.
+
+Also reported (N = 1): GMRES(30) on the cfg3 matrix and on the metric
+matrix, the reference API at the host-array boundary, the secondary BASELINE
+configs with --configs (cfg2 CG Poisson 1000^2, cfg4 block CG 8 RHS, cfg5
+weighted fp32 MINRES 200^3), and the CPU baseline: the oracle (the reference
+iteration on NumPy/SciPy) on a bounded sample of the metric workload, median
+of 5, rank 0 only.
 """
 import argparse
 import json
@@ -34,7 +46,6 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SPMV_TIMED_EVERY = 4  # the live SpMV timing samples one launch in 4 of the timed region
 
 
 def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
@@ -108,7 +119,12 @@ def _iterate(st, k, ncols, chunk=32):
         done += s
 
 
-def run_metric(A_host, steps, warmup, world, rank, local, pg):
+def run_cg_bench(A_host, B, steps, warmup, world, rank, local, pg, roofline_launches=64):
+    """CG on this rank's RHS block B (n or n x k) of A: warmup, then EXACTLY
+    `steps` iterations between barrier + device sync on both sides (max over
+    ranks), then a separate pass of max(steps, roofline_launches) iterations
+    with HIP events around every SpMV launch (the kernel's average launch
+    time; event records add stream time, so this pass is not the timed one)."""
     import krylov_amd
     from krylov_amd import _lib, distributed
     from krylov_amd.device import get_context
@@ -116,13 +132,9 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     ctx = get_context(local)
     A = krylov_amd.CsrOperator(A_host, device=local)
     comm = distributed.ShardComm.from_torch(device=local) if pg is not None else None
-    st, ncols = _cg_state(A, np.ones(A.n), comm, rank, world)
+    st, ncols = _cg_state(A, B, comm, rank, world)
     chunk = st.preferred_chunk()
     _iterate(st, warmup, ncols, chunk)
-    ctx.synchronize()
-    # HIP events around one SpMV launch in 4 (two event records per timed
-    # launch cost ~6 us of stream time; every launch of every kernel, 20 us)
-    ctx.profile(True, kernels=[_lib.PROF_SPMV], every=SPMV_TIMED_EVERY)
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -131,27 +143,67 @@ def run_metric(A_host, steps, warmup, world, rank, local, pg):
     t1 = time.perf_counter()
     barrier(pg)
     elapsed = allmax(pg, t1 - t0)
+    ctx.profile(True, kernels=[_lib.PROF_SPMV], every=1)
+    _iterate(st, max(steps, roofline_launches), ncols, chunk)
+    ctx.synchronize()
     cnt, spmv_ms = ctx.profile_read(_lib.PROF_SPMV)
     ctx.profile(False)
     del st
     if comm is not None:
         comm.close()
     layout = A.layout()
-    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_ms": spmv_ms, "n": A.n, "nnz": A.nnz, "layout": layout}
+    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_avg_s": spmv_ms / max(cnt, 1) / 1e3, "n": A.n,
+            "nnz": A.nnz, "layout": layout, "rhs": ncols // world, "persistent_loop": chunk == 256}
 
 
-def spmv_kernel_desc(layout):
-    """The CG SpMV kernel launch_spmv picks for k = 1 on this image, and the
-    bytes that image moves per launch (next to SURVEY's algorithmic S)."""
+def spmv_kernel_desc(layout, n):
+    """The CG SpMV kernel launch_spmv picks for k = 1 on this image, the
+    bytes that image must move per launch, and how they are counted."""
+    slots, slices = layout["slots"], layout["slices"]
     if layout["dia"]:
+        ds = layout["dia_slots"]
         return ("spmv_dia_kernel<double,double,16,SrcPlain,EpiApDot> (SELL-128/DIA diagonal-offset image, two rows "
                 "per lane: values only, one offset + two lane masks per slot column; Ap stored + <p,Ap> partials)",
-                "the DIA image moves dia_slots*8 + dia_slots/128*20 for the matrix, no index stream")
+                ds * 8 + ds / 128 * 20 + 2 * n * 8,
+                "dia_slots*8 (values) + dia_slots/128*20 (offset + two lane masks per slot column) + 2*n*8 "
+                "(p read once, Ap written once); no index stream")
     if layout["compact"]:
         return ("spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact index "
-                "image, Ap stored + <p,Ap> partials)", "the compact image moves nnz*(8+2) for the matrix")
+                "image: uint16 column deltas over per-slot-column int32 bases; Ap stored + <p,Ap> partials)",
+                slots * (8 + 2) + slots / 64 * 4 + slices * 12 + 2 * n * 8,
+                "slots*(8+2) (values + uint16 deltas) + slots/64*4 (column bases) + slices*12 (slice pointer + "
+                "width) + 2*n*8 (p read once, Ap written once)")
     return ("spmv_sell_kernel<double,double,int,1,16,false,SrcPlain,EpiApDot> (SELL-64 SpMV, int32 indices)",
-            "the SELL image moves slots*(8+4) for the matrix")
+            slots * (8 + 4) + slices * 12 + 2 * n * 8,
+            "slots*(8+4) + slices*12 + 2*n*8")
+
+
+def roofline_of(res, n, nnz, traffic=None):
+    """roofline object of one CG SpMV measurement (run_cg_bench)."""
+    kname, image_bytes, formula = spmv_kernel_desc(res["layout"], n)
+    t = res["spmv_avg_s"]
+    S = spmv_S(n, nnz)
+    traffic = traffic or {}
+    return {
+        "bound": "hbm",
+        "achieved": image_bytes / t / 1e9,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": image_bytes / t / 1e9 / HBM_PEAK_GBS,
+        "traffic": traffic.get("traffic_bytes_per_launch"),
+        "traffic_source": traffic.get("source"),
+        "kernel": kname,
+        "spmv_ms": 1e3 * t,
+        "bytes_per_launch": image_bytes,
+        "bytes_formula": formula,
+        "launches_timed": res["spmv_count"],
+        "timing": "HIP events on the solver stream around every SpMV launch of a pass after the timed region",
+        "csr_S_bytes": S,
+        "effective_gbs": S / t / 1e9,
+        "frac_vs_csr_S": S / t / 1e9 / HBM_PEAK_GBS,
+        "csr_S_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), the int32-CSR algorithmic bytes: an "
+                         "effective rate, not HBM traffic, for an image that moves fewer bytes)",
+    }
 
 
 def run_cg_config(A_host, B, steps, warmup=5):
@@ -268,51 +320,92 @@ def run_minres_cfg5(steps=100):
             "config": "cfg5 shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights (vectors f64 as in the reference)"}
 
 
-PMC_SUMMARY = "r02_pmc_traffic.json"
+PMC_SUMMARY = "r03_pmc_traffic.json"
 
 
 def pmc_traffic(n, nnz, kernel):
-    """HBM bytes per launch of the fused CG SpMV from the committed PMC
-    summary (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes, read side
+    """HBM bytes per launch of a CG SpMV kernel from the committed PMC summary
+    (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes, read side
     calibrated on a same-width stream of known size), if it was taken on this
-    workload and this kernel. PMC needs its own rocprofv3 runs, so it cannot
-    be live here."""
+    workload and this kernel. PMC needs its own rocprofv3 runs, so it cannot be
+    live here."""
     path = os.path.join(REPO, "profiles", PMC_SUMMARY)
     try:
         with open(path) as f:
             d = json.load(f)
     except OSError:
         return {}
-    if d.get("n") != n or d.get("nnz") != nnz or kernel.split("<")[0] not in d.get("kernel", ""):
+    if d.get("n") != n or d.get("nnz") != nnz:
         return {}
-    return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
-            "source": "profiles/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f "
-                      "calibrated)" % (PMC_SUMMARY, d["read_scale_from_calibration"])}
+    key = "dia" if kernel.startswith("spmv_dia_kernel") else "sell"
+    k = d.get("kernels", {}).get(key)
+    if not k:
+        return {}
+    return {"traffic_bytes_per_launch": k["traffic_bytes_per_launch"],
+            "source": "profiles/%s[%s] (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f calibrated)"
+                      % (PMC_SUMMARY, key, d["read_scale_from_calibration"])}
 
 
-def cpu_baseline(A_host, target_s=12.0):
+def cpu_baseline(A_host, runs=5, target_run_s=3.0):
     """The oracle (reference iteration on NumPy/SciPy, oracle/krylov_ref.py)
-    timed on this host: CG with tol=0 on the metric matrix, bounded sample."""
+    timed on this host: CG with tol=0 on the metric matrix. Each sample is one
+    cg call of `iters` iterations minus one call of 0 iterations (its setup
+    residual and final explicit residual), both the median of `runs` calls."""
     from oracle import krylov_ref
 
     b = np.ones(A_host.shape[0])
-    t0 = time.perf_counter()
-    krylov_ref.cg(A_host, b, tol=0.0, atol=0.0, maxiter=2)
-    t_cal = time.perf_counter() - t0
-    iters = int(max(3, min(60, target_s / max(t_cal / 3.0, 1e-3))))
-    t0 = time.perf_counter()
-    krylov_ref.cg(A_host, b, tol=0.0, atol=0.0, maxiter=iters)
-    t = time.perf_counter() - t0
+
+    def call(m):
+        t0 = time.perf_counter()
+        krylov_ref.cg(A_host, b, tol=0.0, atol=0.0, maxiter=m)
+        return time.perf_counter() - t0
+
+    t_setup = call(0)
+    t_cal = call(2) - t_setup
+    iters = int(max(3, min(40, target_run_s / max(t_cal / 2.0, 1e-3))))
+    t0s = [call(0) for _ in range(runs)]
+    tms = [call(iters) for _ in range(runs)]
+    per_it = (float(np.median(tms)) - float(np.median(t0s))) / iters
     threads = os.environ.get("OPENBLAS_NUM_THREADS") or os.environ.get("OMP_NUM_THREADS") or str(os.cpu_count())
     return {
-        "value": iters / t,
+        "value": 1.0 / per_it,
         "unit": "CG iters/s",
         "cores": int(threads),
         "kind": "port",
-        "sample": f"{iters} CG iterations (tol=0) of oracle/krylov_ref.cg on the full 216^3 15-pt matrix "
-                  f"(incl. setup residual + final explicit residual); SciPy csr_matvec 1 thread, "
-                  f"np.dot OpenBLAS {threads} threads",
+        "sample": f"median of {runs} oracle/krylov_ref.cg calls of {iters} iterations (tol=0) minus the median of "
+                  f"{runs} calls of 0 iterations (setup + explicit residual), full 216^3 15-pt matrix; SciPy "
+                  f"csr_matvec 1 thread, np.dot OpenBLAS {threads} threads",
+        "samples_s": tms,
+        "setup_samples_s": t0s,
     }
+
+
+def cfg4_rhs(n, rank, k=8):
+    """cfg4's per-GPU block: 8 standard-normal RHS columns (BASELINE cfg4:
+    B = default_rng(0).standard_normal((n, 64)), 8 per GPU; each rank draws
+    its own 8 columns from default_rng(rank) instead of slicing a 5 GB host
+    array: synthetic data of that shape, timed with tol = 0)."""
+    return np.random.default_rng(rank).standard_normal((n, k))
+
+
+def run_spmv_general(A_host, steps):
+    """The same CG SpMV measurement with the DIA image disabled
+    (KRY_SPMV_DIA=0 at upload): the compact SELL-64 kernel every sorted
+    int32 CSR matrix takes when it is not diagonal-structured."""
+    prev = os.environ.get("KRY_SPMV_DIA")
+    os.environ["KRY_SPMV_DIA"] = "0"
+    try:
+        res = run_cg_bench(A_host, np.ones(A_host.shape[0]), steps, 5, 1, 0, 0, None)
+    finally:
+        if prev is None:
+            del os.environ["KRY_SPMV_DIA"]
+        else:
+            os.environ["KRY_SPMV_DIA"] = prev
+    assert not res["layout"]["dia"]
+    n, nnz = A_host.shape[0], int(A_host.nnz)
+    roof = roofline_of(res, n, nnz, pmc_traffic(n, nnz, "spmv_sell_kernel"))
+    roof["cg_it_per_s"] = steps / res["elapsed"]
+    return roof
 
 
 def main():
@@ -321,7 +414,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=216, help="stencil edge (216 = BASELINE metric)")
-    ap.add_argument("--quick", action="store_true", help="metric only (no GMRES leg, no CPU baseline)")
+    ap.add_argument("--workload", choices=["metric", "cfg4"], default="metric",
+                    help="headline: metric CG (1 RHS per GPU) or cfg4 block CG (8 RHS per GPU, Poisson 3163^2)")
+    ap.add_argument("--quick", action="store_true", help="headline only (no other legs, no CPU baseline)")
     ap.add_argument("--configs", action="store_true", help="also time the secondary BASELINE configs (cfg2, cfg4, cfg5)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -335,62 +430,70 @@ def main():
 
     A_host = problems.stencil15_3d(args.m)
     n, nnz = A_host.shape[0], int(A_host.nnz)
-    res = run_metric(A_host, args.steps, args.warmup, world, rank, local, pg)
+    P3 = None
+    cfg4 = None
+    if args.workload == "cfg4" or not args.quick:
+        P3 = problems.poisson2d(3163)
+        cfg4 = run_cg_bench(P3, cfg4_rhs(P3.shape[0], rank), min(args.steps, 40), min(args.warmup, 5), world, rank,
+                            local, pg, roofline_launches=16)
+    if args.workload == "cfg4":
+        res, hn, hnnz = cfg4, P3.shape[0], int(P3.nnz)
+        workload = (f"krylov.cg block CG, 2-D 5-point Poisson 3163^2, {cfg4['rhs']} RHS per GPU (BASELINE cfg4), "
+                    "tol=0 fixed iterations")
+        steps_timed = min(args.steps, 40)
+    else:
+        res = run_cg_bench(A_host, np.ones(n), args.steps, args.warmup, world, rank, local, pg)
+        hn, hnnz = n, nnz
+        workload = f"krylov.cg, 3-D 15-point stencil {args.m}^3, one RHS per GPU, tol=0 fixed iterations"
+        steps_timed = args.steps
     T = res["elapsed"]
-    spmv_avg_s = res["spmv_ms"] / max(res["spmv_count"], 1) / 1e3
-    spmv_bytes = spmv_S(n, nnz)
-    achieved = spmv_bytes / spmv_avg_s / 1e9
-    kname, image_note = spmv_kernel_desc(res["layout"])
-    image_bytes = None
-    if res["layout"]["dia"]:  # the bytes the DIA image moves per launch (next to the algorithmic S)
-        ds = res["layout"]["dia_slots"]
-        image_bytes = ds * 8 + ds / 128 * 20 + 2 * n * 8
-    traffic = pmc_traffic(n, nnz, kname)
+    rhs = res["rhs"]
+    kname = spmv_kernel_desc(res["layout"], hn)[0]
+    roof = roofline_of(res, hn, hnnz, pmc_traffic(hn, hnnz, kname) if rhs == 1 else None)
     out = {
         "metric": "CG iters/sec + SpMV GB/s (fp64, n=10M, nnz=150M); GMRES(30) iters/sec",
-        "value": world * args.steps / T,
+        "value": world * rhs * steps_timed / T,
         "unit": "CG iters/s (RHS-iterations/s over all GPUs)",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": steps_timed,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * T / args.steps,
+        "ms_per_step": 1e3 * T / steps_timed,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY App. A generator, b = ones)",
+        "data": "synthetic (SURVEY App. A generator, b = ones)" if args.workload == "metric" else
+                "synthetic (SURVEY App. A poisson2d generator, standard-normal RHS)",
         "config": {
-            "workload": f"krylov.cg, 3-D 15-point stencil {args.m}^3, one RHS per GPU, tol=0 fixed iterations",
-            "n": n,
-            "nnz": nnz,
+            "workload": workload,
+            "n": hn,
+            "nnz": hnnz,
             "index": "int32",
-            "rhs_per_gpu": 1,
+            "rhs_per_gpu": rhs,
             "parallelism": f"rhs-shard x{world}" + (" (one RCCL resnorm allreduce per iteration)" if world > 1 else ""),
         },
-        "spmv_gbs": achieved,
-        "spmv_ms": 1e3 * spmv_avg_s,
-        "cg_iter_gbs_per_gpu": cg_iteration_bytes(n, nnz) * args.steps / T / 1e9,
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic.get("traffic_bytes_per_launch"),
-            "traffic_source": traffic.get("source"),
-            "kernel": kname,
-            "bytes_per_launch": spmv_bytes,
-            "bytes_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), int32-CSR algorithmic bytes; "
-                             + image_note + ")",
-            "launches_timed": res["spmv_count"],
-            "timing": f"HIP events on the solver stream around one SpMV launch in {SPMV_TIMED_EVERY} of the timed "
-                      f"region ({args.steps} launches)",
-            "image_bytes_per_launch": image_bytes,
-            "image_gbs": image_bytes / spmv_avg_s / 1e9 if image_bytes else None,
-            "image_frac": image_bytes / spmv_avg_s / 1e9 / HBM_PEAK_GBS if image_bytes else None,
-        },
+        "spmv_gbs": roof["achieved"],
+        "spmv_ms": roof["spmv_ms"],
+        "cg_iter_gbs_per_gpu": cg_iteration_bytes(hn, hnnz, rhs) * steps_timed / T / 1e9,
+        "roofline": roof,
     }
-    if world == 1 and not args.quick:
+    if cfg4 is not None and args.workload != "cfg4":
+        c4 = P3.shape[0]
+        out["cfg4_sharded"] = {
+            "rhs_it_per_s": world * cfg4["rhs"] * min(args.steps, 40) / cfg4["elapsed"],
+            "it_per_s": min(args.steps, 40) / cfg4["elapsed"],
+            "ms_per_it": 1e3 * cfg4["elapsed"] / min(args.steps, 40),
+            "rhs_per_gpu": cfg4["rhs"],
+            "n": c4,
+            "nnz": int(P3.nnz),
+            "spmv_ms": 1e3 * cfg4["spmv_avg_s"],
+            "iteration_gbs_per_gpu": cg_iteration_bytes(c4, int(P3.nnz), cfg4["rhs"]) * min(args.steps, 40)
+                                     / cfg4["elapsed"] / 1e9,
+            "config": "BASELINE cfg4: Poisson 3163^2 block CG, 8 RHS per GPU, one RCCL allreduce per iteration",
+        }
+    del P3
+    if world == 1 and not args.quick and args.workload == "metric":
+        out["spmv_general"] = run_spmv_general(A_host, args.steps)
         g = run_gmres()
         out["gmres30_it_per_s"] = g["it_per_s"]
         out["gmres"] = g
@@ -406,7 +509,7 @@ def main():
         del P3, B
         extra["cfg5_minres_fp32_weighted"] = run_minres_cfg5()
         out["extra"] = extra
-    if rank == 0 and world == 1 and not args.no_cpu and not args.quick:
+    if rank == 0 and world == 1 and not args.no_cpu and not args.quick and args.workload == "metric":
         out["cpu_baseline"] = cpu_baseline(A_host)
     if rank == 0:
         print(json.dumps(out), flush=True)

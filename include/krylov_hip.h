@@ -102,16 +102,21 @@ int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
  * that offset). Call once with null arrays to size them. */
 int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
                  int32_t *widths, int32_t *offsets, uint64_t *masks);
-/* The device image kry_csr_create built: info[0..6] = slices, slots,
- * irregular slices, compact (1 when the column indices are stored as uint16
- * deltas over per-slot-column int32 bases: every slot column spans <= 65534
- * columns, int32 indices and KRY_SELL_COMPACT != 0 in the environment), the
- * number of column blocks of the column-blocked image used by single-RHS
- * SpMVs on scattered sparsity (0 = none; KRY_SPMV_CB=0 disables), dia (1 when
- * the diagonal-offset image serves single-RHS SpMVs: int32 indices, every row
+/* The device image kry_csr_create built, size-checked: writes the first
+ * min(len, KRY_CSR_INFO_LEN) of info[0..6] = slices, slots, irregular slices,
+ * compact (1 when the column indices are stored as uint16 deltas over
+ * per-slot-column int32 bases: every slot column spans <= 65534 columns,
+ * int32 indices and KRY_SELL_COMPACT != 0 in the environment), the number of
+ * column blocks of the column-blocked image used by single-RHS SpMVs on
+ * scattered sparsity (0 = none; KRY_SPMV_CB=0 disables), dia (1 when the
+ * diagonal-offset image serves single-RHS SpMVs: int32 indices, every row
  * strictly sorted, the rows of each 64-row slice sharing a short list of
  * column offsets; KRY_SPMV_DIA=0 disables) and that image's slot count.
- * `info` must hold 7 values. */
+ * Fields added later go at the end, so a caller built against this header
+ * keeps working (kry_version() >= 101). */
+#define KRY_CSR_INFO_LEN 7
+int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len);
+/* The version-100 form: info[0..4] only (`info` holds 5 values). */
 int kry_csr_info(const kry_csr *A, int64_t *info);
 
 /* ---- vectors (n x k row-major blocks) ---------------------------------- */

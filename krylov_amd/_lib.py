@@ -56,6 +56,7 @@ _SIGNATURES = {
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
     "kry_dia_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
     "kry_csr_info": [_vp, _ip64],
+    "kry_csr_info_n": [_vp, _ip64, _i32],
     "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
     "kry_vec_destroy": [_vp],
     "kry_vec_upload": [_vp, _vp],

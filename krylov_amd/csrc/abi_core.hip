@@ -357,7 +357,9 @@ __global__ void lartg_kernel(int64_t count, const T *f, const T *g, T *c, T *s, 
 
 extern "C" {
 
-int kry_version(void) { return 100; }
+// 101: kry_csr_info_n (size-checked image info); kry_csr_info back to its
+// version-100 five values
+int kry_version(void) { return 101; }
 
 const char *kry_last_error(void) { return kry::g_last_error.c_str(); }
 
@@ -429,18 +431,16 @@ int kry_ctx_synchronize(kry_ctx *ctx) {
   KRY_API_END
 }
 
-int kry_csr_info(const kry_csr *A, int64_t *info) {
+int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len) {
   KRY_API_BEGIN
-  KRY_REQUIRE(A && info, KRY_EINVAL, "null argument");
-  info[0] = A->nslices;
-  info[1] = A->nslots;
-  info[2] = A->nirregular;
-  info[3] = A->compact ? 1 : 0;
-  info[4] = A->cb_nb;
-  info[5] = A->dia ? 1 : 0;
-  info[6] = A->dia_nslots;
+  KRY_REQUIRE(A && (info || len == 0) && len >= 0, KRY_EINVAL, "bad argument");
+  const int64_t all[KRY_CSR_INFO_LEN] = {A->nslices, A->nslots, A->nirregular, A->compact ? 1 : 0,
+                                         A->cb_nb,     A->dia ? 1 : 0, A->dia_nslots};
+  for (int i = 0; i < len && i < KRY_CSR_INFO_LEN; ++i) info[i] = all[i];
   KRY_API_END
 }
+
+int kry_csr_info(const kry_csr *A, int64_t *info) { return kry_csr_info_n(A, info, 5); }
 
 int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, int64_t *nslots,
                    int64_t *nirregular) {

@@ -346,7 +346,17 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int G = gridDim.x;
-  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_CGU_FAULT)
+  if (fault_step >= 0 && (fault_step & 0xffff) == step && (int)blockIdx.x == G - 1) {
+    // fault injection (tests, KRY_CGU_FAULT): the last block drops out, or, with
+    // KRY_CGU_FAULT_LATE = L, joins the exchange after ~L * 1024 polls (about when the
+    // others' shortened spin runs out: either outcome must be consistent)
+    const unsigned late = (unsigned)fault_step >> 16;
+    if (late == 0) return;
+    for (unsigned i = 0; i < late * 1024u; ++i) {
+      __builtin_amdgcn_s_sleep(1);
+      (void)__hip_atomic_load(words + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   const int64_t seg = (int64_t)NV * kUpdBlock * W;
   const int64_t e0 = (int64_t)blockIdx.x * seg;
@@ -392,9 +402,9 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   if (tid == 0) publish_partial(gran + 2 * blockIdx.x, tag, bp);
   ld2(sp, sy, 0, ca[0], cb[0]);  // chunk 0 of p and y travels during the exchange
   if (tid < 64) {
-    bool ok = sweep_partials(gran, G, tag, words, ctrl, &shv[0], spin_limit);
-    // a late block must not write after the others gave up
-    if (ok && __hip_atomic_load(words + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) ok = false;
+    // every block commits or every block aborts (decide_exchange): no block
+    // stores its segment after another gave up
+    const bool ok = sweep_partials<true>(gran, G, tag, words, ctrl, &shv[0], spin_limit);
     if (tid == 0) flag = ok ? 1 : 0;
   }
   __syncthreads();
@@ -946,6 +956,8 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
   if (step == 0) KRY_HIP(hipMemsetAsync(s->upd_words, 0, kUpdWords * 4, st));
   const char *fe = getenv("KRY_CGU_FAULT");  // fault injection (tests): step at which a block drops out
   int fault_step = fe ? atoi(fe) : -1;
+  const char *fl = getenv("KRY_CGU_FAULT_LATE");  // ... or joins late (decide_exchange tests)
+  if (fault_step >= 0 && fl) fault_step |= (atoi(fl) & 0x7fff) << 16;
   V *y = static_cast<V *>(s->y), *r = static_cast<V *>(s->r), *p = static_cast<V *>(s->p);
   const V *Ap = static_cast<const V *>(s->Ap);
   double *scal = s->scal, *hist = s->hist;
@@ -1244,6 +1256,15 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     upd = s->upd_used;
   } else if (persistent) {
     cgp_commit(s, done);
+  } else if (upd && c.status == KRY_EDEVICE && s->comm) {
+    // under a communicator every step posts one allreduce on every rank: a
+    // rank that reran part of its chunk alone would pair its collectives with
+    // other iterations of the other ranks (wrong global stop decisions, then
+    // a hang), so a timed-out exchange is a hard error here
+    s->upd_nv = 0;
+    ++s->upd_fallbacks;
+    throw Error{KRY_EDEVICE, "CG: the one-launch update's exchange timed out at step " + std::to_string(done) +
+                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
   } else if (upd && c.status == KRY_EDEVICE) {
     // a one-launch update timed out at step `done` and wrote nothing: the
     // steps before it stand; rerun the rest of the chunk launch per pass,

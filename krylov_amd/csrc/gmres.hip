@@ -1766,6 +1766,14 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   };
   Ctrl c;
   int done = run_chunk(max_steps, resnorms, &c);
+  if (c.status == KRY_EDEVICE && s->mgsp_E > 0 && s->comm) {
+    // one allreduce per step on every rank: no rank may rerun part of a chunk
+    // alone (see kry_cg_run)
+    s->mgsp_E = 0;
+    ++s->mgsp_fallbacks;
+    throw Error{KRY_EDEVICE, "GMRES: the persistent MGS exchange timed out at step " + std::to_string(done) +
+                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
+  }
   if (c.status == KRY_EDEVICE && s->mgsp_E > 0) {
     // the persistent MGS kernel timed out at step `done` (a block was not
     // resident) and halted the chunk there: keep the steps before it and run

@@ -302,7 +302,17 @@ __global__ __launch_bounds__(kMrBlock) void mr_upd_kernel(int64_t N, const doubl
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int G = gridDim.x;
-  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_MRU_FAULT)
+  if (fault_step >= 0 && (fault_step & 0xffff) == step && (int)blockIdx.x == G - 1) {
+    // fault injection (tests, KRY_MRU_FAULT): the last block drops out, or, with
+    // KRY_MRU_FAULT_LATE = L, joins the exchange after ~L * 1024 polls (about when the
+    // others' shortened spin runs out: either outcome must be consistent)
+    const unsigned late = (unsigned)fault_step >> 16;
+    if (late == 0) return;
+    for (unsigned i = 0; i < late * 1024u; ++i) {
+      __builtin_amdgcn_s_sleep(1);
+      (void)__hip_atomic_load(words + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   const int64_t seg = (int64_t)NV * kMrBlock * W;
   const int64_t e0 = (int64_t)blockIdx.x * seg;
@@ -362,8 +372,9 @@ __global__ __launch_bounds__(kMrBlock) void mr_upd_kernel(int64_t N, const doubl
   if (tid == 0) publish_partial(gran + 2 * blockIdx.x, tag, bp);
   ldB(0, 0);  // phase B's first chunk travels during the exchange
   if (tid < 64) {
-    bool ok = sweep_partials(gran, G, tag, words, ctrl, &shv[0], spin_limit);
-    if (ok && __hip_atomic_load(words + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) ok = false;
+    // every block commits or every block aborts (decide_exchange): no block
+    // stores its segment after another gave up
+    const bool ok = sweep_partials<true>(gran, G, tag, words, ctrl, &shv[0], spin_limit);
     if (tid == 0) flag = ok ? 1 : 0;
   }
   __syncthreads();
@@ -597,6 +608,8 @@ inline bool mru_launch(kry_minres *s, const double *w, const double *p, double *
   if (step == 0) KRY_HIP(hipMemsetAsync(s->upd_words, 0, kMrWords * 4, st));
   const char *fe = getenv("KRY_MRU_FAULT");  // fault injection (tests): step at which a block drops out
   int fault_step = fe ? atoi(fe) : -1;
+  const char *fl = getenv("KRY_MRU_FAULT_LATE");  // ... or joins late (decide_exchange tests)
+  if (fault_step >= 0 && fl) fault_step |= (atoi(fl) & 0x7fff) << 16;
   int64_t n = N;
   const double *wtp = s->w;
   double *yk = static_cast<double *>(s->yk), *scal = s->scal, *hist = s->hist;
@@ -886,6 +899,14 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   Ctrl c;
   int done = run_steps(max_steps, resnorms, &c);
   const bool upd = s->upd_used;
+  if (upd && c.status == KRY_EDEVICE && s->comm) {
+    // one allreduce per step on every rank: no rank may rerun part of a chunk
+    // alone (see kry_cg_run)
+    s->upd_nv = 0;
+    ++s->upd_fallbacks;
+    throw Error{KRY_EDEVICE, "MINRES: the one-launch step tail's exchange timed out at step " + std::to_string(done) +
+                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
+  }
   if (upd && c.status == KRY_EDEVICE) {
     // the one-launch step tail timed out at step `done` and wrote nothing:
     // keep the steps before it and rerun the rest with the separate kernels,

@@ -66,12 +66,37 @@ __device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned 
   __hip_atomic_store(g + 1, t | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0 only; returns the same value in every lane (false = timed out / aborted).
+// Commit / abort agreement of one exchange (kernels that update their inputs
+// in place after it: cg_upd_kernel, mr_upd_kernel). Word bar[10] records the
+// decision for the exchange tagged `tag` as tag * 4 + {1 abort, 2 commit}; the
+// first block to decide (a block that saw every partial: commit; a block
+// whose spin ran out: abort) wins by compare-and-swap, and every other block
+// follows it. So no block stores after another gave up, and a block whose
+// spin runs out after some block committed keeps waiting: every partial has
+// been published by then, so its sweep completes. bar[10] starts at 0 (the
+// host clears the words at the start of a chunk) and tags grow within it.
+constexpr unsigned kDecAbort = 1u, kDecCommit = 2u;
+__device__ inline unsigned decide_exchange(unsigned *bar, unsigned tag, unsigned want) {
+  unsigned old = __hip_atomic_load(bar + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while ((old >> 2) != tag) {
+    if (__hip_atomic_compare_exchange_strong(bar + 10, &old, tag * 4u + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return want;
+  }
+  return old & 3u;
+}
+
+// Wave 0 only; returns the same value in every lane (false = timed out /
+// aborted). AGREE: the commit / abort decision is shared by all blocks
+// (decide_exchange); otherwise a timed-out block only raises bar[9] and a
+// caller that has stored nothing yet re-checks it.
+template <bool AGREE = false>
 __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out,
                                       unsigned spin_limit = kSpinLimit) {
   const int lane = threadIdx.x;
   unsigned long long g[4][2];
   unsigned spins = 0;
+  bool committed = false;  // AGREE: another block has committed this exchange
   for (;;) {
     bool ok = true;
 #pragma unroll
@@ -86,15 +111,37 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(1);
     ++spins;
-    if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-      return false;
-    if (spins > spin_limit) {
+    if (committed) continue;
+    if ((spins & 255u) == 0) {
+      if (AGREE) {
+        const unsigned d = __hip_atomic_load(bar + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == tag * 4u + kDecAbort) return false;
+        if (d == tag * 4u + kDecCommit) committed = true;
+      } else if (__hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        return false;
+      }
+    }
+    if (spins > spin_limit && !committed) {
+      unsigned d = kDecAbort;
+      if (AGREE) {
+        if (lane == 0) d = decide_exchange(bar, tag, kDecAbort);
+        d = __shfl(d, 0);
+        if (d == kDecCommit) {
+          committed = true;
+          continue;
+        }
+      }
       if (lane == 0) {
         __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
     }
+  }
+  if (AGREE) {
+    unsigned d = 0;
+    if (lane == 0) d = decide_exchange(bar, tag, kDecCommit);
+    if (__shfl(d, 0) != kDecCommit) return false;
   }
   double s = 0.0;
 #pragma unroll

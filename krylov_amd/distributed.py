@@ -10,9 +10,12 @@ xGMI) of the zero-padded residual-norm vector so that every rank applies the
 global stop rule and records the global history. The result equals the
 unsharded block solve (same per-column recurrences, same stop step).
 
-One process per GPU (launched by ``torch.distributed.run``); the RCCL
-unique id is exchanged over whatever process group the caller has (gloo is
-enough: it is control-plane only).
+One process per GPU. The RCCL unique id is exchanged either over a
+``torch.distributed`` process group the caller already has (any backend:
+control plane only, ``ShardComm.from_torch``) or without PyTorch, through a
+file every rank of the node can see (``ShardComm.from_file``). The rank
+bookkeeping and the outer loop are ``krylov_amd.shard`` (pure NumPy, the code
+the gloo CPU tests run); this module binds them to the device states.
 """
 import ctypes
 import weakref
@@ -24,6 +27,7 @@ from ._helpers import Info, Problem
 from ._lib import check, lib
 from .cg import _CGState
 from .device import get_context
+from .shard import ShardLayout, drive, file_rendezvous
 
 
 class ShardComm:
@@ -61,6 +65,14 @@ class ShardComm:
         uid = idt.numpy().astype(np.uint8).tobytes()
         return cls(rank, world, uid, device=device)
 
+    @classmethod
+    def from_file(cls, path, rank, world, device=None, timeout=120.0):
+        """Create the communicator without PyTorch: rank 0 writes the unique id
+        to ``path`` (a fresh file name on a file system every rank sees, e.g.
+        under /dev/shm), the others read it (``shard.file_rendezvous``)."""
+        uid = file_rendezvous(path, int(rank), cls.unique_id, timeout=timeout)
+        return cls(rank, world, uid, device=device)
+
     def allreduce(self, values):
         """Sum a small float64 vector over ranks (setup-time exchanges)."""
         v = np.ascontiguousarray(values, dtype=np.float64).copy()
@@ -69,6 +81,39 @@ class ShardComm:
 
     def close(self):
         self._fin()
+
+
+def _block(B):
+    B = np.asarray(B)
+    return B[:, None] if B.ndim == 1 else B
+
+
+class _Engine:
+    """A device solver state in the shape ``shard.drive`` expects."""
+
+    def __init__(self, st, run_fn, total, start_fn, norm2_fn):
+        self.st, self._run, self.total = st, run_fn, total
+        self._start, self._norm2 = start_fn, norm2_fn
+
+    def start_norms(self):
+        return self._start()
+
+    def set_criterion(self, crit_full):
+        self.st.set_criterion(crit_full)
+
+    def run(self, steps):
+        return self._run(steps)
+
+    def residual_norm2(self):
+        return self._norm2()
+
+
+def _run_global(lib_run, h, steps, total):
+    out = np.zeros((max(steps, 1), total))
+    done = ctypes.c_int32()
+    inv = ctypes.c_int32()
+    check(lib_run(h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
+    return out[: done.value], bool(inv.value)
 
 
 def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None):
@@ -81,66 +126,17 @@ def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None)
     """
     if callback is not None:
         raise NotImplementedError("callbacks are not supported on the sharded path")
-    B = np.asarray(B)
-    if B.ndim == 1:
-        B = B[:, None]
-    prob = Problem(A, B, x0, None, device=comm.ctx.device)
-    kc, kp, world = prob.kc, prob.kpad, comm.world
-    total = kp * world
-    off = kp * comm.rank
+    prob = Problem(A, _block(B), x0, None, device=comm.ctx.device)
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-
-    def glob(local_vals):
-        """local kpad values -> global zero-padded vector, summed over ranks"""
-        v = np.zeros(total)
-        v[off:off + kp] = local_vals
-        return comm.allreduce(v)
-
-    real = np.concatenate([np.arange(r * kp, r * kp + kc) for r in range(world)])
-
     st = _CGState(prob)
-    check(lib.kry_cg_attach_comm(st.h, comm.handle, off, total))
-    rho0 = st.start()
-    rn0 = glob(np.sqrt(rho0.astype(prob.inner_dtype)).astype(np.float64))
-    resnorms = [rn0[real]]
-    criterion = np.maximum(tol * resnorms[0], atol)
-    crit_full = np.full(total, np.inf)
-    crit_full[real] = criterion
-    st.set_criterion(crit_full)
-    k = 0
-    success = False
-    while True:
-        if np.all(resnorms[-1] <= criterion):
-            sq = glob(st.residual_norm2())
-            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
-            if np.all(resnorms[-1] <= criterion):
-                success = True
-                break
-        if k == maxiter:
-            break
-        hist = st.run(min(_helpers.CHUNK, maxiter - k), ncols=total)
-        for row in hist:
-            resnorms.append(np.asarray(row)[real])
-            k += 1
+    check(lib.kry_cg_attach_comm(st.h, comm.handle, lay.off, lay.total))
+    eng = _Engine(st, lambda steps: (st.run(steps, ncols=lay.total), False), lay.total,
+                  lambda: np.sqrt(st.start().astype(prob.inner_dtype)).astype(np.float64), st.residual_norm2)
+    success, k, resnorms = drive(eng, lay, comm.allreduce, tol, atol, maxiter, prob.inner_dtype, _helpers.CHUNK)
     xk = prob.unpad_vec(st.get(0), prob.r0_dtype)
     ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 2 + 2 * k}
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)
-
-
-def _shard_layout(prob, comm):
-    kp, world = prob.kpad, comm.world
-    total = kp * world
-    off = kp * comm.rank
-    real = np.concatenate([np.arange(r * kp, r * kp + prob.kc) for r in range(world)])
-    return total, off, real
-
-
-def _run_global(lib_run, h, steps, total):
-    out = np.zeros((max(steps, 1), total))
-    done = ctypes.c_int32()
-    inv = ctypes.c_int32()
-    check(lib_run(h, int(steps), ctypes.byref(done), _lib.dptr(out), ctypes.byref(inv)))
-    return out[: done.value], bool(inv.value)
 
 
 def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"):
@@ -155,42 +151,19 @@ def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"
     if not ortho.startswith("mgs"):
         raise NotImplementedError("the sharded path runs MGS Arnoldi (Householder is single right-hand side)")
     sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
-    B = np.asarray(B)
-    if B.ndim == 1:
-        B = B[:, None]
-    prob = Problem(A, B, x0, None, device=comm.ctx.device)
+    prob = Problem(A, _block(B), x0, None, device=comm.ctx.device)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-    total, off, real = _shard_layout(prob, comm)
-
-    def glob(local_vals):
-        v = np.zeros(total)
-        v[off:off + prob.kpad] = local_vals
-        return comm.allreduce(v)
-
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
     st = _GmresState(prob, maxiter, sweeps)
-    check(lib.kry_gmres_attach_comm(st.h, comm.handle, off, total))
-    rn0 = glob(st.start())
-    resnorms = [rn0[real].astype(prob.inner_dtype).astype(np.float64)]
-    criterion = np.maximum(tol * resnorms[0], atol)
-    crit_full = np.full(total, np.inf)
-    crit_full[real] = criterion
-    st.set_criterion(crit_full)
-    k = 0
-    success = False
-    while True:
-        if np.all(resnorms[-1] <= criterion):
-            st.solution()
-            sq = glob(st.residual_norm2())
-            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
-            if np.all(resnorms[-1] <= criterion):
-                success = True
-                break
-        if k == maxiter:
-            break
-        hist, _ = _run_global(lib.kry_gmres_run, st.h, min(_helpers.CHUNK, maxiter - k), total)
-        for row in hist:
-            resnorms.append(np.asarray(row)[real].astype(prob.inner_dtype).astype(np.float64))
-            k += 1
+    check(lib.kry_gmres_attach_comm(st.h, comm.handle, lay.off, lay.total))
+
+    def norm2():
+        st.solution()  # the explicit residual of x0 + V R^-1 y (gmres.py:197-199)
+        return st.residual_norm2()
+
+    eng = _Engine(st, lambda steps: _run_global(lib.kry_gmres_run, st.h, steps, lay.total), lay.total, st.start,
+                  norm2)
+    success, k, resnorms = drive(eng, lay, comm.allreduce, tol, atol, maxiter, prob.inner_dtype, _helpers.CHUNK)
     if k == 0:
         xk = prob.zeros_like_b() if prob.x0 is None else prob.x0
     else:
@@ -208,41 +181,14 @@ def minres(A, B, comm, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None
     Returns ``(xk_local or None, Info)`` with the global history."""
     from .minres import _MinresState
 
-    B = np.asarray(B)
-    if B.ndim == 1:
-        B = B[:, None]
-    prob = Problem(A, B, x0, inner, device=comm.ctx.device)
+    prob = Problem(A, _block(B), x0, inner, device=comm.ctx.device)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-    total, off, real = _shard_layout(prob, comm)
-
-    def glob(local_vals):
-        v = np.zeros(total)
-        v[off:off + prob.kpad] = local_vals
-        return comm.allreduce(v)
-
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
     st = _MinresState(prob)
-    check(lib.kry_minres_attach_comm(st.h, comm.handle, off, total))
-    rn0 = glob(st.start())
-    resnorms = [rn0[real].astype(prob.inner_dtype).astype(np.float64)]
-    criterion = np.maximum(tol * resnorms[0], atol)
-    crit_full = np.full(total, np.inf)
-    crit_full[real] = criterion
-    st.set_criterion(crit_full)
-    k = 0
-    success = False
-    while True:
-        if np.all(resnorms[-1] <= criterion):
-            sq = glob(st.residual_norm2())
-            resnorms[-1] = np.sqrt(sq[real].astype(prob.inner_dtype)).astype(np.float64)
-            if np.all(resnorms[-1] <= criterion):
-                success = True
-                break
-        if k == maxiter:
-            break
-        hist, _ = _run_global(lib.kry_minres_run, st.h, min(_helpers.CHUNK, maxiter - k), total)
-        for row in hist:
-            resnorms.append(np.asarray(row)[real].astype(prob.inner_dtype).astype(np.float64))
-            k += 1
+    check(lib.kry_minres_attach_comm(st.h, comm.handle, lay.off, lay.total))
+    eng = _Engine(st, lambda steps: _run_global(lib.kry_minres_run, st.h, steps, lay.total), lay.total, st.start,
+                  st.residual_norm2)
+    success, k, resnorms = drive(eng, lay, comm.allreduce, tol, atol, maxiter, prob.inner_dtype, _helpers.CHUNK)
     xk = st.xk()
     ops = {"A": 1 + k, "M": 2 + k, "Ml": 2 + k, "Mr": 1 + k, "inner": 2 + 2 * k, "axpy": 4 + 8 * k}
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)

@@ -159,6 +159,14 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
 
     ``ortho``: "mgs", "mgsK" (K MGS sweeps) or "householder" (Householder
     Arnoldi, arnoldi.py:33-104, one right-hand side, default inner, no M)."""
+    return _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback)
+
+
+def _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback, tol_of_r0=None):
+    """``gmres`` proper. ``tol_of_r0`` (restarts only) maps the device's
+    initial residual norm ``||Ml (b - A x0)||`` to the ``tol`` this call is
+    given, for a caller that chooses ``tol`` from that norm (gmres_restarted):
+    the norm is then read once, not recomputed on the host."""
     if ortho.startswith("mgs"):
         sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
     elif ortho == "householder":
@@ -182,6 +190,8 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
     if callback is not None:
         # the reference passes Ml_r0 = Ml (b - A x0) here (gmres.py:143-144)
         callback(prob.x0_or_zeros(), prob.apply_host("Ml", prob.b - prob.A @ prob.x0_or_zeros()))
+    if tol_of_r0 is not None:
+        tol = tol_of_r0(resnorms[0])
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))
 
@@ -232,29 +242,46 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)
 
 
-def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycles=100, ortho="mgs", inner=None):
-    """Restarted GMRES(restart): the reference's x0-chaining of ``gmres`` with
-    ``maxiter=restart`` (SURVEY §5 checkpoint/resume). The matrix is uploaded
-    once. Returns ``(x, infos)`` with one ``Info`` per cycle; the stop test of
-    every cycle uses ``tol`` relative to the residual at the start of the run.
+def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycles=100, ortho="mgs", M=None,
+                    Ml=None, Mr=None, inner=None, callback=None):
+    """Restarted GMRES(restart): the reference's ``gmres`` (``gmres.py:41-54``,
+    no restart parameter of its own) chained through ``x0``, one call of
+    ``maxiter=restart`` per cycle, exactly as the reference's restart fixture
+    drives it (tests/golden/make_golden.py, ``gmres_restart_*``):
+
+        cycle c:  gmres(A, b, x0=x_c, maxiter=restart,
+                        tol=tol * ||b|| / max(||b - A x_c||, 1e-300), atol=atol)
+                  x_{c+1} = info.xk; stop after the first cycle with success
+
+    so every cycle's criterion is ``tol * ||b||`` (relative to b, not to the
+    cycle's start) and the run stops when ``||b - A x|| <= tol ||b||``.
+    ``||b - A x_c||`` is the device's own initial residual norm of the cycle
+    (the norm of the Euclidean or ``WeightedInner`` inner product; with Ml,
+    of ``Ml (b - A x_c)``); ``||b||`` is the same norm of b, taken on the host
+    as ``np.linalg.norm`` (default inner) or ``sqrt(inner(b, b))``. The operator
+    is uploaded once.
+
+    Returns ``(x, infos)``: the last iterate and one ``Info`` per cycle; the
+    chained history is ``sum(info.resnorms for info in infos)``.
     """
     from .sparse import as_device_operator
 
     Aop = as_device_operator(A)
     b = np.asarray(b)
+    if inner is None:
+        bnorm = np.linalg.norm(b, axis=0)
+    else:
+        bnorm = np.sqrt(np.asarray(inner(b, b)).real)
     x = np.zeros_like(b) if x0 is None else np.asarray(x0)
+
+    def tol_of_r0(r0):
+        return tol * bnorm / np.maximum(r0, 1e-300)
+
     infos = []
-    r0 = None
     for _ in range(max_cycles):
-        if r0 is None:
-            _, info0 = gmres(Aop, b, x0=x, maxiter=0, tol=0.0, atol=0.0, ortho=ortho, inner=inner)
-            r0 = info0.resnorms[0]
-        cur = None
-        _, info = gmres(Aop, b, x0=x, maxiter=restart, tol=0.0, atol=np.maximum(tol * r0, atol), ortho=ortho,
-                        inner=inner)
+        _, info = _gmres(Aop, b, M, Ml, Mr, inner, ortho, x, tol, atol, restart, callback, tol_of_r0=tol_of_r0)
         infos.append(info)
         x = info.xk
-        cur = info.resnorms[-1]
-        if info.success or np.all(cur <= np.maximum(tol * r0, atol)):
+        if info.success:
             break
     return x, infos

@@ -74,7 +74,7 @@ class CsrOperator:
         """The device image: {"slices", "slots", "irregular", "compact",
         "col_blocks", "dia", "dia_slots"}."""
         info = np.zeros(7, dtype=np.int64)
-        check(lib.kry_csr_info(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        check(lib.kry_csr_info_n(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 7))
         return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3]),
                 "col_blocks": int(info[4]), "dia": bool(info[5]), "dia_slots": int(info[6])}
 

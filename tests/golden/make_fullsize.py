@@ -46,6 +46,35 @@ def _store(prefix, sol, info, out):
     out[f"{prefix}_xsample"] = x[sample_idx(x.shape[0])]
 
 
+def restart_chain(krylov, A, b, restart, tol, max_cycles, quiet):
+    """GMRES(restart) by x0-chaining, the same loop as make_golden.py's
+    gmres_restart_* fixture: cycle c calls gmres(A, b, x0=x_c, maxiter=restart,
+    tol=tol ||b|| / ||b - A x_c||) until success or max_cycles."""
+    x = np.zeros_like(b)
+    bnorm = np.linalg.norm(b)
+    hist, steps, succ = [], [], []
+    for _ in range(max_cycles):
+        with quiet:
+            _, info = krylov.gmres(A, b, x0=x, maxiter=restart, tol=tol * bnorm / max(np.linalg.norm(b - A @ x), 1e-300))
+        hist.extend(np.asarray(info.resnorms, dtype=np.float64))
+        steps.append(info.numsteps)
+        succ.append(info.success)
+        x = info.xk
+        print(f"  cycle {len(steps)}: {info.numsteps} steps, last {hist[-1]:.3e}", flush=True)
+        if info.success:
+            break
+    return np.array(hist), np.array(steps), np.array(succ), x
+
+
+def _store_restart(prefix, hist, steps, succ, x, out):
+    out[f"{prefix}_hist"] = hist
+    out[f"{prefix}_cycle_steps"] = steps
+    out[f"{prefix}_cycle_success"] = succ
+    xa = np.abs(x.astype(np.float64))
+    out[f"{prefix}_xstats"] = np.array([xa.sum(axis=0), np.sqrt((xa * xa).sum(axis=0)), xa.max(axis=0)])
+    out[f"{prefix}_xsample"] = x[sample_idx(x.shape[0])]
+
+
 def main():
     krylov = _import_reference()
     quiet = contextlib.redirect_stdout(io.StringIO())  # gmres.py:201-205 prints every iteration
@@ -55,7 +84,7 @@ def main():
     def want(name):
         return not only or name in only
 
-    if want("metric_cg") or want("metric_gmres30"):
+    if want("metric_cg") or want("metric_gmres30") or want("metric_gmres30_restart"):
         A = problems.stencil15_3d(216)
         b = np.ones(A.shape[0])
         if want("metric_cg"):
@@ -69,6 +98,12 @@ def main():
                 sol, info = krylov.gmres(A, b, maxiter=30, tol=0.0)  # north_star: GMRES(30) on the same matrix
             _store("metric_gmres30", sol, info, out)
             print("metric_gmres30", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        if want("metric_gmres30_restart"):
+            # north_star: GMRES(30) on the metric matrix, restarted; bounded to
+            # 10 cycles of the 1e-8 chaining (it needs far more to converge)
+            t = time.time()
+            _store_restart("metric_gmres30_restart", *restart_chain(krylov, A, b, 30, 1e-8, 10, quiet), out)
+            print("metric_gmres30_restart", f"{time.time() - t:.0f}s", flush=True)
         del A
     if want("cfg2_cg"):
         P = problems.poisson2d(1000)
@@ -84,6 +119,13 @@ def main():
             sol, info = krylov.gmres(R, np.ones(R.shape[0]), maxiter=30, tol=0.0)
         _store("cfg3_gmres30", sol, info, out)
         print("cfg3_gmres30", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
+        del R
+    if want("cfg3_gmres30_restart"):
+        # cfg3: GMRES restart=30 converging, chained to 1e-8 relative
+        R = problems.random_nonsym(2_000_000)
+        t = time.time()
+        _store_restart("cfg3_gmres30_restart", *restart_chain(krylov, R, np.ones(R.shape[0]), 30, 1e-8, 20, quiet), out)
+        print("cfg3_gmres30_restart", f"{time.time() - t:.0f}s", flush=True)
         del R
     if want("cfg4_blockcg"):
         P = problems.poisson2d(3163)
@@ -105,7 +147,9 @@ def main():
             sol, info = krylov.minres(W, bW, inner=inner, tol=0.0, maxiter=100)
         _store("cfg5_minres", sol, info, out)
         print("cfg5_minres", info.numsteps, f"{time.time() - t:.0f}s", flush=True)
-    path = os.path.join(HERE, "fullsize.npz" if not only else "fullsize_part.npz")
+    path = os.path.join(HERE, "fullsize.npz")
+    if only and os.path.exists(path):  # regenerate the named cases, keep the rest
+        out = {**dict(np.load(path)), **out}
     np.savez_compressed(path, **out)
     print("written", path)
 

@@ -33,7 +33,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
-from krylov_amd import problems  # noqa: E402
+
+def _load_problems():
+    """krylov_amd/problems.py by path: the generators are plain NumPy/SciPy, and
+    importing the package would load libkrylov_hip.so (not needed here, and
+    mid-rebuild while a long fixture run is going)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_kry_problems", os.path.join(REPO, "krylov_amd", "problems.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+problems = _load_problems()
 
 
 def _import_reference():

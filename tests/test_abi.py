@@ -42,7 +42,7 @@ def test_library_is_gfx950_code_object():
 def test_version_and_device_count_without_gpu():
     from krylov_amd import _lib
 
-    assert _lib.lib.kry_version() >= 100
+    assert _lib.lib.kry_version() >= 101
     n = _lib.device_count()
     assert n >= 0
 

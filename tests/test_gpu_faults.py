@@ -141,6 +141,53 @@ def test_cg_update_kernel_timeout_falls_back(monkeypatch, fault_step):
     assert st.update_path() == (False, 1)
 
 
+@pytest.mark.parametrize("late", [1, 3, 4, 6])
+def test_cg_update_kernel_late_block_all_or_nothing(monkeypatch, late):
+    """The last block joins the exchange late, about when the others' spin
+    runs out (KRY_CGU_FAULT_LATE): the blocks agree on commit or abort
+    (decide_exchange), so whichever way the race goes no block stores y / p /
+    r after another gave up, and the solve equals a clean one."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    R = problems.poisson2d(300)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(15).standard_normal(R.shape[0])
+    _, clean = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.setenv("KRY_CGU_FAULT", "2")
+    monkeypatch.setenv("KRY_CGU_FAULT_LATE", str(late))
+    _, faulted = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    assert faulted.numsteps == clean.numsteps
+    f, c = np.asarray(faulted.resnorms), np.asarray(clean.resnorms)
+    np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-10)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-10, atol=1e-12 * np.abs(clean.xk).max())
+
+
+def test_cg_update_kernel_timeout_under_communicator_is_an_error(monkeypatch):
+    """Under a communicator a rank must not rerun part of a chunk alone (its
+    allreduces would pair with other iterations of the other ranks): a
+    timed-out exchange of the one-launch update raises instead (1-rank RCCL
+    communicator; the update kernel forced with KRY_CG_PERSIST=0)."""
+    from krylov_amd import distributed, problems
+    import krylov_amd
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    P = krylov_amd.CsrOperator(problems.poisson2d(300))
+    b = np.random.default_rng(16).standard_normal((P.shape[0], 1))
+    comm = distributed.ShardComm(0, 1, distributed.ShardComm.unique_id())
+    try:
+        monkeypatch.setenv("KRY_CGU_FAULT", "1")
+        with pytest.raises(RuntimeError, match="cannot rerun alone"):
+            distributed.cg(P, b, comm, tol=1e-9, maxiter=100)
+        monkeypatch.delenv("KRY_CGU_FAULT")
+        _, info = distributed.cg(P, b, comm, tol=1e-9, maxiter=100)
+        _, ref = krylov_amd.cg(P, b, tol=1e-9, maxiter=100)
+        np.testing.assert_array_equal(np.asarray(info.resnorms), np.asarray(ref.resnorms))
+    finally:
+        comm.close()
+
+
 def test_cg_update_kernel_matches_separate_passes(monkeypatch):
     """n = 2.0 M (Poisson 1414^2, above the persistent loop's 1 M): the
     one-launch update against the alpha / r / yp passes (KRY_CG_UPD=0) and

@@ -63,8 +63,13 @@ def test_spmv_int64_image_through_abi(golden, key):
                                        _lib.dtype_code(dv.dtype), _lib.KRY_I64, ctypes.byref(h)))
     try:
         info = np.zeros(7, dtype=np.int64)
-        _lib.check(_lib.lib.kry_csr_info(h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        _lib.check(_lib.lib.kry_csr_info_n(h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 7))
         assert info[3] == 0
+        # the version-100 entry point writes its five values and nothing past them
+        info5 = np.full(8, -7, dtype=np.int64)
+        _lib.check(_lib.lib.kry_csr_info(h, info5.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        np.testing.assert_array_equal(info5[:5], info[:5])
+        assert np.all(info5[5:] == -7)
         x = DeviceVector.from_host(ctx, d[f"{key}_x"])
         y = DeviceVector(ctx, n, 1, dv.dtype)
         _lib.check(_lib.lib.kry_spmv(ctx.handle, h, x.handle, y.handle))

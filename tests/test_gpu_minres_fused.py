@@ -85,3 +85,25 @@ def test_fused_tail_timeout_falls_back(fault_step, monkeypatch):
     st = _state(A, b)
     h, _ = st.run(8)
     assert len(h) == 8 and st.update_path() == (True, 1)
+
+
+@pytest.mark.parametrize("late", [1, 3, 4, 6])
+def test_fused_tail_late_block_all_or_nothing(late, monkeypatch):
+    """A block that joins the exchange late, about when the others' spin runs
+    out (KRY_MRU_FAULT_LATE): every block commits or every block aborts
+    (decide_exchange), so whichever way the race goes the history and iterate
+    equal a clean solve's; a split decision would leave a partly updated step
+    behind the rerun."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    P = problems.poisson2d(150)
+    b = np.random.default_rng(23).standard_normal(P.shape[0])
+    A = krylov_amd.CsrOperator(P)
+    _, clean = krylov_amd.minres(A, b, tol=1e-9, maxiter=300)
+    monkeypatch.setenv("KRY_MRU_FAULT", "3")
+    monkeypatch.setenv("KRY_MRU_FAULT_LATE", str(late))
+    _, faulted = krylov_amd.minres(A, b, tol=1e-9, maxiter=300)
+    assert faulted.numsteps == clean.numsteps
+    np.testing.assert_allclose(np.asarray(faulted.resnorms)[:-1], np.asarray(clean.resnorms)[:-1], rtol=1e-10)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=0, atol=1e-10 * np.abs(clean.xk).max())

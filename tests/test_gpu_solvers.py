@@ -226,15 +226,37 @@ def test_cg_weighted_histories(golden):
                     final_atol=1e-8 * d["cg_w20_weighted_resnorms"][0])
 
 
-def test_restarted_gmres_reaches_tolerance():
+def _restart_dev(hist, ref):
+    """Per-entry relative deviation of a chained restart history."""
+    return np.abs(hist - ref) / np.abs(ref)
+
+
+def test_restarted_gmres_matches_reference_chaining(golden):
+    """GMRES(30) restarted by x0-chaining to 1e-8 relative, against what the
+    reference itself recorded for the same chaining (tests/golden/make_golden.py,
+    gmres_restart_*: gmres(R, b, x0=x, maxiter=30, tol=1e-8 ||b|| / ||b - R x||)
+    until success): the same number of cycles, the whole chained history within
+    1e-10 rel (each cycle's first entry is the explicit ||b - A x_c||), and the
+    final iterate."""
     import krylov_amd
     from krylov_amd import problems
 
+    d = golden["solvers"]
     R = problems.random_nonsym(5000)
     b = np.ones(5000)
-    x, infos = krylov_amd.gmres_restarted(R, b, restart=30, tol=1e-8, max_cycles=10)
-    assert np.linalg.norm(b - R @ x) <= 1.01e-8 * np.linalg.norm(b)
-    assert len(infos) >= 2
+    x, infos = krylov_amd.gmres_restarted(R, b, restart=30, tol=1e-8, max_cycles=20)
+    hist = np.concatenate([np.asarray(i.resnorms, dtype=np.float64) for i in infos])
+    ref = d["gmres_restart_hist"]
+    assert len(infos) == int(d["gmres_restart_cycles"])
+    assert infos[-1].success and not any(i.success for i in infos[:-1])
+    assert all(i.numsteps == 30 for i in infos[:-1])
+    assert hist.shape == ref.shape
+    rel = _restart_dev(hist, ref)
+    print(f"\nrestart rand5k: {len(infos)} cycles, history max rel {np.max(rel):.2e}")
+    assert np.max(rel) <= 1e-10, (np.max(rel), int(np.argmax(rel)))
+    xr = d["gmres_restart_x"]
+    np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-9 * np.max(np.abs(xr)))
+    assert np.linalg.norm(b - R @ x) <= 1e-8 * np.linalg.norm(b)
 
 
 def test_device_matches_oracle_on_metric_shape_small():

@@ -69,6 +69,31 @@ def test_oracle_gmres_histories(golden):
     _check("gmres_rand5k_blk3", *K.gmres(R, d["rand5k_B3"], maxiter=20, tol=0.0), d)
 
 
+def oracle_restart_chain(A, b, restart, tol, max_cycles):
+    """The x0-chaining of tests/golden/make_golden.py (gmres_restart_*) over the
+    oracle's gmres: tol = tol ||b|| / ||b - A x_c|| per cycle, until success."""
+    x = np.zeros_like(b)
+    bnorm = np.linalg.norm(b)
+    hist, cycles = [], 0
+    while cycles < max_cycles:
+        _, info = K.gmres(A, b, x0=x, maxiter=restart, tol=tol * bnorm / max(np.linalg.norm(b - A @ x), 1e-300))
+        hist.extend(np.asarray(info.resnorms, dtype=np.float64))
+        x = info.xk
+        cycles += 1
+        if info.success:
+            break
+    return np.array(hist), x, cycles
+
+
+def test_oracle_gmres_restart_chain(golden):
+    d = golden["solvers"]
+    R = problems.random_nonsym(5000)
+    hist, x, cycles = oracle_restart_chain(R, np.ones(5000), 30, 1e-8, 20)
+    assert cycles == int(d["gmres_restart_cycles"])
+    np.testing.assert_array_equal(hist, d["gmres_restart_hist"])
+    np.testing.assert_array_equal(x, d["gmres_restart_x"])
+
+
 def test_oracle_minres_histories(golden):
     d = golden["solvers"]
     P = problems.poisson2d(64)

@@ -1,18 +1,25 @@
-"""RHS-column sharding semantics on CPU (world_size 2, gloo).
+"""RHS-column sharding on CPU: the product's host code over gloo.
 
-The sharded path (krylov_amd.distributed.cg on GPUs over RCCL) splits the
-reference's block right-hand side into per-rank column blocks and couples
-them only through one allreduce of the zero-padded residual-norm vector per
-iteration (the global stop rule, cg.py:156,162). This test restates that
-decomposition on the host with gloo and checks it reproduces the reference's
-own unsharded block-CG fixture bit for bit (per-column recurrences are
-independent, so sharding must not change a single bit of the history).
+``krylov_amd.shard`` is the rank bookkeeping and the outer loop of
+``krylov_amd.distributed`` (the layout of every rank's columns in the global
+per-column vectors, the zero-padded allreduce, the global criterion with its
++inf padding, the explicit-residual recheck, the global history). Here it
+runs exactly as on GPUs, with the device solver state replaced by a host
+engine restating the device step (tests/shard_engines.py) and RCCL by gloo,
+at world sizes 2, 3 and 4. The reference couples a block's columns only
+through ``np.all(resnorms[-1] <= criterion)`` (cg.py:156,162, gmres.py:193,
+minres.py:162) and the invariance test (arnoldi.py:187, 270-272), so the
+sharded solve must reproduce the reference's own unsharded block fixtures.
 """
 import os
 import socket
+import threading
 
 import numpy as np
 import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
 
 
 def _free_port():
@@ -21,50 +28,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _sharded_cg_host(A, B_local, allreduce, rank, world, tol, atol=1e-15, maxiter=None):
-    """Host restatement of the device loop of krylov_amd.distributed.cg."""
-    kl = B_local.shape[1]
-    total = kl * world
-
-    def glob(v):
-        full = np.zeros(total)
-        full[rank * kl:(rank + 1) * kl] = v
-        return allreduce(full)
-
-    def inner(x, y):
-        return np.einsum("i...,i...->...", x, y)
-
-    x = np.zeros_like(B_local)
-    r = B_local - A @ x
-    rho = inner(r, r)
-    resn = [np.sqrt(glob(rho))]
-    crit = np.maximum(tol * resn[0], atol)
-    y = np.zeros_like(B_local)
-    p = r.copy()
-    rho_prev = None
-    k = 0
-    maxiter = A.shape[0] if maxiter is None else maxiter
-    while True:
-        if np.all(resn[-1] <= crit):
-            rr = B_local - A @ (x + y)
-            resn[-1] = np.sqrt(glob(inner(rr, rr)))
-            if np.all(resn[-1] <= crit):
-                break
-        if k == maxiter:
-            break
-        if k > 0:
-            p = r + (rho / np.where(rho_prev != 0, rho_prev, 1.0)) * p
-        Ap = A @ p
-        alpha = rho / np.where(inner(p, Ap) != 0, inner(p, Ap), 1.0)
-        y += alpha * p
-        r -= alpha * Ap
-        rho_prev, rho = rho, inner(r, r)
-        resn.append(np.sqrt(glob(rho)))
-        k += 1
-    return k, np.array(resn), x + y
-
-
-def _worker(rank, world, port, outdir):
+def _gloo(rank, world, port):
     import torch
     import torch.distributed as dist
 
@@ -73,137 +37,150 @@ def _worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def allreduce(v):
-        t = torch.from_numpy(np.ascontiguousarray(v))
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64).copy())
         dist.all_reduce(t)
         return t.numpy().copy()
 
+    return dist, allreduce
+
+
+def _worker(rank, world, port, outdir, which):
     import sys
 
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, REPO)
+    dist, allreduce = _gloo(rank, world, port)
     from krylov_amd import problems
+    from krylov_amd.shard import ShardLayout, drive
+    from tests import shard_engines as E
 
-    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "solvers.npz"))
-    P = problems.poisson2d(64)
-    B = d["poisson64_B"]
-    kl = B.shape[1] // world
-    k, resn, x = _sharded_cg_host(P, B[:, rank * kl:(rank + 1) * kl].copy(), allreduce, rank, world, tol=1e-8)
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), k=k, resn=resn, x=x)
-    dist.destroy_process_group()
-
-
-def test_rhs_sharding_reproduces_block_cg_bitwise(tmp_path):
-    torch = pytest.importorskip("torch")
-    import torch.multiprocessing as mp
-
-    world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "solvers.npz"))
-    ref_k = int(d["cg_poisson64_blk8_numsteps"])
-    ref_res = d["cg_poisson64_blk8_resnorms"]
-    xs = []
-    for r in range(world):
-        o = np.load(tmp_path / f"r{r}.npz")
-        assert int(o["k"]) == ref_k
-        np.testing.assert_array_equal(o["resn"], ref_res)  # global history on every rank
-        xs.append(o["x"])
-    np.testing.assert_array_equal(np.concatenate(xs, axis=1), d["cg_poisson64_blk8_xk"])
-
-
-# ---------------------------------------------------------------- GMRES / MINRES
-# krylov_amd.distributed.gmres / .minres couple the ranks through one
-# allreduce per step of the residual norms and a non-invariant count. The
-# oracle restatements take the same coupling as a `shard` hook; over gloo,
-# one column per rank must reproduce the unsharded block solve (same stop
-# step; per-column recurrences equal up to the einsum of a (n, 1) vs (n, 3)
-# block) and the reference's block-GMRES fixture.
-
-
-def _solver_worker(rank, world, port, outdir, which):
-    import sys
-
-    import torch
-    import torch.distributed as dist
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from krylov_amd import problems
-    from oracle import krylov_ref
-
-    def shard(local):
-        local = np.atleast_1d(np.asarray(local, dtype=np.float64))
-        full = np.zeros(world * local.size)
-        full[rank * local.size:(rank + 1) * local.size] = local
-        t = torch.from_numpy(full)
-        dist.all_reduce(t)
-        return t.numpy().copy()
-
-    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "solvers.npz"))
+    d = np.load(os.path.join(HERE, "golden", "solvers.npz"))
     out = {}
-    if which == "gmres":
+    if which == "cg":
+        P = problems.poisson2d(64)
+        B = d["poisson64_B"]
+        kl = B.shape[1] // world
+        lay = ShardLayout(kl, kl, rank, world)
+        eng = E.HostCG(P, B[:, rank * kl:(rank + 1) * kl], lay, allreduce)
+        out["success"], out["k"], res = drive(eng, lay, allreduce, 1e-8, 1e-15, P.shape[0], np.float64)
+        out["res"], out["x"] = np.array(res), eng.xk()
+    elif which == "gmres":
         R = problems.random_nonsym(5000)
         B = d["rand5k_B3"]
-        Bl = B[:, [rank]].copy()
-        _, info = krylov_ref.gmres(R, Bl, maxiter=20, tol=0.0, shard=shard)
-        out["fixed_k"], out["fixed_res"], out["fixed_x"] = info.numsteps, np.array(info.resnorms), info.xk
-        # columns converge at different steps: the global rule keeps all going
-        _, info = krylov_ref.gmres(R, Bl, maxiter=60, tol=1e-6, shard=shard)
-        out["tol_k"], out["tol_res"] = info.numsteps, np.array(info.resnorms)
+        lay = ShardLayout(1, 1, rank, world)
+        eng = E.HostGMRES(R, B[:, [rank]], lay, allreduce, 20)
+        out["success"], out["k"], res = drive(eng, lay, allreduce, 0.0, 1e-15, 20, np.float64)
+        out["res"], out["x"] = np.array(res), eng.xk()
+        # a tolerance at which the columns converge at different steps: the
+        # global rule keeps every rank going until the slowest column is done
+        eng = E.HostGMRES(R, B[:, [rank]], lay, allreduce, 60)
+        out["tol_success"], out["tol_k"], res = drive(eng, lay, allreduce, 1e-6, 1e-15, 60, np.float64)
+        out["tol_res"] = np.array(res)
     else:
         P = problems.poisson2d(32)
         B = np.random.default_rng(3).standard_normal((P.shape[0], world))
         B[:, 1] *= 1e-3
-        _, info = krylov_ref.minres(P, B[:, [rank]].copy(), tol=1e-8, shard=shard)
-        out["tol_k"], out["tol_res"], out["x"] = info.numsteps, np.array(info.resnorms), info.xk
+        lay = ShardLayout(1, 1, rank, world)
+        eng = E.HostMINRES(P, B[:, [rank]], lay, allreduce)
+        out["success"], out["k"], res = drive(eng, lay, allreduce, 1e-8, 1e-15, P.shape[0], np.float64)
+        out["res"], out["x"] = np.array(res), eng.xk()
     np.savez(os.path.join(outdir, f"{which}{rank}.npz"), **out)
     dist.destroy_process_group()
 
 
-def test_rhs_sharding_gmres_global_rules(tmp_path):
+def _spawn(tmp_path, which, world):
     pytest.importorskip("torch")
     import torch.multiprocessing as mp
 
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), which), nprocs=world, join=True)
+    return [np.load(tmp_path / f"{which}{r}.npz") for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_cg_reproduces_block_cg_bitwise(tmp_path, world):
+    """8 columns over 2 or 4 ranks: the reference's block-CG fixture bit for
+    bit (the per-column recurrences are independent; sharding changes no bit)."""
+    d = np.load(os.path.join(HERE, "golden", "solvers.npz"))
+    outs = _spawn(tmp_path, "cg", world)
+    for o in outs:
+        assert bool(o["success"]) and int(o["k"]) == int(d["cg_poisson64_blk8_numsteps"])
+        np.testing.assert_array_equal(o["res"], d["cg_poisson64_blk8_resnorms"])  # global history on every rank
+    np.testing.assert_array_equal(np.concatenate([o["x"] for o in outs], axis=1), d["cg_poisson64_blk8_xk"])
+
+
+def test_sharded_gmres_global_rules(tmp_path):
     from krylov_amd import problems
     from oracle import krylov_ref
 
     world = 3
-    mp.spawn(_solver_worker, args=(world, _free_port(), str(tmp_path), "gmres"), nprocs=world, join=True)
-    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "solvers.npz"))
+    outs = _spawn(tmp_path, "gmres", world)
+    d = np.load(os.path.join(HERE, "golden", "solvers.npz"))
     R = problems.random_nonsym(5000)
-    B = d["rand5k_B3"]
-    _, blk = krylov_ref.gmres(R, B, maxiter=60, tol=1e-6)
-    ref_k = int(d["gmres_rand5k_blk3_numsteps"])
+    _, blk = krylov_ref.gmres(R, d["rand5k_B3"], maxiter=60, tol=1e-6)
     ref_res = np.asarray(d["gmres_rand5k_blk3_resnorms"])
-    for r in range(world):
-        o = np.load(tmp_path / f"gmres{r}.npz")
-        assert int(o["fixed_k"]) == ref_k
-        np.testing.assert_allclose(o["fixed_res"], ref_res, rtol=1e-12)  # global history on every rank
-        np.testing.assert_allclose(o["fixed_x"][:, 0], d["gmres_rand5k_blk3_xk"][:, r], rtol=1e-9, atol=1e-12)
-        assert int(o["tol_k"]) == blk.numsteps  # the slowest column decides the global stop step
+    for r, o in enumerate(outs):
+        assert int(o["k"]) == int(d["gmres_rand5k_blk3_numsteps"]) and not bool(o["success"])
+        np.testing.assert_allclose(o["res"], ref_res, rtol=1e-12)  # global history on every rank
+        np.testing.assert_allclose(o["x"][:, 0], d["gmres_rand5k_blk3_xk"][:, r], rtol=1e-9, atol=1e-12)
+        assert bool(o["tol_success"]) and int(o["tol_k"]) == blk.numsteps  # the slowest column decides
         ref = np.asarray(blk.resnorms)
         np.testing.assert_allclose(o["tol_res"][:-1], ref[:-1], rtol=1e-12)
         # the final entry is the explicit residual: compared absolutely (SURVEY §8(c))
         np.testing.assert_allclose(o["tol_res"][-1], ref[-1], rtol=0, atol=1e-12 * ref[0].max())
 
 
-def test_rhs_sharding_minres_global_rules(tmp_path):
-    pytest.importorskip("torch")
-    import torch.multiprocessing as mp
-
+def test_sharded_minres_global_rules(tmp_path):
     from krylov_amd import problems
     from oracle import krylov_ref
 
     world = 2
-    mp.spawn(_solver_worker, args=(world, _free_port(), str(tmp_path), "minres"), nprocs=world, join=True)
+    outs = _spawn(tmp_path, "minres", world)
     P = problems.poisson2d(32)
     B = np.random.default_rng(3).standard_normal((P.shape[0], world))
     B[:, 1] *= 1e-3
     _, blk = krylov_ref.minres(P, B, tol=1e-8)
-    for r in range(world):
-        o = np.load(tmp_path / f"minres{r}.npz")
-        assert int(o["tol_k"]) == blk.numsteps
-        ref = np.asarray(blk.resnorms)
-        np.testing.assert_allclose(o["tol_res"][:-1], ref[:-1], rtol=1e-12)
-        np.testing.assert_allclose(o["tol_res"][-1], ref[-1], rtol=0, atol=1e-12 * ref[0].max())
+    ref = np.asarray(blk.resnorms)
+    for r, o in enumerate(outs):
+        assert bool(o["success"]) and int(o["k"]) == blk.numsteps
+        np.testing.assert_allclose(o["res"][:-1], ref[:-1], rtol=1e-12)
+        np.testing.assert_allclose(o["res"][-1], ref[-1], rtol=0, atol=1e-12 * ref[0].max())
         np.testing.assert_allclose(o["x"][:, 0], blk.xk[:, r], rtol=1e-10, atol=1e-13)
+
+
+# ------------------------------------------------------------- layout units
+def test_shard_layout_padding_and_global_vectors():
+    """3 real columns padded to 4 on each of 3 ranks: real slots, the
+    zero-padded all-gather, and +inf criterion on the padded slots."""
+    from krylov_amd.shard import ShardLayout
+
+    lays = [ShardLayout(3, 4, r, 3) for r in range(3)]
+    np.testing.assert_array_equal(lays[0].real, [0, 1, 2, 4, 5, 6, 8, 9, 10])
+    assert lays[2].off == 8 and lays[2].total == 12
+    parts = [lay.glob(np.array([r + 0.5, r + 1.5, r + 2.5, 99.0]), lambda v: v) for r, lay in enumerate(lays)]
+    summed = np.sum(parts, axis=0)
+    np.testing.assert_array_equal(summed[lays[0].real], [0.5, 1.5, 2.5, 1.5, 2.5, 3.5, 2.5, 3.5, 4.5])
+    crit = lays[1].criterion_full(np.arange(9.0))
+    np.testing.assert_array_equal(crit[lays[1].real], np.arange(9.0))
+    assert np.all(np.isinf(crit[[3, 7, 11]]))
+    with pytest.raises(ValueError):
+        ShardLayout(2, 1, 0, 2)
+
+
+def test_file_rendezvous_threads(tmp_path):
+    """The torch-free unique-id exchange: rank 0 publishes, others poll."""
+    from krylov_amd.shard import file_rendezvous
+
+    path = str(tmp_path / "uid")
+    payload = os.urandom(128)
+    got = [None] * 4
+
+    def rank(r):
+        got[r] = file_rendezvous(path, r, lambda: payload, timeout=20)
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in (3, 2, 1, 0)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(g == payload for g in got)
+    with pytest.raises(TimeoutError):
+        file_rendezvous(str(tmp_path / "never"), 1, lambda: b"", timeout=0.2)
