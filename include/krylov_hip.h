@@ -69,7 +69,7 @@ int kry_ctx_synchronize(kry_ctx *ctx);
  * the same rounded size (after one device synchronisation), instead of a
  * hipMalloc + hipFree pair per reference-API call (the reference allocates
  * its NumPy work arrays per call, cg.py:116-131, arnoldi.py:129-131).
- * KRYLOV_ALLOC_CACHE=0 disables it; KRYLOV_ALLOC_CACHE_MAX_GB caps it (64).
+ * KRYLOV_ALLOC_CACHE=0 disables it; KRYLOV_ALLOC_CACHE_MAX_GB caps it (16).
  * stats: out[0..5] = bytes in use, bytes cached, reuses, hipMallocs, device
  * syncs taken to retire freed blocks, enabled (0/1). release: hipFree every
  * cached block (in use blocks are untouched). */

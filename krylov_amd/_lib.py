@@ -3,8 +3,11 @@
 The shared library is the only compute path of this package. If it is missing
 the import fails loudly; there is no CPU fallback.
 """
+import atexit
 import ctypes
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -211,3 +214,52 @@ def csr_layout(indptr):
     check(lib.kry_csr_layout(indptr.shape[0] - 1, ptr(indptr), itype_code(indptr.dtype), ctypes.byref(ns),
                              ctypes.byref(slots), ctypes.byref(irr)))
     return ns.value, slots.value, irr.value
+
+
+# ------------------------------------------------------------- teardown
+# Every C-ABI handle a Python object owns is released by a weakref.finalize
+# created through `own` and marked not to run from weakref's exit hook. At
+# interpreter exit `_shutdown` (an atexit hook registered when this module
+# loads) releases them in a fixed order while the HIP runtime is still up:
+# wait for
+# every context's stream, destroy solvers / operators / vectors /
+# communicators (newest first), return the allocator's cached blocks to the
+# runtime (kry_mem_release), then destroy the contexts. Nothing is left for
+# static destructors or a profiler's exit hooks to race with.
+_owned = []
+_owned_lock = threading.Lock()
+
+
+def own(obj, destroy, handle, context=False):
+    """weakref.finalize(obj, destroy, handle), released in order at exit."""
+    fin = weakref.finalize(obj, destroy, handle)
+    fin.atexit = False  # _shutdown runs it, in order
+    with _owned_lock:
+        _owned.append((fin, context))
+        if len(_owned) > 4096:  # drop finalizers that already ran
+            _owned[:] = [(f, c) for f, c in _owned if f.alive]
+    return fin
+
+
+def _shutdown():
+    with _owned_lock:
+        owned = list(_owned)
+        _owned.clear()
+    ctxs = [f for f, c in owned if c and f.alive]
+    for f in ctxs:  # drain every stream before anything is freed
+        info = f.peek()  # (obj, func, args, kwargs)
+        if info is not None:
+            lib.kry_ctx_synchronize(info[2][0])
+    for f, c in reversed(owned):
+        if not c:
+            f()
+    lib.kry_mem_release()
+    for f in reversed(ctxs):
+        f()
+    maps = os.environ.get("KRY_EXIT_MAPS")  # diagnostics: the address map at exit (tools/gpu_exit_bisect.sh)
+    if maps:
+        with open("/proc/self/maps") as src, open(maps, "w") as dst:
+            dst.write(src.read())
+
+
+atexit.register(_shutdown)

@@ -9,7 +9,6 @@ residual norms satisfy the criterion, so the host sees exactly the
 iterations the reference performs.
 """
 import ctypes
-import weakref
 
 import numpy as np
 
@@ -24,7 +23,7 @@ class _CGState:
         h = ctypes.c_void_p()
         check(lib.kry_cg_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype), ctypes.byref(h)))
         self.h = h
-        self._fin = weakref.finalize(self, lib.kry_cg_destroy, h)
+        self._fin = _lib.own(self, lib.kry_cg_destroy, h)
         if prob.ops["Mr"] is not None:
             raise TypeError("cg has no right preconditioner Mr")
         if prob.has_precond():

@@ -65,21 +65,26 @@ bool cache_enabled() {
   return on;
 }
 
-// Bytes the cache may hold (KRYLOV_ALLOC_CACHE_MAX_GB, default 64 of the
-// 288 GB): a larger free goes straight back to the runtime.
+// Bytes the cache may hold (KRYLOV_ALLOC_CACHE_MAX_GB, default 16 of the
+// 288 GB: every state of the BASELINE configurations, the metric GMRES(30)
+// basis of 2.5 GB included, several times over; other allocators in the
+// process see the rest): a larger free goes straight back to the runtime.
 size_t cache_cap() {
   static const size_t cap = [] {
     const char *e = getenv("KRYLOV_ALLOC_CACHE_MAX_GB");
-    const double gb = e ? atof(e) : 64.0;
+    const double gb = e ? atof(e) : 16.0;
     return (size_t)(gb > 0 ? gb * 1e9 : 0);
   }();
   return cap;
 }
 
-// 64 KiB granules below 2 MiB, 2 MiB granules above (the HBM page size the
-// runtime maps large buffers with): a reused block wastes < 2 MiB.
+// 4 KiB granules below 64 KiB (control words, scalars, partials), 64 KiB
+// below 2 MiB, 2 MiB above (the HBM page size the runtime maps large buffers
+// with): a reused block wastes < 4 KiB / 64 KiB / 2 MiB.
 size_t round_alloc(size_t total) {
-  const size_t g = total < ((size_t)2 << 20) ? ((size_t)64 << 10) : ((size_t)2 << 20);
+  const size_t g = total < ((size_t)64 << 10)  ? ((size_t)4 << 10)
+                   : total < ((size_t)2 << 20) ? ((size_t)64 << 10)
+                                               : ((size_t)2 << 20);
   return (total + g - 1) / g * g;
 }
 

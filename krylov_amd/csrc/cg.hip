@@ -779,12 +779,11 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
     s->cgp_spw = 0;
     const char *e = getenv("KRY_CG_PERSIST");
     if (!(e && atoi(e) == 0)) {
-      int dev = 0, ncu = 0, coop = 0;
+      int dev = 0, ncu = 0;
       KRY_HIP(hipGetDevice(&dev));
       KRY_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      KRY_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
       const int gmax = ncu < 256 ? ncu : 256;
-      for (int spw = 1; coop && spw <= 4; spw *= 2) {
+      for (int spw = 1; spw <= 4; spw *= 2) {
         const int64_t G = (A->nslices + (int64_t)kCgpWaves * spw - 1) / ((int64_t)kCgpWaves * spw);
         if (G > gmax) continue;
         int per_cu = 0;
@@ -834,9 +833,19 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
                   &bufs,   &hist,     &words,  &ctrl,     &max_steps, &tb,    &fault_step};
   hipError_t le;
   {
+    // A plain launch, as for cg_upd_kernel: residency is the occupancy check
+    // above (at most one block per CU) and a block that still does not become
+    // resident makes the exchange time out, the chunk then reruns launch per
+    // pass from its untouched start state. A cooperative launch guaranteed
+    // residency but left HIP runtime state behind that crashed the process at
+    // exit under rocprofv3 (libamdhip64's exit handler into
+    // libhsa-runtime64, profiles/r03_exit_crash.txt); KRY_CGP_COOP=1 keeps
+    // it for comparison.
     ProfScope ps(s->ctx, PROF_OTHER);
-    le = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern_for(spw)), dim3(G), dim3(kCgpBlock), args, 0,
-                                    st);
+    const char *ce = getenv("KRY_CGP_COOP");
+    const void *kf = reinterpret_cast<const void *>(kern_for(spw));
+    le = (ce && atoi(ce) == 1) ? hipLaunchCooperativeKernel(kf, dim3(G), dim3(kCgpBlock), args, 0, st)
+                               : hipLaunchKernel(kf, dim3(G), dim3(kCgpBlock), args, 0, st);
   }
   if (le != hipSuccess) {
     (void)hipGetLastError();  // clear the refusal; the solve continues on the launch-per-pass path

@@ -2,7 +2,6 @@
 import ctypes
 import os
 import threading
-import weakref
 
 import numpy as np
 
@@ -21,7 +20,7 @@ class Context:
         check(lib.kry_ctx_create(int(device), ctypes.byref(h)))
         self.device = int(device)
         self.handle = h
-        self._fin = weakref.finalize(self, lib.kry_ctx_destroy, h)
+        self._fin = _lib.own(self, lib.kry_ctx_destroy, h, context=True)
 
     def synchronize(self):
         check(lib.kry_ctx_synchronize(self.handle))
@@ -82,7 +81,7 @@ class DeviceVector:
         h = ctypes.c_void_p()
         check(lib.kry_vec_create(ctx.handle, self.n, self.k, _lib.dtype_code(self.dtype), ctypes.byref(h)))
         self.handle = h
-        self._fin = weakref.finalize(self, lib.kry_vec_destroy, h)
+        self._fin = _lib.own(self, lib.kry_vec_destroy, h)
 
     @classmethod
     def from_host(cls, ctx, a, dtype=None):

@@ -18,7 +18,6 @@ bookkeeping and the outer loop are ``krylov_amd.shard`` (pure NumPy, the code
 the gloo CPU tests run); this module binds them to the device states.
 """
 import ctypes
-import weakref
 
 import numpy as np
 
@@ -42,7 +41,7 @@ class ShardComm:
         h = ctypes.c_void_p()
         check(lib.kry_comm_create(self.ctx.handle, self.world, self.rank, _lib.ptr(idb), ctypes.byref(h)))
         self.handle = h
-        self._fin = weakref.finalize(self, lib.kry_comm_destroy, h)
+        self._fin = _lib.own(self, lib.kry_comm_destroy, h)
 
     @staticmethod
     def unique_id():

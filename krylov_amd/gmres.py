@@ -8,7 +8,6 @@ Arnoldi basis, and restarted GMRES(m) is ``gmres(..., maxiter=m)`` chained
 through ``x0`` (see ``gmres_restarted``).
 """
 import ctypes
-import weakref
 
 import numpy as np
 
@@ -57,7 +56,7 @@ class _GmresState:
         check(lib.kry_gmres_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype),
                                    int(maxiter), int(sweeps), ctypes.byref(h)))
         self.h = h
-        self._fin = weakref.finalize(self, lib.kry_gmres_destroy, h)
+        self._fin = _lib.own(self, lib.kry_gmres_destroy, h)
         if prob.has_precond():
             check(lib.kry_gmres_set_preconditioners(h, *prob.op_handles("M", "Ml", "Mr")))
 

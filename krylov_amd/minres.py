@@ -4,7 +4,6 @@ three-term direction recurrence and the x update run on the GPU
 (``kry_minres_*``), in chunks with one host sync per chunk.
 """
 import ctypes
-import weakref
 
 import numpy as np
 
@@ -20,7 +19,7 @@ class _MinresState:
         check(lib.kry_minres_create(prob.ctx.handle, prob.A.handle, prob.kpad, _lib.dtype_code(prob.dtype),
                                     ctypes.byref(h)))
         self.h = h
-        self._fin = weakref.finalize(self, lib.kry_minres_destroy, h)
+        self._fin = _lib.own(self, lib.kry_minres_destroy, h)
         if prob.has_precond():
             check(lib.kry_minres_set_preconditioners(h, *prob.op_handles("M", "Ml", "Mr")))
 

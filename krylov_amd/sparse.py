@@ -64,7 +64,7 @@ class CsrOperator:
             )
         )
         self.handle = h
-        self._fin = weakref.finalize(self, lib.kry_csr_destroy, h)
+        self._fin = _lib.own(self, lib.kry_csr_destroy, h)
 
     @property
     def device(self):

@@ -16,6 +16,9 @@ only the summation order of its inner product changes, every other line of
              configuration the committed fixtures were recorded under
   pairwise   inner = numpy's pairwise sum of the products (np.add.reduce)
   longdouble inner = dot accumulated in x87 extended precision, rounded once
+  fsum       inner = math.fsum of the products: the correctly rounded sum
+  permK      (small cases only) inner = numpy's pairwise sum of the products
+             taken in a fixed random order (permutation seed K, 0..39)
 
 Each variant is a valid evaluation of the reference's <x, y>; the spread
 between them is the reference's own rounding noise. Every variant runs in
@@ -27,6 +30,7 @@ per-entry tolerance from them.
 """
 import contextlib
 import io
+import math
 import os
 import subprocess
 import sys
@@ -51,23 +55,42 @@ VARIANTS = {
     "blasN": {},
     "pairwise": {},
     "longdouble": {},
+    "fsum": {},
 }
 
 
-def _inner_for(variant, kind, w):
+SMALL_ONLY = tuple(f"perm{k}" for k in range(40))
+for _v in SMALL_ONLY:
+    VARIANTS[_v] = {}
+
+
+def _perm_inner(seed, n, w=None):
+    perm = np.random.default_rng(seed).permutation(n)
+    if w is None:
+        return lambda x, y: np.add.reduce((x.conj() * y)[perm])
+    return lambda x, y: np.add.reduce((x * (w * y))[perm])
+
+
+def _inner_for(variant, kind, w, n):
     """The inner product a variant hands to krylov.cg (None = the reference's
     default np.dot)."""
+    if variant.startswith("perm"):
+        return _perm_inner(int(variant[4:]), n, None if kind == "default" else w)
     if kind == "default":
         if variant.startswith("blas"):
             return None
         if variant == "pairwise":
             return lambda x, y: np.add.reduce(x.conj() * y)
+        if variant == "fsum":
+            return lambda x, y: np.float64(math.fsum(x.conj() * y))
         return lambda x, y: np.float64(np.dot(x.astype(np.longdouble), y.astype(np.longdouble)))
     # tests/test_solvers.py:157-161 weighted form np.dot(x.T, w * y)
     if variant.startswith("blas"):
         return lambda x, y: np.dot(x.T, w * y)
     if variant == "pairwise":
         return lambda x, y: np.add.reduce(x * (w * y))
+    if variant == "fsum":
+        return lambda x, y: np.float64(math.fsum(x * (w * y)))
     return lambda x, y: np.float64(np.dot(x.astype(np.longdouble), (w * y).astype(np.longdouble)))
 
 
@@ -87,7 +110,7 @@ def run_one(case, variant, out_path):
     b = np.ones(A.shape[0])
     t = time.time()
     with contextlib.redirect_stdout(io.StringIO()):
-        _, info = krylov.cg(A, b, tol=tol, inner=_inner_for(variant, kind, w))
+        _, info = krylov.cg(A, b, tol=tol, inner=_inner_for(variant, kind, w, A.shape[0]))
     np.save(out_path, np.asarray(info.resnorms, dtype=np.float64))
     print(f"{case} {variant}: {info.numsteps} steps, {time.time() - t:.0f}s", flush=True)
 
@@ -104,6 +127,8 @@ def main():
             continue
         for variant, env in VARIANTS.items():
             if f"{case}_{variant}" in out:  # recorded by an earlier run
+                continue
+            if variant in SMALL_ONLY and case != "cg_w20_weighted":
                 continue
             e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", **env)
             subprocess.check_call([sys.executable, __file__, "--one", case, variant, tmp], env=e)

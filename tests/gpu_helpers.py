@@ -1,8 +1,33 @@
 """Small systems and the consistency check used by the reference's own test
 suite (tests/linear_problems.py, tests/helpers.py:4-23), restated for the
 real-valued problems the MI355X path covers."""
+import os
+
 import numpy as np
 import scipy.sparse
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# The device sums its inner products in one more valid order; its deviation
+# from the fixture is allowed twice the envelope of the reference's own
+# deviation under 5 other orders (tests/golden/make_selfnoise.py).
+NOISE_FACTOR = 2.0
+
+
+def selfnoise_envelope(case, ref):
+    """Per history entry (all but the final explicit one): the spread of the
+    reference's own history when only the summation order of its inner
+    product changes (tests/golden/selfnoise.npz: OpenBLAS 1 / 2 / 4 / 8
+    threads, pairwise, extended precision, fsum, and for small cases 40
+    random orders), as the largest relative difference between any two of
+    those histories and the fixture ``ref``, carried forward as a running
+    maximum along the history (rounding differences propagate through the
+    recurrence)."""
+    d = np.load(os.path.join(GOLD, "selfnoise.npz"))
+    hs = [d[k] for k in sorted(d.files) if k.startswith(case + "_")]
+    assert hs and all(h.shape == ref.shape for h in hs), case
+    H = np.array([ref[:-1]] + [h[:-1] for h in hs])
+    spread = (H.max(axis=0) - H.min(axis=0)) / np.abs(ref[:-1])
+    return np.maximum.accumulate(spread)
 
 
 def _spd_diag(n):
@@ -59,15 +84,14 @@ def assert_consistent(A, b, info, sol, tol):
     assert np.asarray(info.resnorms).shape == (info.numsteps + 1, *b.shape[1:])
 
 
-def assert_parity(info, d, prefix, rtol=1e-10, xtol=1e-9, final_atol=None, prefix_steps=None, tail_rtol=None,
-                  floor=0.0):
+def assert_parity(info, d, prefix, rtol=1e-10, xtol=1e-9, final_atol=None, noise=None, floor=0.0):
     """Device run vs the reference fixture: identical step count and success,
     updated-residual history within rtol, final explicit residual within an
     absolute round-off bound, solution within xtol.
 
-    prefix_steps / tail_rtol: for problems whose history is chaotic in the
-    summation order of the inner products (documented per test), check the
-    first prefix_steps entries at rtol and the rest at tail_rtol."""
+    noise: for a history the reference's own summation-order noise moves by
+    more than rtol, the per-entry envelope of that noise (selfnoise_envelope):
+    entry i may deviate by max(rtol, NOISE_FACTOR * noise[i]) rel."""
     assert info.numsteps == int(d[prefix + "_numsteps"])
     assert info.success == bool(d[prefix + "_success"])
     got = np.asarray(info.resnorms, dtype=np.float64)
@@ -77,11 +101,8 @@ def assert_parity(info, d, prefix, rtol=1e-10, xtol=1e-9, final_atol=None, prefi
     # updated residual loses relative accuracy as it decreases (eps ||r_0|| / ||r_k||)
     diff = np.maximum(np.abs(got[:-1] - ref[:-1]) - floor * np.max(np.abs(ref[0])), 0.0)
     rel = diff / np.maximum(np.abs(ref[:-1]), 1e-300)
-    if prefix_steps is None:
-        assert np.all(rel <= rtol), (np.max(rel), int(np.argmax(rel)))
-    else:
-        assert np.all(rel[:prefix_steps] <= rtol), (np.max(rel[:prefix_steps]), int(np.argmax(rel[:prefix_steps])))
-        assert np.all(rel[prefix_steps:] <= tail_rtol), (np.max(rel[prefix_steps:]),)
+    tol = rtol if noise is None else np.maximum(rtol, NOISE_FACTOR * noise)
+    assert np.all(rel <= tol), (np.max(rel / tol), int(np.argmax(rel / tol)))
     if final_atol is None:
         final_atol = 1e-12 * np.max(np.abs(ref[0])) + 1e-300
     assert np.all(np.abs(got[-1] - ref[-1]) <= final_atol)

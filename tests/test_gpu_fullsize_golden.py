@@ -8,11 +8,15 @@ sum|x|, ||x||, max|x| and 4096 sampled entries. The device path must give:
 
 * the same numsteps and success flag (bit-exact iteration counts);
 * every recurrence residual norm within 1e-10 rel (fp64) / 1e-4 rel (fp32),
-  the north_star tolerances, with an absolute floor of one ulp of the initial
-  residual norm (eps ||r0||) for entries a converged history drives many
-  orders of magnitude below ||r0||; the last entry is the explicit residual
-  ||b - A x||, a cancellation-dominated quantity, compared with an absolute
-  bound of 64 eps (||b|| + ||A||_1 ||x||) (SURVEY.md §8(c));
+  the north_star tolerances, except where the reference's OWN history moves
+  by more than that when only the summation order of its inner product
+  changes (tests/golden/selfnoise.npz: OpenBLAS 1/2/4/8 threads, pairwise,
+  extended precision, fsum; the metric CG's last entries move by up to 3e-9
+  rel, 1e-8 x ||r0|| below the start): there entry i may deviate by
+  2 x that measured envelope (tests/gpu_helpers.selfnoise_envelope); the
+  last entry is the explicit residual ||b - A x||, a cancellation-dominated
+  quantity, compared with an absolute bound of 64 eps (||b|| + ||A||_1 ||x||)
+  (SURVEY.md §8(c));
 * the solution's summaries and samples within the drift that bound implies.
 
 The observed worst deviations are printed (pytest -s) so the headroom under
@@ -22,6 +26,8 @@ import os
 
 import numpy as np
 import pytest
+
+from tests import gpu_helpers as H
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -38,18 +44,19 @@ def _sample(n, m):
     return np.sort(np.random.default_rng(12345).choice(n, m, replace=False))
 
 
-def _check(info, F, prefix, A, b, rtol, xtol):
+def _check(info, F, prefix, A, b, rtol, xtol, noise_case=None):
     assert info.numsteps == int(F[f"{prefix}_numsteps"])
     assert bool(info.success) == bool(F[f"{prefix}_success"])
     ref = F[f"{prefix}_resnorms"]
     got = np.asarray(info.resnorms, dtype=np.float64)
     assert got.shape == ref.shape
-    dev = np.abs(got[:-1] - ref[:-1])
-    rel = np.max(dev / np.abs(ref[:-1]))
-    # 1e-10 rel, with a floor of one ulp of the initial residual norm for the
-    # entries a converged history drives 8+ orders of magnitude below it
-    # (two correctly rounded dot orders already differ by ~eps ||r0|| there)
-    budget = np.max(dev / (rtol * np.abs(ref[:-1]) + EPS * np.abs(ref[0])))
+    dev = np.abs(got[:-1] - ref[:-1]) / np.abs(ref[:-1])
+    rel = np.max(dev)
+    # rtol, or twice the reference's own summation-order noise at that entry
+    tol = np.full(dev.shape, rtol)
+    if noise_case is not None:
+        tol = np.maximum(tol, H.NOISE_FACTOR * H.selfnoise_envelope(noise_case, ref))
+    budget = np.max(dev / tol)
     x = np.asarray(info.xk, dtype=np.float64)
     xa = np.abs(x)
     stats = np.array([xa.sum(axis=0), np.sqrt((xa * xa).sum(axis=0)), xa.max(axis=0)])
@@ -61,8 +68,8 @@ def _check(info, F, prefix, A, b, rtol, xtol):
     xs = x[_sample(x.shape[0], int(F["nsample"]))]
     xdev = np.max(np.abs(xs - F[f"{prefix}_xsample"]) / rstats[2])
     sdev = np.max(np.abs(stats - rstats) / rstats)
-    print(f"\n{prefix}: numsteps {info.numsteps}, history max rel {rel:.2e} ({budget:.2f} of the tolerance "
-          f"{rtol:.0e} rel + eps ||r0||), final "
+    print(f"\n{prefix}: numsteps {info.numsteps}, history max rel {rel:.2e} ({budget:.2f} of the per-entry "
+          f"tolerance: {rtol:.0e} rel{' or 2x the reference self-noise' if noise_case else ''}), final "
           f"{fin:.2e} of the explicit-residual bound, x samples {xdev:.2e} of max|x|, x summaries {sdev:.2e} rel")
     assert budget <= 1.0
     assert fin <= 1.0
@@ -83,7 +90,7 @@ def test_metric_cg_to_convergence(full, stencil216):
 
     b = np.ones(stencil216.shape[0])
     _, info = krylov_amd.cg(krylov_amd.CsrOperator(stencil216), b, tol=1e-8)
-    _check(info, full, "metric_cg", stencil216, b, 1e-10, 1e-8)
+    _check(info, full, "metric_cg", stencil216, b, 1e-10, 1e-8, noise_case="metric_cg")
 
 
 def test_metric_gmres30(full, stencil216):
@@ -104,7 +111,7 @@ def test_cfg2_cg_to_convergence(full):
     P = problems.poisson2d(1000)
     b = np.ones(P.shape[0])
     _, info = krylov_amd.cg(krylov_amd.CsrOperator(P), b, tol=1e-8)
-    _check(info, full, "cfg2_cg", P, b, 1e-10, 1e-8)
+    _check(info, full, "cfg2_cg", P, b, 1e-10, 1e-8, noise_case="cfg2_cg")
 
 
 def test_cfg3_gmres30(full):

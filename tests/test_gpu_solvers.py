@@ -209,21 +209,23 @@ def test_minres_fp32_weighted(golden):
 
 def test_cg_weighted_histories(golden):
     """641 weighted-CG iterations on the shifted 20^3 Laplacian. This history
-    is chaotic in the summation order of the inner products: the oracle run
-    with an exactly rounded dot (math.fsum) already departs from the
-    reference's OpenBLAS order by up to 8.7% relative late in the run (and a
-    pairwise order by 7.4%), while agreeing to ~1e-9 over the first 100 steps.
-    The device is held to the same envelope: identical step count and
-    success, 1e-7 over the first 100 steps, <= 20% afterwards, and the
-    solution to the solve tolerance."""
+    is chaotic in the summation order of the inner products: the reference's
+    own history moves by up to 8.7% relative late in the run when only its
+    inner product's summation order changes (correctly rounded fsum; 5.6%
+    pairwise, 2.0% extended precision), and by 5e-8 at step 100
+    (tests/golden/selfnoise.npz, make_selfnoise.py). The device is held to
+    that measured envelope: identical step count and success, every entry
+    within max(1e-10, 2 x the reference's own deviation up to that step), the
+    final explicit residual and the solution to the solve tolerance."""
     import krylov_amd
     from krylov_amd import problems
 
     d = golden["solvers"]
     W, w = problems.shifted_lap3d_weighted(20)
     info = krylov_amd.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=krylov_amd.WeightedInner(w), tol=1e-8)[1]
-    H.assert_parity(info, d, "cg_w20_weighted", rtol=1e-7, xtol=1e-6, prefix_steps=100, tail_rtol=0.2,
-                    final_atol=1e-8 * d["cg_w20_weighted_resnorms"][0])
+    ref = d["cg_w20_weighted_resnorms"]
+    H.assert_parity(info, d, "cg_w20_weighted", rtol=1e-10, xtol=1e-6, noise=H.selfnoise_envelope("cg_w20_weighted", ref),
+                    final_atol=1e-8 * ref[0])
 
 
 def _restart_dev(hist, ref):
@@ -251,9 +253,19 @@ def test_restarted_gmres_matches_reference_chaining(golden):
     assert infos[-1].success and not any(i.success for i in infos[:-1])
     assert all(i.numsteps == 30 for i in infos[:-1])
     assert hist.shape == ref.shape
-    rel = _restart_dev(hist, ref)
-    print(f"\nrestart rand5k: {len(infos)} cycles, history max rel {np.max(rel):.2e}")
+    # every entry but the last within 1e-10 rel (the cycles' first entries are
+    # explicit residuals ||b - A x_c|| too, at 1e-8..1e-3 of ||b||: measured
+    # <= 1e-12 rel); the last one, the explicit residual at convergence
+    # (~1e-8 ||b||), is cancellation-dominated and compared with the absolute
+    # bound of the other parity tests, 64 eps (||b|| + ||A||_1 ||x||)
+    rel = _restart_dev(hist[:-1], ref[:-1])
+    normA1 = float(abs(R).sum(axis=0).max())
+    bound = 64 * np.finfo(float).eps * (np.linalg.norm(b) + normA1 * np.linalg.norm(d["gmres_restart_x"]))
+    fin = abs(hist[-1] - ref[-1]) / bound
+    print(f"\nrestart rand5k: {len(infos)} cycles, history max rel {np.max(rel):.2e}, final explicit residual "
+          f"{fin:.2e} of its bound")
     assert np.max(rel) <= 1e-10, (np.max(rel), int(np.argmax(rel)))
+    assert fin <= 1.0
     xr = d["gmres_restart_x"]
     np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-9 * np.max(np.abs(xr)))
     assert np.linalg.norm(b - R @ x) <= 1e-8 * np.linalg.norm(b)
