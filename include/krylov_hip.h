@@ -179,7 +179,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
 int kry_cg_preferred_chunk(kry_cg *s, int32_t *steps);
 /* Which path the last kry_cg_run chunk took (host-side bookkeeping, no
  * device work): info[0] = 1 if it ran as the persistent small-n loop (one
- * cooperative launch per chunk), 0 if launch per pass; info[1] = chunks that
+ * launch per chunk), 0 if launch per pass; info[1] = chunks that
  * were rerun launch per pass after an in-launch exchange timed out (a block
  * that never became resident). The rerun starts from the chunk-start state,
  * which the persistent loop never overwrites, so the history is that of an
@@ -192,7 +192,10 @@ int kry_cg_path(kry_cg *s, int32_t *info);
  * kry_cg_run chunk used it; info[1] = chunks whose remaining steps were rerun
  * with separate passes after its exchange timed out (it writes nothing
  * before the exchange completes). KRY_CG_UPD=0 disables it; KRY_CGU_FAULT=t
- * makes the last block drop out at step t of a chunk (tests). */
+ * makes the last block drop out at step t of a chunk (tests). info[0] = 2:
+ * the last chunk ran the block path (2 <= k <= 8 on the diagonal-offset
+ * image) with each step's y / p pass folded into the next step's SpMV
+ * (KRY_CG_FUSEP=1 enables it; measured slower, off by default). */
 int kry_cg_update_path(kry_cg *s, int32_t *info);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);

@@ -63,11 +63,13 @@ class _CGState:
         return bool(info[0]), int(info[1])
 
     def update_path(self):
-        """(one_launch_update, fallbacks) of the launch-per-pass form
-        (kry_cg_update_path)."""
+        """(path, fallbacks) of the launch-per-pass form (kry_cg_update_path):
+        path 1 (== True) = the one-launch update (k = 1), 2 = the block path
+        with the y / p pass folded into the next SpMV, 0 (== False) = separate
+        passes."""
         info = (ctypes.c_int32 * 2)()
         check(lib.kry_cg_update_path(self.h, info))
-        return bool(info[0]), int(info[1])
+        return int(info[0]), int(info[1])
 
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)

@@ -72,6 +72,13 @@ struct kry_cg {
   int upd_fallbacks = 0;
   bool upd_used = false;  // an update kernel was launched in the current chunk
   bool upd_last = false;  // ... in the last kry_cg_run chunk
+  // block right-hand sides on the DIA image: the y / p pass folded into the
+  // next SpMV (EpiCgApY); p alternates between p and p_alt within a chunk.
+  // fusep = -1 undecided, 0 not used, 1 used
+  void *p_alt = nullptr;
+  int fusep = -1;
+  bool fusep_used = false;  // the current chunk ran it
+  bool fusep_last = false;  // ... the last kry_cg_run chunk
 };
 
 namespace {
@@ -158,6 +165,41 @@ struct OpCgP {
       pv[v] = rv[v] + t;
     }
     VIO<V>::store(p, e, N, pv);
+  }
+};
+
+// The end of a chunk of the fused-p block path: the deferred update of the
+// last step that ran, m - 1 (m = min(stop_at, steps) >= 1; the launch is
+// skipped when no step ran): yk += alpha p_{m-1} (cg.py:196) and p_m = r_m +
+// omega p_{m-1} (cg.py:178) into the solver's own p buffer, p_{m-1} being in
+// p0 (m - 1 even) or p1 (odd). Leaves the state a separate y / p pass leaves.
+template <typename V>
+struct OpCgYPFinal {
+  V *y, *p0;
+  const V *p1, *r;
+  const double *alpha, *omega;
+  const Ctrl *ctrl;
+  int steps, k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    const int m = ctrl->stop_at < steps ? ctrl->stop_at : steps;
+    const V *src = ((m - 1) & 1) ? p1 : p0;
+    V yv[W], pv[W], rv[W];
+    VIO<V>::load_nt(y, e, N, yv);
+    VIO<V>::load(src, e, N, pv);
+    VIO<V>::load(r, e, N, rv);
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const int c = (int)((e + v) & (k - 1));
+      const V a = (V)alpha[c];
+      const V t1 = a * pv[v];
+      yv[v] = yv[v] + t1;
+      const V om = (V)omega[c];
+      const V t = om * pv[v];
+      pv[v] = rv[v] + t;
+    }
+    VIO<V>::store_nt(y, e, N, yv);
+    VIO<V>::store(p0, e, N, pv);
   }
 };
 
@@ -995,6 +1037,89 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
   return true;
 }
 
+// Block right-hand sides (2 <= k <= 8) on the diagonal-offset image, no M /
+// Ml: the y / p pass of step s - 1 runs inside the SpMV of step s (SrcCgP +
+// EpiCgApY), so an iteration is SpMV (reads r, p, y; writes p', Ap, y), the
+// alpha kernel, the r pass (r -= alpha Ap, <r, r>) and the one-block rho
+// kernel (omega, history, stop test): 9 vectors per iteration instead of 10,
+// bitwise the same iterates. Measured SLOWER, so off unless KRY_CG_FUSEP=1:
+// on cfg4 (Poisson 3163^2, k = 8) the SpMV that gathers r and p_{s-1} and
+// updates y takes 1.30 ms against 0.44 ms for the plain one, 1.71 against
+// 1.32 ms per iteration (profiles/r03_cfg4_fusep.txt): the doubled x-run
+// traffic through L2 costs far more than the 640 MB pass it saves.
+template <typename V, typename MV, typename I>
+bool fusep_eligible(kry_cg *s) {
+  if (s->fusep < 0) {
+    const char *e = getenv("KRY_CG_FUSEP");
+    constexpr int CPLB = 16 / (int)sizeof(V);
+    s->fusep = ((e && atoi(e) == 1) && sizeof(I) == 4 && s->A->dia && s->k >= CPLB && s->k >= 2 && s->k <= 8 &&
+                !s->M && !s->Ml && !dia_blk_off())
+                   ? 1
+                   : 0;
+    if (s->fusep) {
+      const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * sizeof(V);
+      s->p_alt = dev_alloc(vb);
+    }
+  }
+  return s->fusep == 1;
+}
+
+template <typename V, typename MV, typename I>
+void cg_run_fusep(kry_cg *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  double *partA = s->part, *partB = s->part + part_rows(k) * k;
+  V *P[2] = {static_cast<V *>(s->p), static_cast<V *>(s->p_alt)};
+  V *r = static_cast<V *>(s->r), *y = static_cast<V *>(s->y), *Ap = static_cast<V *>(s->Ap);
+  double *gb = s->comm ? s->gbuf : nullptr;
+  for (int step = 0; step < max_steps; ++step) {
+    int PA, PB;
+    {
+      ProfScope ps(s->ctx, PROF_SPMV);
+      if (step == 0)  // p is the solver's own (the previous chunk ended with its y / p update)
+        launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{P[0], k}, EpiApDot<V>{Ap, s->w, k}, partA, &PA, s->ctrl, step,
+                              st);
+      else
+        launch_spmv<V, MV, I>(s->A, k, SrcCgP<V>{r, P[(step - 1) & 1], s->scal + S_OMEGA * k, k, 0},
+                              EpiCgApY<V>{Ap, P[step & 1], P[(step - 1) & 1], y, s->scal + S_ALPHA * k, s->w, k},
+                              partA, &PA, s->ctrl, step, st);
+    }
+    if (s->scalar_f32)
+      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                         step);
+    else
+      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                         step);
+    {
+      ProfScope ps(s->ctx, PROF_UPDATE);
+      PB = launch_elementwise<V>(N, k, OpCgR<V>{r, Ap, s->scal + S_ALPHA * k, s->w, k}, partB, s->ctrl, step, st,
+                                 kCgUpdateGrid);
+    }
+    if (s->scalar_f32)
+      hipLaunchKernelGGL(cg_rho_kernel<float>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist, s->ctrl,
+                         step, gb, s->col_offset, s->total_k);
+    else
+      hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
+                         s->ctrl, step, gb, s->col_offset, s->total_k);
+    KRY_HIP(hipGetLastError());
+    if (s->comm) {
+      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k, ncclDouble, ncclSum, s->comm->comm, st);
+      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      hipLaunchKernelGGL(cg_global_check, dim3(1), dim3(kBlock), 0, st, s->gbuf, s->gcrit, s->total_k, s->hist,
+                         s->ctrl, step);
+      KRY_HIP(hipGetLastError());
+    }
+  }
+  // the deferred y / p update of the last step that ran (none ran: stop_at = 0, skipped)
+  ProfScope ps(s->ctx, PROF_OTHER);
+  launch_elementwise<V>(N, k,
+                        OpCgYPFinal<V>{y, P[0], P[1], r, s->scal + S_ALPHA * k, s->scal + S_OMEGA * k, s->ctrl,
+                                       max_steps, k},
+                        nullptr, s->ctrl, 0, st);
+  s->fusep_used = true;
+}
+
 // Returns true when the chunk ran as one persistent launch.
 template <typename V, typename MV, typename I>
 bool cg_run_impl(kry_cg *s, int max_steps) {
@@ -1002,6 +1127,10 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   if (cgp_launch<V, MV, I>(s, max_steps)) return true;
+  if (fusep_eligible<V, MV, I>(s)) {
+    cg_run_fusep<V, MV, I>(s, max_steps);
+    return false;
+  }
   double *partA = s->part, *partB = s->part + part_rows(k) * k;
   for (int step = 0; step < max_steps; ++step) {
     V *p = static_cast<V *>(s->p);
@@ -1127,7 +1256,7 @@ static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
                   s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
                   s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
-                  s->cgp_scal, s->cgp_words, s->upd_words};
+                  s->cgp_scal, s->cgp_words, s->upd_words, s->p_alt};
   for (void *b : bufs) dev_free(b);
 }
 
@@ -1247,6 +1376,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     reset_ctrl(s->ctrl, st);
     bool persistent = false;
     s->upd_used = false;
+    s->fusep_used = false;
     dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) {
       persistent = cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, steps);
     });
@@ -1288,6 +1418,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: device error status " + std::to_string(c.status));
   s->cgp_last = persistent;
   s->upd_last = upd;
+  s->fusep_last = s->fusep_used;
   s->it += done;
   *steps_done = done;
   KRY_API_END
@@ -1319,7 +1450,7 @@ int kry_cg_path(kry_cg *s, int32_t *info) {
 int kry_cg_update_path(kry_cg *s, int32_t *info) {
   KRY_API_BEGIN
   KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
-  info[0] = s->upd_last ? 1 : 0;
+  info[0] = s->upd_last ? 1 : (s->fusep_last ? 2 : 0);
   info[1] = s->upd_fallbacks;
   KRY_API_END
 }

@@ -154,3 +154,59 @@ def test_cfg5_minres_weighted_fp32(full):
     print(f"\ncfg5_minres: history max rel {rel:.2e} (tol 1e-4), x samples {xdev:.2e} of max|x|")
     assert rel <= 1e-4
     assert xdev <= 1e-4
+
+
+def _check_restart(F, prefix, A, b, max_cycles, xtol):
+    """x0-chained GMRES(30) (krylov_amd.gmres_restarted, the chaining of
+    make_fullsize.restart_chain) against the reference's own chained run:
+    the same cycles with the same step counts and success flags, every entry
+    of the chained history within 1e-10 rel (each cycle starts from the
+    explicit residual ||b - A x_c||; the very last entry of a converged run is
+    the explicit residual at convergence, compared with the absolute bound
+    64 eps (||b|| + ||A||_1 ||x||)), and the iterate's samples / summaries."""
+    import krylov_amd
+
+    x, infos = krylov_amd.gmres_restarted(krylov_amd.CsrOperator(A), b, restart=30, tol=1e-8, max_cycles=max_cycles)
+    steps = np.array([i.numsteps for i in infos])
+    succ = np.array([bool(i.success) for i in infos])
+    np.testing.assert_array_equal(steps, F[f"{prefix}_cycle_steps"])
+    np.testing.assert_array_equal(succ, F[f"{prefix}_cycle_success"])
+    hist = np.concatenate([np.asarray(i.resnorms, dtype=np.float64) for i in infos])
+    ref = F[f"{prefix}_hist"]
+    assert hist.shape == ref.shape
+    last_explicit = bool(succ[-1])
+    body = slice(0, len(ref) - 1) if last_explicit else slice(0, len(ref))
+    rel = np.max(np.abs(hist[body] - ref[body]) / np.abs(ref[body]))
+    rstats = F[f"{prefix}_xstats"]
+    fin = 0.0
+    if last_explicit:
+        normA1 = float(abs(A).sum(axis=0).max())
+        bound = 64 * EPS * (np.linalg.norm(b) + normA1 * rstats[1])
+        fin = abs(hist[-1] - ref[-1]) / bound
+    xa = np.abs(np.asarray(x, dtype=np.float64))
+    stats = np.array([xa.sum(), np.sqrt((xa * xa).sum()), xa.max()])
+    xs = np.asarray(x)[_sample(len(b), int(F["nsample"]))]
+    xdev = np.max(np.abs(xs - F[f"{prefix}_xsample"]) / rstats[2])
+    sdev = np.max(np.abs(stats - rstats) / rstats)
+    print(f"\n{prefix}: {len(infos)} cycles {steps.tolist()}, chained history max rel {rel:.2e}, final explicit "
+          f"{fin:.2e} of its bound, x samples {xdev:.2e} of max|x|, x summaries {sdev:.2e} rel")
+    assert rel <= 1e-10
+    assert fin <= 1.0
+    assert xdev <= xtol and sdev <= xtol
+
+
+def test_metric_gmres30_restarted(full, stencil216):
+    """north_star: GMRES(30) on the metric matrix, restarted through x0 as the
+    reference is driven (10 cycles of the 1e-8 chaining: 300 Arnoldi steps,
+    residual 3175 -> 337), against the reference's own chained history."""
+    b = np.ones(stencil216.shape[0])
+    _check_restart(full, "metric_gmres30_restart", stencil216, b, 10, 1e-9)
+
+
+def test_cfg3_gmres30_restarted_to_convergence(full):
+    """cfg3: GMRES restart=30 converging to 1e-8 relative (2 cycles, 30 + 26
+    steps), against the reference's own chained run."""
+    from krylov_amd import problems
+
+    R = problems.random_nonsym(2_000_000)
+    _check_restart(full, "cfg3_gmres30_restart", R, np.ones(R.shape[0]), 20, 1e-9)

@@ -206,3 +206,15 @@ def test_oracle_fullsize_cfg3_gmres30():
                                rtol=1e-12, atol=0)
     idx = np.sort(np.random.default_rng(12345).choice(R.shape[0], int(F["nsample"]), replace=False))
     np.testing.assert_allclose(info.xk[idx], F["cfg3_gmres30_xsample"], rtol=1e-12, atol=0)
+
+
+def test_oracle_fullsize_cfg3_restart_chain():
+    """The oracle's x0-chained GMRES(30) on cfg3 to 1e-8 against the
+    reference's own chained run (fullsize.npz cfg3_gmres30_restart_*)."""
+    F = np.load(os.path.join(os.path.dirname(__file__), "golden", "fullsize.npz"))
+    R = problems.random_nonsym(2_000_000)
+    hist, x, cycles = oracle_restart_chain(R, np.ones(R.shape[0]), 30, 1e-8, 20)
+    assert cycles == len(F["cfg3_gmres30_restart_cycle_steps"])
+    np.testing.assert_allclose(hist, F["cfg3_gmres30_restart_hist"], rtol=1e-12, atol=0)
+    idx = np.sort(np.random.default_rng(12345).choice(R.shape[0], int(F["nsample"]), replace=False))
+    np.testing.assert_allclose(x[idx], F["cfg3_gmres30_restart_xsample"], rtol=1e-11, atol=0)

@@ -54,25 +54,29 @@ def main(out):
     mf, bf, bw = f("micro", "FETCH_SIZE"), f("bench", "FETCH_SIZE"), f("bench", "WRITE_SIZE")
     cal_fetch, _ = find(mf, "dia_probe<16, 4>")
     scale = 8.0 * slots / cal_fetch
-    fetch, name = find(bf, "spmv_dia_kernel", "EpiApDot")
-    write, _ = find(bw, "spmv_dia_kernel", "EpiApDot")
     alg = bench.spmv_S(n, nnz)
-    phys = 8.0 * slots + 20.0 * slots / 128 + 2.0 * n * 8  # values, per-column offset + 2 masks, x and Ap
+    kernels = {}
+    for key, parts in (("dia", ("spmv_dia_kernel", "EpiApDot")), ("sell", ("spmv_sell_kernel", "EpiApDot"))):
+        fetch, name = find(bf, *parts)
+        write, _ = find(bw, *parts)
+        traffic = fetch * scale + write
+        kernels[key] = {
+            "kernel": name,
+            "fetch_raw_bytes": fetch,
+            "write_bytes": write,
+            "traffic_bytes_per_launch": traffic,
+            "traffic_over_algorithmic_S": traffic / alg,
+        }
     res = {
-        "kernel": name,
-        "fetch_raw_bytes": fetch,
-        "write_bytes": write,
         "read_scale_from_calibration": scale,
-        "calibration": "dia_probe<16,4> (tools/dia_bench 'values only'): the diagonal-offset image's 16 B/lane (two rows' values) "
-                       "nontemporal value stream, 8 B x dia_slots known bytes, FETCH_SIZE x 1024 measured",
-        "traffic_bytes_per_launch": fetch * scale + write,
+        "calibration": "dia_probe<16,4> (tools/dia_bench 'values only'): the diagonal-offset image's 16 B/lane (two "
+                       "rows' values) nontemporal value stream, 8 B x dia_slots known bytes, FETCH_SIZE x 1024 measured",
+        "kernels": kernels,
         "algorithmic_bytes_per_launch": alg,
-        "image_bytes_per_launch": phys,
-        "traffic_over_algorithmic": (fetch * scale + write) / alg,
-        "traffic_over_image": (fetch * scale + write) / phys,
         "dia_slots": slots,
         "n": n,
         "nnz": nnz,
+        "program": "tools/spmv_legs.py 64 (64 metric CG iterations on each image)",
     }
     print(json.dumps(res, indent=1))
 
