@@ -462,7 +462,12 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int G = gridDim.x;
-  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // fault injection (tests, KRY_MGS_FAULT)
+  // fault injection (tests, KRY_MGS_FAULT): the last block drops out at chunk
+  // step fault_step, at its start, or (KRY_MGS_FAULT_FINAL=1, bit 16) at the
+  // final normalising exchange, after the other blocks' passes are done
+  const bool fault_here = fault_step >= 0 && (fault_step & 0xffff) == step && (int)blockIdx.x == G - 1;
+  const bool fault_final = (fault_step >> 16) == 1;
+  if (fault_here && !fault_final) return;
   const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   auto abort_step = [&]() {
     if (tid == 0) atomicMin(&ctrl->stop_at, step);
@@ -606,6 +611,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       // its registers; w itself is not written back. The QR kernel reads
       // the exchanged sum as a single partial row (slot 2, row 0).
       double *tot = pbuf + (size_t)2 * G * k;
+      if (fault_here) return;  // KRY_MGS_FAULT_FINAL: never joins the normalising exchange
       if (k == 1) {
         unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
         const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
@@ -1346,7 +1352,8 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   double *pbuf = s->part2;  // [pass parity 0 | parity 1 | last pass], G * k each
   ProfScope ps(s->ctx, PROF_MGS);
   const char *fe = getenv("KRY_MGS_FAULT");  // fault injection (tests): chunk step at which a block drops out
-  const int fault_step = fe ? atoi(fe) : -1;
+  const char *ff = getenv("KRY_MGS_FAULT_FINAL");  // ... at the streamed kernel's final exchange instead
+  const int fault_step = fe ? (atoi(fe) | ((ff && atoi(ff) == 1) ? (1 << 16) : 0)) : -1;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
                        pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step);

@@ -214,3 +214,37 @@ def test_cg_update_kernel_matches_separate_passes(monkeypatch):
     np.testing.assert_allclose(h1, h0, rtol=1e-12)
     _, ref = krylov_ref.cg(P, b, tol=0.0, atol=0.0, maxiter=40)
     np.testing.assert_allclose(h1, np.asarray(ref.resnorms)[1:41], rtol=1e-10)
+
+
+@pytest.mark.parametrize("fault_step", [0, 5])
+def test_streamed_mgs_timeout_at_final_exchange(monkeypatch, fault_step):
+    """The streamed persistent MGS kernel (gm_mgsl_kernel, chosen above 2 M
+    unknowns: 15-point stencil 140^3, n = 2.74 M) timing out at its final,
+    normalising exchange (KRY_MGS_FAULT_FINAL): the other blocks have already
+    written their segments of V_{k+1} and block 0 its h entries. The host
+    reruns the step from its SpMV on the per-pass kernels, which rewrite both,
+    so the history and iterate equal a clean solve's."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.gmres import _GmresState
+
+    S = problems.stencil15_3d(140)
+    A = krylov_amd.CsrOperator(S)
+    b = np.random.default_rng(17).standard_normal(S.shape[0])
+    _, clean = krylov_amd.gmres(A, b, maxiter=20, tol=0.0)
+    st = _GmresState(_helpers.Problem(A, b, None, None), 20, 1)
+    st.start()
+    st.set_criterion(np.zeros(1))
+    st.run(3)
+    assert st.path() == (True, 0)  # the persistent (streamed) MGS serves this size
+    monkeypatch.setenv("KRY_MGS_FAULT", str(fault_step))
+    monkeypatch.setenv("KRY_MGS_FAULT_FINAL", "1")
+    _, faulted = krylov_amd.gmres(A, b, maxiter=20, tol=0.0)
+    assert faulted.numsteps == clean.numsteps == 20
+    np.testing.assert_allclose(np.asarray(faulted.resnorms)[:-1], np.asarray(clean.resnorms)[:-1], rtol=1e-11)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-9, atol=1e-12 * np.abs(clean.xk).max())
+    st = _GmresState(_helpers.Problem(A, b, None, None), 20, 1)
+    st.start()
+    st.set_criterion(np.zeros(1))
+    hist, _ = st.run(8)
+    assert len(hist) == 8 and st.path() == (False, 1)
