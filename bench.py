@@ -263,6 +263,27 @@ def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"
             "n": R.shape[0], "nnz": int(R.nnz), "config": label}
 
 
+def run_bicgstab(R, iters=30):
+    """krylov_amd.bicgstab on the cfg3 matrix (tol = 0, `iters` iterations,
+    3 SpMVs and 6 inner products each, the scalars chained on the device):
+    the call's rate at the host-array boundary, median of 3 after a warm-up."""
+    import krylov_amd
+
+    A = krylov_amd.CsrOperator(R)
+    b = np.ones(R.shape[0])
+    krylov_amd.bicgstab(A, b, tol=0.0, atol=0.0, maxiter=iters)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        _, info = krylov_amd.bicgstab(A, b, tol=0.0, atol=0.0, maxiter=iters)
+        ts.append(time.perf_counter() - t0)
+        assert info.numsteps == iters
+    t = float(np.median(ts))
+    return {"it_per_s": iters / t, "call_ms": 1e3 * t, "n": R.shape[0], "nnz": int(R.nnz),
+            "config": f"cfg3 random nonsym n=2e6, krylov_amd.bicgstab tol=0 maxiter={iters} (b upload and x download "
+                      "included)"}
+
+
 def run_end_to_end(A_host, steps):
     """The reference API at the host-array boundary: krylov_amd.cg(A, b) and
     gmres(A, b, maxiter=30) with numpy b in and numpy x out, on an operator
@@ -494,9 +515,12 @@ def main():
     del P3
     if world == 1 and not args.quick and args.workload == "metric":
         out["spmv_general"] = run_spmv_general(A_host, args.steps)
-        g = run_gmres()
+        R3 = problems.random_nonsym(2_000_000)
+        g = run_gmres(R3)
         out["gmres30_it_per_s"] = g["it_per_s"]
         out["gmres"] = g
+        out["bicgstab_cfg3"] = run_bicgstab(R3)
+        del R3
         # north_star: GMRES(30) on the same (metric) matrix
         out["gmres_metric"] = run_gmres(A_host, f"metric 15-point {args.m}^3, GMRES(30) mgs, one cycle")
         out["end_to_end"] = run_end_to_end(A_host, args.steps)

@@ -37,6 +37,7 @@ typedef struct kry_cg kry_cg;
 typedef struct kry_gmres kry_gmres;
 typedef struct kry_minres kry_minres;
 typedef struct kry_comm kry_comm;
+typedef struct kry_prog kry_prog;
 
 /* value / index types */
 enum { KRY_F32 = 1, KRY_F64 = 2 };
@@ -146,6 +147,47 @@ int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y);
  * solvers (bicgstab.py, cgs.py, cgr.py, gcr.py; krylov_amd/extra.py). */
 int kry_vec_lincomb(kry_ctx *ctx, int form, kry_vec *z, kry_vec *x, kry_vec *y, kry_vec *w,
                     const double *a, const double *b);
+/* ---- device-resident scalar chain of the other solvers --------------------
+ * bicgstab.py:24-144, cgs.py:24-117, cgr.py:16-100, gcr.py:18-97 (driven by
+ * krylov_amd/extra.py): the per-iteration scalars live in a device register
+ * file of nregs rows of k float64 values, so a chunk of iterations is
+ * enqueued with no host round trip and read back with one sync.
+ * create: nregs registers, k columns (power of two <= 64), history capacity
+ *         `cap` steps per chunk.
+ * set / get: register r (r = -1 in set: the criterion row, +inf on padded
+ *         columns) from / to k host doubles (synchronous).
+ * begin: start a chunk (every step runs until a check stops it).
+ * scalar: register ops of the reference's scalar lines, float64:
+ *         op 0 d = a; 1 d = a / g(b); 2 d = (a * b) / g(c * e); 3 d = sqrt(a);
+ *         4 d = g(a); 5 d = value   (g(x) = x != 0 ? x : 1, np.where guard)
+ * dot:   register d = inner(x, y) per column (w: weights or NULL).
+ * lincomb: kry_vec_lincomb's forms with a = sa * reg[ra], b = sb * reg[rb]
+ *         (register -1 = unused; sa, sb = +1 / -1).
+ * spmv:  y = A x.
+ * check: register r against the criterion: mode 0 appends it to the chunk
+ *         history and stops the chunk after this step when every column
+ *         meets it; mode 1 (bicgstab's mid-step test on the previous iterate,
+ *         bicgstab.py:123-127) stops the chunk AT this step on success and
+ *         records its row there; mode | 4: compare the norm rounded to
+ *         float32 (the history of a float32 solve).
+ * end:   one sync: *done steps ran in full, *midstep = 1 if a mode-1 check
+ *         stopped step *done; rows receives done (+ midstep) rows of k.
+ * Every launch takes the chunk step it belongs to and does nothing once a
+ * check has stopped the chunk before it. */
+int kry_prog_create(kry_ctx *ctx, int32_t nregs, int32_t k, int32_t cap, kry_prog **out);
+int kry_prog_destroy(kry_prog *p);
+int kry_prog_set(kry_prog *p, int32_t r, const double *vals);
+int kry_prog_get(kry_prog *p, int32_t r, double *vals);
+int kry_prog_begin(kry_prog *p);
+int kry_prog_end(kry_prog *p, int32_t steps, int32_t *done, int32_t *midstep, double *rows);
+int kry_prog_scalar(kry_prog *p, int32_t op, int32_t d, int32_t a, int32_t b, int32_t c, int32_t e, double value,
+                    int32_t step);
+int kry_prog_dot(kry_prog *p, kry_vec *x, kry_vec *y, kry_vec *w, int32_t d, int32_t step);
+int kry_prog_lincomb(kry_prog *p, int32_t form, kry_vec *z, kry_vec *x, kry_vec *y, kry_vec *w, int32_t ra, double sa,
+                     int32_t rb, double sb, int32_t step);
+int kry_prog_spmv(kry_prog *p, kry_csr *A, kry_vec *x, kry_vec *y, int32_t step);
+int kry_prog_check(kry_prog *p, int32_t r, int32_t mode, int32_t step);
+
 /* Batched LAPACK >= 3.10 ?lartg on device (givens.py:35-40); host arrays of
  * `count` values of `dtype`. Bitwise equal to scipy.linalg.lapack ?lartg. */
 int kry_lartg(kry_ctx *ctx, int64_t count, int dtype, const void *f, const void *g,

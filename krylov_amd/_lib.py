@@ -114,6 +114,17 @@ _SIGNATURES = {
     "kry_profile_enable": [_vp, _int],
     "kry_profile_select": [_vp, ctypes.c_uint32, ctypes.c_int32],
     "kry_profile_read": [_vp, _int, _ip64, _dp],
+    "kry_prog_create": [_vp, _i32, _i32, _i32, _pvp],
+    "kry_prog_destroy": [_vp],
+    "kry_prog_set": [_vp, _i32, _dp],
+    "kry_prog_get": [_vp, _i32, _dp],
+    "kry_prog_begin": [_vp],
+    "kry_prog_end": [_vp, _i32, _ip32, _ip32, _dp],
+    "kry_prog_scalar": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.c_double, _i32],
+    "kry_prog_dot": [_vp, _vp, _vp, _vp, _i32, _i32],
+    "kry_prog_lincomb": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, ctypes.c_double, _i32, ctypes.c_double, _i32],
+    "kry_prog_spmv": [_vp, _vp, _vp, _vp, _i32],
+    "kry_prog_check": [_vp, _i32, _i32, _i32],
     "kry_mem_stats": [_ip64],
     "kry_mem_release": [],
 }

@@ -236,6 +236,21 @@ __global__ __launch_bounds__(kAlphaBlock) void cg_alpha_kernel(const double *par
   }
 }
 
+// First stage of the alpha reduction when the SpMV left many block partials
+// (the block DIA kernel at cfg4: 19,541 rows of k): block b sums rows
+// [b P / G, (b + 1) P / G) in reduce_partials' fixed order into row b of
+// `out`, so the one-block alpha kernel sums G rows instead of P (one block
+// reading 1.25 MB took 29 us per iteration, profiles/r03_bench_kernel_stats.csv).
+constexpr int kAlphaStage = 128;
+__global__ __launch_bounds__(kBlock) void partial_stage_kernel(const double *part, int P, int k, double *out,
+                                                               const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  const int r0 = (int)((int64_t)blockIdx.x * P / gridDim.x), r1 = (int)((int64_t)(blockIdx.x + 1) * P / gridDim.x);
+  reduce_partials(part + (int64_t)r0 * k, r1 - r0, k, red);
+  if ((int)threadIdx.x < k) out[(int64_t)blockIdx.x * k + threadIdx.x] = red[threadIdx.x];
+}
+
 // rhos = [rhos[-1], <r, r>]; omega for the next p-update; resnorm =
 // sqrt(<r, r>); global stop test (cg.py:209-217, 156, 177).
 template <typename S>
@@ -1047,6 +1062,26 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
 // updates y takes 1.30 ms against 0.44 ms for the plain one, 1.71 against
 // 1.32 ms per iteration (profiles/r03_cfg4_fusep.txt): the doubled x-run
 // traffic through L2 costs far more than the 640 MB pass it saves.
+// alpha = rho / <p, Ap> from the SpMV's PA partial rows (cg_alpha_kernel),
+// through partial_stage_kernel first when there are many; `scratch` (k x
+// kAlphaStage doubles) is free until the r pass writes its partials there.
+static void launch_alpha(kry_cg *s, const double *partA, int PA, double *scratch, int step) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  if (PA > 4 * kAlphaStage) {
+    hipLaunchKernelGGL(partial_stage_kernel, dim3(kAlphaStage), dim3(kBlock), 0, st, partA, PA, k, scratch, s->ctrl,
+                       step);
+    partA = scratch;
+    PA = kAlphaStage;
+  }
+  if (s->scalar_f32)
+    hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl, step);
+  else
+    hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
+                       step);
+  KRY_HIP(hipGetLastError());
+}
+
 template <typename V, typename MV, typename I>
 bool fusep_eligible(kry_cg *s) {
   if (s->fusep < 0) {
@@ -1085,12 +1120,7 @@ void cg_run_fusep(kry_cg *s, int max_steps) {
                               EpiCgApY<V>{Ap, P[step & 1], P[(step - 1) & 1], y, s->scal + S_ALPHA * k, s->w, k},
                               partA, &PA, s->ctrl, step, st);
     }
-    if (s->scalar_f32)
-      hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
-                         step);
-    else
-      hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
-                         step);
+    launch_alpha(s, partA, PA, partB, step);
     {
       ProfScope ps(s->ctx, PROF_UPDATE);
       PB = launch_elementwise<V>(N, k, OpCgR<V>{r, Ap, s->scal + S_ALPHA * k, s->w, k}, partB, s->ctrl, step, st,
@@ -1151,12 +1181,7 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     if (!s->M && !s->Ml && k == 1 && cgu_launch<V>(s, partA, PA, step, gb)) {
       // alpha, r, rho, omega, y and p in one launch (cg_upd_kernel)
     } else if (!s->M && k <= 8) {  // alpha kernel, r pass, then the fused rho / y / p pass
-      if (s->scalar_f32)
-        hipLaunchKernelGGL(cg_alpha_kernel<float>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
-                           step);
-      else
-        hipLaunchKernelGGL(cg_alpha_kernel<double>, dim3(1), dim3(kAlphaBlock), 0, st, partA, PA, k, s->scal, s->ctrl,
-                           step);
+      launch_alpha(s, partA, PA, partB, step);
       {
         ProfScope ps(s->ctx, PROF_UPDATE);
         PB = launch_elementwise<V>(N, k,

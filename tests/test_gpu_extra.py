@@ -1,0 +1,93 @@
+"""bicgstab / cgs / cgr / gcr on the device-resident scalar chain
+(krylov_amd/extra.py over kry_prog_*): a chunk of iterations is enqueued with
+no host round trip and ends with one sync. The reference fixtures of these
+solvers are checked in tests/test_gpu_precond.py; here: the chain's own
+semantics, and that chunking changes nothing (a run with a callback goes one
+iteration per chunk)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _chain(k=4, cap=8):
+    from krylov_amd import _helpers, extra, problems
+
+    prob = _helpers.Problem(problems.poisson2d(16), np.ones((256, k)), None, None)
+    D = extra._Dev(prob)
+    return extra._Chain(D, ["a", "b", "c", "d", "n"], cap=cap), D
+
+
+def test_chain_scalar_ops_and_checks():
+    from krylov_amd import extra
+
+    C, D = _chain()
+    a = np.array([3.0, -2.0, 0.0, 5.0])
+    b = np.array([2.0, 0.0, 4.0, -1.0])
+    C.set("a", a)
+    C.set("b", b)
+    C.set(None, np.array([1.0, 1.0, 1.0, np.inf]))
+    C.begin()
+    C.sc(extra.SOP_DIVG, "c", 0, a="a", b="b")
+    C.sc(extra.SOP_MULDIVG, "d", 0, a="a", b="b", c="b", e="a")
+    C.sc(extra.SOP_GUARD, "n", 0, a="a")
+    C.end(1)
+    g = np.where(b != 0, b, 1.0)
+    np.testing.assert_array_equal(C.get("c"), a / g)
+    np.testing.assert_array_equal(C.get("d"), (a * b) / np.where(b * a != 0, b * a, 1.0))
+    np.testing.assert_array_equal(C.get("n"), np.where(a != 0, a, 1.0))
+    # mode 0: appended every step, the chunk stops after the step that meets the criterion
+    C.begin()
+    for st, v in enumerate([5.0, 2.0, 0.5, 0.1]):
+        C.sc(extra.SOP_SET, "n", st, value=v)
+        C.check("n", st)
+    rows, mid = C.end(4)
+    assert mid is None and len(rows) == 3
+    np.testing.assert_array_equal(rows[:, 0], [5.0, 2.0, 0.5])
+    # mode 1 (bicgstab's mid-step test): stops AT the step, its row reported apart
+    C.begin()
+    for st, v in enumerate([5.0, 4.0, 0.25, 0.1]):
+        C.sc(extra.SOP_SET, "n", st, value=v + 10.0)
+        C.check("n", st)  # never met
+        C.sc(extra.SOP_SET, "a", st, value=v)
+        C.check("a", st, mode=1)
+    rows, mid = C.end(4)
+    assert len(rows) == 2 and mid is not None and mid[0] == 0.25
+    # launches of steps after a stop do nothing
+    C.set("c", np.zeros(4))
+    C.begin()
+    C.sc(extra.SOP_SET, "n", 0, value=0.0)
+    C.check("n", 0)
+    C.sc(extra.SOP_SET, "c", 1, value=7.0)
+    C.end(2)
+    np.testing.assert_array_equal(C.get("c"), np.zeros(4))
+
+
+@pytest.mark.parametrize("solver", ["bicgstab", "cgs", "cgr", "gcr"])
+def test_extra_solvers_chunking_is_invisible(solver):
+    """Chunks of 32 iterations against one iteration per chunk (callback):
+    bitwise the same history and iterate, the callback seeing every iterate,
+    and the oracle's history to round-off. The matrices are ones on which the
+    reference's history is stable in the summation order (the random
+    nonsymmetric one; Poisson for cgr, which needs symmetry): on Poisson 40^2
+    bicgstab is not (the oracle with a pairwise dot takes 101 steps instead
+    of 98), and the oracle with a pairwise dot moves by 5e-9 (cgs), 5e-10
+    (bicgstab) and 2e-15 (cgr, gcr) here."""
+    import krylov_amd
+    from krylov_amd import problems
+    from oracle import krylov_ref as K
+
+    A = problems.poisson2d(40) if solver == "cgr" else problems.random_nonsym(5000)
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    kw = dict(tol=1e-9, maxiter=150)
+    _, fast = getattr(krylov_amd, solver)(A, b, **kw)
+    seen = []
+    _, slow = getattr(krylov_amd, solver)(A, b, callback=lambda x, r: seen.append(r.copy()), **kw)
+    assert fast.numsteps == slow.numsteps and fast.success == slow.success
+    np.testing.assert_array_equal(np.asarray(fast.resnorms), np.asarray(slow.resnorms))
+    np.testing.assert_array_equal(fast.xk, slow.xk)
+    assert len(seen) == slow.numsteps + 1
+    _, ref = getattr(K, solver)(A, b, **kw)
+    assert ref.numsteps == fast.numsteps
+    got, want = np.asarray(fast.resnorms), np.asarray(ref.resnorms)
+    np.testing.assert_allclose(got[:-1], want[:-1], rtol=1e-7, atol=1e-14 * want[0])
