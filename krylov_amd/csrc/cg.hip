@@ -1068,7 +1068,11 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
 static void launch_alpha(kry_cg *s, const double *partA, int PA, double *scratch, int step) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
-  if (PA > 4 * kAlphaStage) {
+  static const bool stage = [] {
+    const char *e = getenv("KRY_ALPHA_STAGE");  // A/B switch: 0 = one-block alpha only
+    return !(e && atoi(e) == 0);
+  }();
+  if (stage && PA > 4 * kAlphaStage) {
     hipLaunchKernelGGL(partial_stage_kernel, dim3(kAlphaStage), dim3(kBlock), 0, st, partA, PA, k, scratch, s->ctrl,
                        step);
     partA = scratch;
