@@ -405,14 +405,12 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   const int G = gridDim.x;
   if (fault_step >= 0 && (fault_step & 0xffff) == step && (int)blockIdx.x == G - 1) {
     // fault injection (tests, KRY_CGU_FAULT): the last block drops out, or, with
-    // KRY_CGU_FAULT_LATE = L, joins the exchange after ~L * 1024 polls (about when the
-    // others' shortened spin runs out: either outcome must be consistent)
+    // KRY_CGU_FAULT_LATE = L, joins the exchange L x 0.25 ms late (the others' spin
+    // gives up after kSpinLimitFault = 1 ms: either outcome must be consistent)
     const unsigned late = (unsigned)fault_step >> 16;
     if (late == 0) return;
-    for (unsigned i = 0; i < late * 1024u; ++i) {
-      __builtin_amdgcn_s_sleep(1);
-      (void)__hip_atomic_load(words + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const unsigned long long t0 = wall_clock64();
+    while (!spin_expired(t0, late * (kSpinLimitFault / 4))) __builtin_amdgcn_s_sleep(8);
   }
   const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   const int64_t seg = (int64_t)NV * kUpdBlock * W;

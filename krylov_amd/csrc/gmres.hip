@@ -227,14 +227,16 @@ __device__ bool mgs_wait(unsigned *bar, unsigned epoch, Ctrl *ctrl, int *flag, u
     const unsigned ngroups = G < 8 ? (unsigned)G : 8u;
     int ok = 1;
     unsigned spins = 0;
+    const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ngroups * epoch) {
       __builtin_amdgcn_s_sleep(1);
       ++spins;
-      if ((spins & 255u) == 0 && __hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if ((spins & 255u) != 0) continue;
+      if (__hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         ok = 0;
         break;
       }
-      if (spins > spin_limit) {
+      if (spin_expired(t0, spin_limit)) {
         __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;

@@ -54,10 +54,20 @@ namespace kry {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "the in-launch exchanges of the persistent kernels are validated for gfx950 (MI355X) only"
 #endif
-constexpr unsigned kSpinLimit = 1u << 20;
-// Shorter bound for the fault-injection runs (KRY_CGP_FAULT / KRY_MGS_FAULT),
-// so that a test of the timeout path finishes in milliseconds.
-constexpr unsigned kSpinLimitFault = 1u << 12;
+// Bounds on the exchanges' spins, in ticks of the 100 MHz constant clock
+// (wall_clock64): a block that has not seen every partial after 20 ms gives
+// up (the callers then fall back to kernels that need no co-residency), so a
+// non-resident block costs at most ~20 ms once per solver, not an unbounded
+// or poll-count-dependent stall (round 2 counted 2^20 polls: about a second).
+constexpr unsigned kSpinLimit = 2000000u;
+// Shorter bound for the fault-injection runs (KRY_CGP_FAULT / KRY_MGS_FAULT /
+// KRY_CGU_FAULT / KRY_MRU_FAULT), so that a test of the timeout path
+// finishes in milliseconds: 1 ms.
+constexpr unsigned kSpinLimitFault = 100000u;
+// Time since `t0` has exceeded `limit` ticks (checked every 256 polls).
+__device__ __forceinline__ bool spin_expired(unsigned long long t0, unsigned limit) {
+  return wall_clock64() - t0 > (unsigned long long)limit;
+}
 
 __device__ __forceinline__ void publish_partial(unsigned long long *g, unsigned tag, double v) {
   const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
@@ -87,7 +97,7 @@ __device__ inline unsigned decide_exchange(unsigned *bar, unsigned tag, unsigned
 }
 
 // Wave 0 only; returns the same value in every lane (false = timed out /
-// aborted). AGREE: the commit / abort decision is shared by all blocks
+// aborted). spin_limit: ticks of wall_clock64 (kSpinLimit). AGREE: the commit / abort decision is shared by all blocks
 // (decide_exchange); otherwise a timed-out block only raises bar[9] and a
 // caller that has stored nothing yet re-checks it.
 template <bool AGREE = false>
@@ -96,6 +106,8 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
   const int lane = threadIdx.x;
   unsigned long long g[4][2];
   unsigned spins = 0;
+  bool expired = false;
+  const unsigned long long t0 = wall_clock64();
   bool committed = false;  // AGREE: another block has committed this exchange
   for (;;) {
     bool ok = true;
@@ -113,6 +125,7 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
     ++spins;
     if (committed) continue;
     if ((spins & 255u) == 0) {
+      expired = spin_expired(t0, spin_limit);
       if (AGREE) {
         const unsigned d = __hip_atomic_load(bar + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (d == tag * 4u + kDecAbort) return false;
@@ -121,7 +134,7 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
         return false;
       }
     }
-    if (spins > spin_limit && !committed) {
+    if (expired && !committed) {
       unsigned d = kDecAbort;
       if (AGREE) {
         if (lane == 0) d = decide_exchange(bar, tag, kDecAbort);

@@ -248,3 +248,34 @@ def test_streamed_mgs_timeout_at_final_exchange(monkeypatch, fault_step):
     st.set_criterion(np.zeros(1))
     hist, _ = st.run(8)
     assert len(hist) == 8 and st.path() == (False, 1)
+
+
+def test_exchange_timeout_is_time_bounded(monkeypatch):
+    """The exchanges give up after a fixed time (wall_clock64 ticks, 100 MHz:
+    1 ms under fault injection, 20 ms in production), not after a poll count.
+    A block that never joins costs about that bound once, then the chunk runs
+    on the per-pass kernels: the faulted solve takes ~1 ms longer than the
+    clean one (well under the 2^20-poll stall of round 2)."""
+    import time
+
+    import krylov_amd
+    from krylov_amd import problems
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    R = problems.poisson2d(300)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(18).standard_normal(R.shape[0])
+
+    def timed():
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=64)
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    clean = timed()
+    monkeypatch.setenv("KRY_CGU_FAULT", "0")
+    faulted = timed()
+    print(f"\nclean {1e3 * clean:.2f} ms, faulted {1e3 * faulted:.2f} ms (extra {1e3 * (faulted - clean):.2f} ms)")
+    assert faulted - clean < 0.1
