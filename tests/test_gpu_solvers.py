@@ -476,3 +476,43 @@ def test_cg_preferred_chunk(monkeypatch):
     assert chunk(krylov_amd.WeightedInner(np.full(R.shape[0], 2.0))) == 32
     monkeypatch.setenv("KRY_CG_PERSIST", "0")
     assert chunk() == 32
+
+
+@pytest.mark.parametrize("case", ["Mr", "block3", "householder"])
+def test_restarted_gmres_variants_match_oracle_chaining(case):
+    """gmres_restarted with a right preconditioner, with a 3-column block
+    (per-column tol = 1e-8 ||b_c|| / ||b_c - A x_c||) and with Householder
+    Arnoldi, against the same x0-chaining of the oracle (restart 15)."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+    from tests import solver_cases
+
+    q = solver_cases.inputs()
+    R = q["R"]
+    kw, okw = {}, {}
+    b = np.ones(R.shape[0])
+    if case == "Mr":
+        kw = okw = {"Mr": q["RMj"]}
+    elif case == "block3":
+        b = np.random.default_rng(21).standard_normal((R.shape[0], 3))
+    else:
+        kw = okw = {"ortho": "householder"}
+    x, infos = krylov_amd.gmres_restarted(R, b, restart=15, tol=1e-8, max_cycles=12, **kw)
+    # the oracle, chained the same way
+    xo = np.zeros_like(b)
+    bnorm = np.linalg.norm(b, axis=0)
+    hist, steps = [], []
+    for _ in range(12):
+        _, info = K.gmres(R, b, x0=xo, maxiter=15, tol=1e-8 * bnorm / np.maximum(np.linalg.norm(b - R @ xo, axis=0), 1e-300),
+                          **okw)
+        hist.extend(np.asarray(info.resnorms, dtype=np.float64))
+        steps.append(info.numsteps)
+        xo = info.xk
+        if info.success:
+            break
+    assert [i.numsteps for i in infos] == steps
+    got = np.concatenate([np.asarray(i.resnorms, dtype=np.float64) for i in infos])
+    ref = np.array(hist)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got[:-1], ref[:-1], rtol=1e-9)
+    np.testing.assert_allclose(x, xo, rtol=1e-8, atol=1e-10 * np.abs(xo).max())
