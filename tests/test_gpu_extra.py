@@ -91,3 +91,39 @@ def test_extra_solvers_chunking_is_invisible(solver):
     assert ref.numsteps == fast.numsteps
     got, want = np.asarray(fast.resnorms), np.asarray(ref.resnorms)
     np.testing.assert_allclose(got[:-1], want[:-1], rtol=1e-7, atol=1e-14 * want[0])
+
+
+def _ref_cases(solver):
+    """The real-valued cases of the reference's tests/test_<solver>.py
+    (tests/linear_problems.py restated in tests/gpu_helpers.py); hpd,
+    hermitian_indefinite and complex_unsymmetric are complex: outside the
+    MI355X path."""
+    from tests import gpu_helpers as H
+
+    if solver in ("bicgstab", "cgs"):
+        return [H.spd_dense((5,)), H.spd_sparse((5,)), H.spd_dense((5, 1)), H.spd_dense((5, 3)),
+                H.spd_rhs_0((5,)), H.spd_rhs_0sol0(), H.symmetric_indefinite(), H.real_unsymmetric()]
+    return [H.spd_dense((5,)), H.spd_sparse((5,)), H.spd_sparse((5, 1)), H.spd_sparse((5, 3)),
+            H.spd_rhs_0((5,)), H.spd_rhs_0sol0(), H.symmetric_indefinite()]
+
+
+@pytest.mark.parametrize("solver", ["bicgstab", "cgs", "cgr", "gcr"])
+def test_reference_solver_cases(solver):
+    """tests/test_bicgstab.py / test_cgs.py / test_cgr.py / test_gcr.py of
+    the reference, restated: tol 1e-7, maxiter 10, the callback called
+    numsteps + 1 times, success, and helpers.assert_consistent (the explicit
+    residual agrees with the last history entry)."""
+    import krylov_amd
+    from tests import gpu_helpers as H
+
+    for A, b in _ref_cases(solver):
+        count = 0
+
+        def callback(x, r):
+            nonlocal count
+            count += 1
+
+        sol, info = getattr(krylov_amd, solver)(A, b, tol=1.0e-7, maxiter=10, callback=callback)
+        assert count == info.numsteps + 1
+        assert info.success
+        H.assert_consistent(A, b, info, sol, 1.0e-7)
