@@ -579,6 +579,11 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
           wr[g][v] = wr[g][v] - t;  // Av -= alpha * V[j] (arnoldi.py:162)
           const double a = qp ? (double)cn[b][u][v] : (double)wr[g][v];
           acc[v] += dterm(a, (double)wr[g][v]);  // out-of-range elements are 0: they add 0
+          // keeps the accumulation in program order: otherwise, for float
+          // vectors, LLVM schedules the products of a whole chunk ahead of
+          // the float64 adds and holds them in registers (218-578 VGPRs
+          // spilled at NV = 24-40; 4-15 with this)
+          asm volatile("" : "+v"(acc[v]));
         }
       }
     }
