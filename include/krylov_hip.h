@@ -143,7 +143,7 @@ int kry_axpy(kry_ctx *ctx, const double *alpha, kry_vec *x, kry_vec *y);
  *   form 2: z = x + a[c] * (y - b[c] * w)  (bicgstab.py:109)
  *   form 3: z = x / a[c]   form 4: z = x - y   form 5: z = x + y
  *   form 6: z = x          form 7: z = a[c] * x
- * z may alias x, y or w. Replaces the AXPY-type lines of the host-driven
+ * z may alias x, y or w. Replaces the AXPY-type lines of the other
  * solvers (bicgstab.py, cgs.py, cgr.py, gcr.py; krylov_amd/extra.py). */
 int kry_vec_lincomb(kry_ctx *ctx, int form, kry_vec *z, kry_vec *x, kry_vec *y, kry_vec *w,
                     const double *a, const double *b);

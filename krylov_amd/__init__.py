@@ -1,6 +1,7 @@
 """krylov_amd — MI355X-native inner loop for the Krylov solvers of
 ``ju-liu/krylov`` (cg / gmres / minres with the reference call signatures;
-bicgstab / cgs / cgr / gcr as host-driven loops over the same device kernels).
+bicgstab / cgs / cgr / gcr with their scalars chained on the device, over the
+same kernels).
 
 The per-iteration work (CSR SpMV, AXPY/scale updates, inner products and
 norms, GMRES modified Gram-Schmidt + Givens, the MINRES Lanczos/QR

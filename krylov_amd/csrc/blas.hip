@@ -1,4 +1,4 @@
-// Device vector operations for the host-driven solver loops (bicgstab, cgs,
+// Device vector operations for the other solver loops (bicgstab, cgs,
 // cgr, gcr, ... of the reference; krylov_amd/extra.py). Each call is one
 // stream-ordered launch evaluating exactly the NumPy expression tree of the
 // reference line it replaces, with per-column scalars handed over by value.
@@ -61,7 +61,7 @@ struct OpLincomb {
 };
 
 // ---------------------------------------------- device-resident scalar chain
-// The host-driven solvers (bicgstab, cgs, cgr, gcr) keep their per-iteration
+// These solvers (bicgstab, cgs, cgr, gcr) keep their per-iteration
 // scalars in a device register file (kry_prog: nregs rows of k doubles), so
 // a whole chunk of iterations is enqueued without a host round trip: inner
 // products reduce into registers, scalar lines of the reference evaluate on

@@ -32,7 +32,7 @@ class _Dev:
 
     def __init__(self, prob):
         if prob.kpad > 64:
-            raise NotImplementedError("at most 64 right-hand-side columns on the host-driven solvers")
+            raise NotImplementedError("at most 64 right-hand-side columns on bicgstab / cgs / cgr / gcr")
         self.prob = prob
         self.ctx = prob.ctx
         self.w = prob.w_dev
