@@ -1174,6 +1174,87 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
   }
 }
 
+// One (column block, row group) segment of the column-blocked image: its
+// entries [s0, s0 + len) are multiplied against the x block in chunks of
+// kCbCap products staged in LDS, then thread r adds its row's products
+// [r0, r1) to acc in stored order. VEC: each thread loads 4 consecutive
+// entries (one 16-B column load, 16-B value loads) from the 4-entry-aligned
+// quads covering the segment (entries outside it are masked), against one
+// 4- or 8-B load per entry and array.
+template <bool VEC, typename V, typename MV, class BS>
+__device__ __forceinline__ void cb_segment(int64_t s0, int len, int r0, int r1, const int *__restrict__ col,
+                                           const MV *__restrict__ val, const BS &bs, V *prod, V &acc, int tid) {
+  constexpr int U = kCbCap / kBlock;
+  if constexpr (VEC) {
+    static_assert(U == 4, "one quad of entries per thread and chunk");
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    const int64_t q0 = s0 >> 2, qend = (s0 + len + 3) >> 2;
+    for (int64_t qc = q0; qc < qend; qc += kBlock) {
+      const int64_t base = qc * 4 - s0;  // segment-relative entry held by prod[0]
+      __syncthreads();                   // the previous chunk has been consumed
+      const int64_t q = qc + tid;
+      int j[4];
+      V a[4];
+      if (q < qend) {
+        const i4 c = __builtin_nontemporal_load(reinterpret_cast<const i4 *>(col) + q);
+        MV m[4];
+        if constexpr (sizeof(MV) == 8) {
+          typedef double d2 __attribute__((ext_vector_type(2)));
+          const d2 v0 = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q);
+          const d2 v1 = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q + 1);
+          m[0] = v0.x; m[1] = v0.y; m[2] = v1.x; m[3] = v1.y;
+        } else {
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(val) + q);
+          m[0] = v.x; m[1] = v.y; m[2] = v.z; m[3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t e = base + 4 * (int64_t)tid + i;
+          const bool in = e >= 0 && e < len;
+          j[i] = in ? c[i] : -1;
+          a[i] = (V)m[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { j[i] = -1; a[i] = V(0); }
+      }
+      V xj[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xj[i] = j[i] >= 0 ? bs(j[i], 0) : V(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (j[i] >= 0) prod[4 * tid + i] = a[i] * xj[i];
+      __syncthreads();
+      const int64_t lo = r0 > base ? r0 : base, hi = r1 < base + kCbCap ? r1 : base + kCbCap;
+      for (int64_t e = lo; e < hi; ++e) acc = acc + prod[e - base];
+    }
+  } else {
+    for (int c0 = 0; c0 < len; c0 += kCbCap) {
+      const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
+      __syncthreads();  // the previous chunk has been consumed
+      // U entries per thread, all loads issued before the gathers
+      int j[U];
+      V a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = c0 + tid + u * kBlock;
+        j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
+        a[u] = e < c1 ? (V)__builtin_nontemporal_load(val + s0 + e) : V(0);
+      }
+      V xj[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xj[u] = j[u] >= 0 ? bs(j[u], 0) : V(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j[u] >= 0) prod[tid + u * kBlock] = a[u] * xj[u];
+      __syncthreads();
+      const int lo = r0 > c0 ? r0 : c0, hi = r1 < c1 ? r1 : c1;
+      for (int e = lo; e < hi; ++e) acc = acc + prod[e - c0];
+    }
+  }
+}
+
 // ------------------------------------------- column-blocked SpMV (k = 1)
 // Pass b of cb_nb: each block takes 256-row groups; the group's entries with
 // columns in block b (stored in row order) are multiplied against the
@@ -1182,7 +1263,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
 // sequence of roundings as csr_matvec: sum from 0, product rounded, then
 // added). The running sums live in cb_y between passes; the last pass applies
 // the epilogue.
-template <typename V, typename MV, class Src, class Epi>
+template <bool VEC, typename V, typename MV, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t n, int64_t ng,
                                                          const int64_t *__restrict__ gptr,
                                                          const uint16_t *__restrict__ roff,
@@ -1207,29 +1288,7 @@ __global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t 
       r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
     }
     V acc = (b == 0 || !has) ? V(0) : (V)ysum[row];
-    for (int c0 = 0; c0 < len; c0 += kCbCap) {
-      const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
-      __syncthreads();  // the previous chunk has been consumed
-      // kCbCap / kBlock entries per thread, all loads issued before the gathers
-      constexpr int U = kCbCap / kBlock;
-      int j[U];
-      V a[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = c0 + tid + u * kBlock;
-        j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
-        a[u] = e < c1 ? (V)__builtin_nontemporal_load(val + s0 + e) : V(0);
-      }
-      V xj[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) xj[u] = j[u] >= 0 ? bs(j[u], 0) : V(0);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (j[u] >= 0) prod[tid + u * kBlock] = a[u] * xj[u];
-      __syncthreads();
-      const int lo = r0 > c0 ? r0 : c0, hi = r1 < c1 ? r1 : c1;
-      for (int e = lo; e < hi; ++e) acc = acc + prod[e - c0];
-    }
+    cb_segment<VEC, V, MV>(s0, len, r0, r1, col, val, bs, prod, acc, tid);
     if (has) {
       if (!last) ysum[row] = (double)acc;
       else dacc += epi(row, 0, acc, bs(row, 0));
@@ -1252,7 +1311,7 @@ __global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t 
 // the current x block L2-resident. Same per-row summation order => bitwise.
 constexpr int kCbMaxOwn = 16;
 constexpr int kCbPersistGrid = 1024;  // 4 blocks per CU: all resident, so they start together
-template <typename V, typename MV, class Src, class Epi>
+template <bool VEC, typename V, typename MV, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int64_t ng,
                                                           const int64_t *__restrict__ gptr,
                                                           const uint16_t *__restrict__ roff,
@@ -1281,28 +1340,7 @@ __global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int
         r0 = roff[(int64_t)b * n + row];
         r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
       }
-      for (int c0 = 0; c0 < len; c0 += kCbCap) {
-        const int c1 = len < c0 + kCbCap ? len : c0 + kCbCap;
-        __syncthreads();
-        constexpr int U = kCbCap / kBlock;
-        int j[U];
-        V a[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = c0 + tid + u * kBlock;
-          j[u] = e < c1 ? __builtin_nontemporal_load(col + s0 + e) : -1;
-          a[u] = e < c1 ? (V)__builtin_nontemporal_load(val + s0 + e) : V(0);
-        }
-        V xj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xj[u] = j[u] >= 0 ? bs(j[u], 0) : V(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (j[u] >= 0) prod[tid + u * kBlock] = a[u] * xj[u];
-        __syncthreads();
-        const int lo = r0 > c0 ? r0 : c0, hi = r1 < c1 ? r1 : c1;
-        for (int e = lo; e < hi; ++e) acc[o] = acc[o] + prod[e - c0];
-      }
+      cb_segment<VEC, V, MV>(s0, len, r0, r1, col, val, bs, prod, acc[o], tid);
     }
   }
   double dacc = 0.0;
@@ -1352,12 +1390,31 @@ int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const C
 
 // KRY_SPMV_DIA_BLK=0: block right-hand sides on the lane-group SELL kernel
 // instead of the diagonal-offset image (A/B and tests)
+// 16-B quad loads in the column-blocked kernels (KRY_CB_VEC=0: one load per
+// entry and array, the round-2 form; A/B switch)
+inline bool cb_vec() {
+  static const bool on = [] {
+    const char *e = getenv("KRY_CB_VEC");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 inline bool dia_blk_off() {
   static const bool off = [] {
     const char *e = getenv("KRY_SPMV_DIA_BLK");
     return e && atoi(e) == 0;
   }();
   return off;
+}
+
+// launch_spmv takes the column-blocked kernels for this operator and k: its
+// SpMV is bound by the random x gathers, so a source that computes on every
+// gathered value (SrcScaled's division) costs more than a pass forming the
+// vector first.
+template <typename I>
+inline bool spmv_column_blocked(const kry_csr *A, int k) {
+  return sizeof(I) == 4 && k == 1 && !A->dia && A->cb_nb > 0;
 }
 
 // y-side epilogue Epi / x-side source Src composition of one SpMV launch;
@@ -1415,10 +1472,14 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
     }
     if (k == 1 && A->cb_nb > 0 && A->cb_ng <= (int64_t)kCbPersistGrid * kCbMaxOwn) {
       grid = (int)std::min<int64_t>(A->cb_ng, kCbPersistGrid);
-      hipLaunchKernelGGL((spmv_cbp_kernel<V, MV, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n,
-                         A->cb_ng, static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
-                         static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val), src, epi, part, ctrl,
-                         step);
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n, A->cb_ng,
+                           static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
+                           static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val), src, epi, part,
+                           ctrl, step);
+      };
+      if (cb_vec()) go(spmv_cbp_kernel<true, V, MV, Src, Epi>);
+      else go(spmv_cbp_kernel<false, V, MV, Src, Epi>);
       KRY_HIP(hipGetLastError());
       if (grid_out) *grid_out = grid;
       return;
@@ -1429,12 +1490,15 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
         return e ? std::max(1, std::min(atoi(e), kMaxGrid)) : kMaxGrid;
       }();
       grid = (int)std::min<int64_t>(A->cb_ng, cb_grid);
-      for (int b = 0; b < (int)A->cb_nb; ++b)
-        hipLaunchKernelGGL((spmv_cb_kernel<V, MV, Src, Epi>), dim3(grid), dim3(kBlock), 0, st, b, (int)A->cb_nb,
-                           A->n, A->cb_ng, static_cast<const int64_t *>(A->cb_gptr),
-                           static_cast<const uint16_t *>(A->cb_roff), static_cast<const int *>(A->cb_col),
-                           static_cast<const MV *>(A->cb_val), static_cast<double *>(A->cb_y), src, epi, part,
-                           ctrl, step);
+      auto go = [&](auto kern) {
+        for (int b = 0; b < (int)A->cb_nb; ++b)
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, b, (int)A->cb_nb, A->n, A->cb_ng,
+                             static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
+                             static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val),
+                             static_cast<double *>(A->cb_y), src, epi, part, ctrl, step);
+      };
+      if (cb_vec()) go(spmv_cb_kernel<true, V, MV, Src, Epi>);
+      else go(spmv_cb_kernel<false, V, MV, Src, Epi>);
       KRY_HIP(hipGetLastError());
       if (grid_out) *grid_out = grid;
       return;

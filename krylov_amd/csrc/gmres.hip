@@ -1468,10 +1468,13 @@ void gm_run_impl(kry_gmres *s, int max_steps) {
       // the QR kernel reads the persistent kernel's <w, w> partials
       gm_qr_step<V>(s, s->mgsp_out, s->mgsp_grid, col, step);
       if (s->mgsp_norm) continue;  // V_{col+1} is in the basis already
-      if (col + 1 < s->maxiter) {
+      if (col + 1 < s->maxiter && !spmv_column_blocked<I>(s->A, k)) {
         s->vpending = true;  // V_{col+1} is formed by the next step's SpMV
         continue;
       }
+      // last column, or a gather-bound SpMV (cfg3: the division on every
+      // gathered value cost 269 -> 285 us with the quad-loading kernel, the
+      // separate pass ~6 us): V_{col+1} = w / hsafe as its own pass
       launch_elementwise<V>(N, k, OpScaleDiv<V>{w, basis<V>(s->V, s->vstride, col + 1), s->scal + G_HSAFE * k, k},
                             nullptr, s->ctrl, step, st);
       continue;
