@@ -1388,8 +1388,6 @@ int launch_sell(const kry_csr *A, int k, Src src, Epi epi, double *part, const C
   return launch_sell_img<V, MV, I, KT, UNR, false>(A, k, src, epi, part, ctrl, step, st);
 }
 
-// KRY_SPMV_DIA_BLK=0: block right-hand sides on the lane-group SELL kernel
-// instead of the diagonal-offset image (A/B and tests)
 // 16-B quad loads in the column-blocked kernels (KRY_CB_VEC=0: one load per
 // entry and array, the round-2 form; A/B switch)
 inline bool cb_vec() {
@@ -1400,6 +1398,8 @@ inline bool cb_vec() {
   return on;
 }
 
+// KRY_SPMV_DIA_BLK=0: block right-hand sides on the lane-group SELL kernel
+// instead of the diagonal-offset image (A/B and tests)
 inline bool dia_blk_off() {
   static const bool off = [] {
     const char *e = getenv("KRY_SPMV_DIA_BLK");
