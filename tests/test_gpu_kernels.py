@@ -109,6 +109,36 @@ def test_compact_boundary_spread(monkeypatch):
         np.testing.assert_array_equal(op @ x, A @ x)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sell64_k1_regular_compact_bitwise(monkeypatch, dtype):
+    """SELL-64 at k = 1 on a compact image of regular slices (no DIA image):
+    rows of 0-16 banded entries, an empty slice, a 16-wide slice, a partial
+    last slice; bitwise SciPy csr_matvec. (The solvers on this path:
+    tests/test_gpu_dia.py with KRY_SPMV_DIA=0.)"""
+    import krylov_amd
+
+    monkeypatch.setenv("KRY_SPMV_DIA", "0")
+    rng = np.random.default_rng(7)
+    n = 64 * 37 + 5
+    lens = rng.integers(0, 17, n)
+    lens[64:128] = 0  # an empty slice
+    lens[128:192] = 16  # a full-width slice
+    rows, cols = [], []
+    for i in range(n):
+        c = np.unique(rng.integers(max(0, i - 400), min(n, i + 400), lens[i]))
+        rows.append(np.full(c.shape[0], i))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    vals = rng.standard_normal(rows.shape[0]).astype(dtype)
+    A = scipy.sparse.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sort_indices()
+    op = krylov_amd.CsrOperator(A)
+    lay = op.layout()
+    assert lay["compact"] and not lay["dia"] and lay["irregular"] == 0 and lay["col_blocks"] == 0
+    x = rng.standard_normal(n).astype(dtype)
+    np.testing.assert_array_equal(np.asarray(op @ x).view(np.uint8), (A @ x).view(np.uint8))
+
+
 def _scattered_csr(n, lens, seed, sort=True, dtype=np.float64):
     """CSR with lens[i] uniform random columns in row i (scattered sparsity)."""
     rng = np.random.default_rng(seed)
