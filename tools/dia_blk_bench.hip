@@ -304,6 +304,136 @@ __global__ __launch_bounds__(256) void dia_split(const int64_t *__restrict__ spt
   if (tid < K) part[(int64_t)g * K + tid] = red[tid];
 }
 
+// Shifted windows (round 3): one slice per wave, CPL 2 (lane = row rl0 of
+// each 16-row group, columns c0, c0 + 1). A slot column whose offset is the
+// previous one's + 1 reads the previous window one row further on: lane l
+// takes lane l + 4's value of the same group register, lanes 60..63 take
+// lanes 0..3 of the next group (the same rotation of register r + 1), and
+// the last group's last row is one extra 16-B load. The 5-point stencil's
+// -1 / 0 / +1 slots then cost one window of loads instead of three, and the
+// offset-0 window is kept for the epilogue's p (no reload). Every window
+// position is loaded at its clamped row whether or not its mask bit is set,
+// so a derived position is always the true x row (a row out of range is a
+// hole in every slot). MODE bits: 1 values loaded once per slot (16 B per
+// lane) and handed to the row groups by lane shuffles; 2 nontemporal value
+// loads; 4 never derive (full window loads, clamped; epilogue p captured).
+template <int MODE>
+__global__ __launch_bounds__(256) void dia_shift(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                 const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                 const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                 const double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ part) {
+  constexpr int CPL = 2, LPR = K / CPL, RPG = 64 / LPR, NG = kDiaSlice / RPG;
+  constexpr bool SHUF = (MODE & 1) != 0, NTV = (MODE & 2) != 0, NODER = (MODE & 4) != 0;
+  __shared__ double red[256 * CPL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
+  const int src4 = (lane + 4) & 63;
+  const bool tail = lane >= 64 - LPR;  // row rl0 = RPG - 1: its +1 neighbour is the next group's row 0
+  const int64_t W = (int64_t)gridDim.x * 4;
+  double dacc[CPL] = {0.0, 0.0};
+  auto ldrow = [&](int64_t row, double (&o)[CPL]) {
+    row = row < 0 ? 0 : (row >= n ? n - 1 : row);
+    ldx<CPL>(x + row * K + c0, o);
+  };
+  for (int64_t s = (int64_t)g * 4 + wid; s < nslices; s += W) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s], cb = base / kDiaSlice;
+    const int64_t row0 = s * kDiaSlice + rl0;
+    double acc[NG][CPL], xw[NG][CPL], xi[NG][CPL];
+#pragma unroll
+    for (int r = 0; r < NG; ++r)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[r][c] = 0.0;
+    bool have_i = false;
+    int prev = 0;
+    for (int j = 0; j < w; ++j) {
+      const int off = doff[cb + j];
+      const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+      double a[NG];
+      d2v vv;
+      if (SHUF) {
+        const d2v *vp = reinterpret_cast<const d2v *>(val + base + (int64_t)j * kDiaSlice) + lane;
+        vv = NTV ? __builtin_nontemporal_load(vp) : *vp;
+      } else {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) {
+          const double *vp = val + base + (int64_t)j * kDiaSlice + r * RPG + rl0;
+          a[r] = NTV ? __builtin_nontemporal_load(vp) : *vp;
+        }
+      }
+      if (!NODER && j > 0 && off == prev + 1) {
+        double e[CPL];
+        ldrow(s * kDiaSlice + kDiaSlice + prev, e);  // row 128 of the previous window
+        double R[NG][CPL];
+#pragma unroll
+        for (int r = 0; r < NG; ++r)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) R[r][c] = __shfl(xw[r][c], src4);
+#pragma unroll
+        for (int r = 0; r < NG; ++r)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) xw[r][c] = tail ? (r + 1 < NG ? R[r + 1 < NG ? r + 1 : r][c] : e[c]) : R[r][c];
+      } else {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) ldrow(row0 + r * RPG + off, xw[r]);
+      }
+      prev = off;
+      if (SHUF) {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) {
+          const int rl = r * RPG + rl0;
+          const double lo = __shfl(vv.x, rl >> 1), hi = __shfl(vv.y, rl >> 1);
+          a[r] = (rl & 1) ? hi : lo;
+        }
+      }
+      if (off == 0) {
+        have_i = true;
+#pragma unroll
+        for (int r = 0; r < NG; ++r)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) xi[r][c] = xw[r][c];
+      }
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        const bool on = ((((rl & 1) ? m1 : m0) >> (rl >> 1)) & 1u) != 0;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const double p = a[r] * xw[r][c];
+          const double t = acc[r][c] + p;
+          acc[r][c] = on ? t : acc[r][c];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NG; ++r) {
+      const int64_t row = row0 + r * RPG;
+      if (row < n) {
+        double q[CPL];
+        if (have_i) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) q[c] = xi[r][c];
+        } else {
+          ldx<CPL>(x + row * K + c0, q);
+        }
+        d2v v;
+        v.x = acc[r][0];
+        v.y = acc[r][1];
+        __builtin_nontemporal_store(v, reinterpret_cast<d2v *>(y + row * K + c0));
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) dacc[c] += dterm(q[c], acc[r][c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];
+  block_tree_reduce(red, 256 * CPL, K);
+  if (tid < K) part[(int64_t)g * K + tid] = red[tid];
+}
+
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 3163;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -394,6 +524,28 @@ int main(int argc, char **argv) {
     });                                                                                                           \
     if (CHECK) check(nm);                                                                                         \
   }
+  if (getenv("DIA_BLK_SHIFT")) {  // shifted-window variants against the slot-major kernel
+    const int full = (int)((A->dia_nslices + 3) / 4);
+    if (full > 65536) return 1;
+#define SH(MODE, NAME)                                                                                              \
+  {                                                                                                                 \
+    timeit(NAME, [&] {                                                                                              \
+      hipLaunchKernelGGL((dia_shift<MODE>), dim3(full), dim3(256), 0, st, (const int64_t *)A->dia_sptr,             \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,        \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);               \
+    });                                                                                                             \
+    check(NAME);                                                                                                    \
+  }
+    for (int rep = 0; rep < 2; ++rep) {
+      gr = full;
+      SM(2, 0, "slot-major CPL 2, 1 slice/wave", true);
+      SH(4, "shift: no derive (clamped windows, p captured)");
+      SH(0, "shift: -1/0/+1 derived");
+      SH(2, "shift: derived, nt values");
+      SH(1, "shift: derived, shuffled values");
+      SH(3, "shift: derived, shuffled nt values");
+    }
+  } else
   if (getenv("DIA_BLK_SPLIT")) {
 #define SPL(GPW, SPR)                                                                                              \
   {                                                                                                                \
