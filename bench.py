@@ -167,6 +167,16 @@ def spmv_kernel_desc(layout, n):
                 ds * 8 + ds / 128 * 20 + 2 * n * 8,
                 "dia_slots*8 (values) + dia_slots/128*20 (offset + two lane masks per slot column) + 2*n*8 "
                 "(p read once, Ap written once); no index stream")
+    if layout.get("pair"):
+        ps = layout["pair_slots"]
+        pslices = (n + 127) // 128
+        return ("spmv_pair_kernel<double,double,8,SrcPlain,EpiApDot> (paired-row SELL-128 SpMV for general CSR: "
+                "two rows per lane, one 16-B value load, one 4-B load of two uint16 column deltas over a "
+                "per-slot-column int32 base and one 16-B x load for adjacent columns per slot column; Ap stored + "
+                "<p,Ap> partials)",
+                ps * (8 + 2) + ps / 128 * 4 + pslices * 12 + 2 * n * 8,
+                "pair_slots*(8+2) (values + uint16 deltas) + pair_slots/128*4 (column bases) + slices*12 (slice "
+                "pointer + width) + 2*n*8 (p read once, Ap written once)")
     if layout["compact"]:
         return ("spmv_sell_kernel<double,double,int,1,16,true,SrcPlain,EpiApDot> (SELL-64 SpMV, compact index "
                 "image: uint16 column deltas over per-slot-column int32 bases; Ap stored + <p,Ap> partials)",
@@ -358,7 +368,8 @@ def pmc_traffic(n, nnz, kernel):
         return {}
     if d.get("n") != n or d.get("nnz") != nnz:
         return {}
-    key = "dia" if kernel.startswith("spmv_dia_kernel") else "sell"
+    key = ("dia" if kernel.startswith("spmv_dia_kernel") else
+           "pair" if kernel.startswith("spmv_pair_kernel") else "sell")
     k = d.get("kernels", {}).get(key)
     if not k:
         return {}
@@ -411,8 +422,9 @@ def cfg4_rhs(n, rank, k=8):
 
 def run_spmv_general(A_host, steps):
     """The same CG SpMV measurement with the DIA image disabled
-    (KRY_SPMV_DIA=0 at upload): the compact SELL-64 kernel every sorted
-    int32 CSR matrix takes when it is not diagonal-structured."""
+    (KRY_SPMV_DIA=0 at upload): the kernel a general CSR matrix takes when it
+    is not diagonal-structured (the paired-row SELL-128 image since round 3;
+    KRY_SPMV_PAIR=0: the compact SELL-64 kernel)."""
     prev = os.environ.get("KRY_SPMV_DIA")
     os.environ["KRY_SPMV_DIA"] = "0"
     try:
@@ -424,7 +436,7 @@ def run_spmv_general(A_host, steps):
             os.environ["KRY_SPMV_DIA"] = prev
     assert not res["layout"]["dia"]
     n, nnz = A_host.shape[0], int(A_host.nnz)
-    roof = roofline_of(res, n, nnz, pmc_traffic(n, nnz, "spmv_sell_kernel"))
+    roof = roofline_of(res, n, nnz, pmc_traffic(n, nnz, spmv_kernel_desc(res["layout"], n)[0]))
     roof["cg_it_per_s"] = steps / res["elapsed"]
     return roof
 

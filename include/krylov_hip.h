@@ -104,7 +104,7 @@ int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
 int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
                  int32_t *widths, int32_t *offsets, uint64_t *masks);
 /* The device image kry_csr_create built, size-checked: writes the first
- * min(len, KRY_CSR_INFO_LEN) of info[0..6] = slices, slots, irregular slices,
+ * min(len, KRY_CSR_INFO_LEN) of info[0..8] = slices, slots, irregular slices,
  * compact (1 when the column indices are stored as uint16 deltas over
  * per-slot-column int32 bases: every slot column spans <= 65534 columns,
  * int32 indices and KRY_SELL_COMPACT != 0 in the environment), the number of
@@ -112,10 +112,14 @@ int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices
  * scattered sparsity (0 = none; KRY_SPMV_CB=0 disables), dia (1 when the
  * diagonal-offset image serves single-RHS SpMVs: int32 indices, every row
  * strictly sorted, the rows of each 64-row slice sharing a short list of
- * column offsets; KRY_SPMV_DIA=0 disables) and that image's slot count.
- * Fields added later go at the end, so a caller built against this header
- * keeps working (kry_version() >= 101). */
-#define KRY_CSR_INFO_LEN 7
+ * column offsets; KRY_SPMV_DIA=0 disables) and that image's slot count,
+ * then (kry_version() >= 102) pair (1 when the paired-row SELL-128 image
+ * serves single-RHS SpMVs of a general matrix: no diagonal-offset or
+ * column-blocked image, n < 2^31, every 128-row slot column spans <= 65534
+ * columns, at most 1.25x the SELL-64 slots; KRY_SPMV_PAIR=0 disables) and
+ * that image's slot count. Fields added later go at the end, so a caller
+ * built against this header keeps working (kry_version() >= 101). */
+#define KRY_CSR_INFO_LEN 9
 int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len);
 /* The version-100 form: info[0..4] only (`info` holds 5 values). */
 int kry_csr_info(const kry_csr *A, int64_t *info);

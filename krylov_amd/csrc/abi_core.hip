@@ -363,8 +363,8 @@ __global__ void lartg_kernel(int64_t count, const T *f, const T *g, T *c, T *s, 
 extern "C" {
 
 // 101: kry_csr_info_n (size-checked image info); kry_csr_info back to its
-// version-100 five values
-int kry_version(void) { return 101; }
+// version-100 five values. 102: kry_csr_info_n reports the paired-row image
+int kry_version(void) { return 102; }
 
 const char *kry_last_error(void) { return kry::g_last_error.c_str(); }
 
@@ -440,7 +440,8 @@ int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len) {
   KRY_API_BEGIN
   KRY_REQUIRE(A && (info || len == 0) && len >= 0, KRY_EINVAL, "bad argument");
   const int64_t all[KRY_CSR_INFO_LEN] = {A->nslices, A->nslots, A->nirregular, A->compact ? 1 : 0,
-                                         A->cb_nb,     A->dia ? 1 : 0, A->dia_nslots};
+                                         A->cb_nb,     A->dia ? 1 : 0, A->dia_nslots, A->sp ? 1 : 0,
+                                         A->sp_nslots};
   for (int i = 0; i < len && i < KRY_CSR_INFO_LEN; ++i) info[i] = all[i];
   KRY_API_END
 }
@@ -721,6 +722,77 @@ static bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<M
   return true;
 }
 
+// Paired-row SELL-128 image (see kry_csr::sp_*). Pass 1: slice widths (the
+// longest row of each 128 rows); pass 2: per slot column the smallest column
+// as base and every entry's delta and value at row position r - 128 s.
+// Returns false (nothing built) when a slot column spans more than 65534
+// columns, a column does not fit int32, or the image would hold more than
+// 1.25x the SELL-64 image's slots (very uneven rows).
+template <typename MV>
+struct PairHost {
+  std::vector<int64_t> sptr;
+  std::vector<int32_t> width;
+  std::vector<int32_t> cbase;
+  std::vector<uint16_t> delta;
+  std::vector<MV> val;
+  int max_width = 0;
+};
+
+template <typename I, typename MV>
+static bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, PairHost<MV> &p) {
+  constexpr int H = kPairSlice;
+  if (n == 0 || n >= (int64_t(1) << 31)) return false;
+  const int64_t ns = (n + H - 1) / H;
+  p.width.assign(ns, 0);
+  p.sptr.assign(ns + 1, 0);
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t r = s * H; r < std::min<int64_t>(n, (s + 1) * H); ++r) w = std::max<int64_t>(w, ip[r + 1] - ip[r]);
+    if (w > INT32_MAX / H) return false;
+    p.width[s] = (int32_t)w;
+    p.max_width = std::max(p.max_width, (int)w);
+    p.sptr[s + 1] = p.sptr[s] + H * w;
+  }
+  const int64_t slots = p.sptr[ns];
+  if (slots == 0 || slots * 4 > sell_slots * 5 + (int64_t)4 * H * p.max_width) return false;
+  p.cbase.assign(slots / H + kDiaPad, 0);
+  p.delta.assign(slots + 2 * H, 0xFFFF);
+  p.val.assign(slots + 2 * H, MV(0));
+  std::atomic<bool> ok{true};
+  auto fill = [&](int64_t sa, int64_t sb) {
+    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
+      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H), base = p.sptr[s];
+      for (int64_t j = 0; j < p.width[s]; ++j) {
+        int64_t mn = INT64_MAX, mx = -1;
+        for (int64_t r = r0; r < r1; ++r)
+          if ((int64_t)ip[r] + j < (int64_t)ip[r + 1]) {
+            const int64_t c = (int64_t)ix[ip[r] + j];
+            mn = std::min(mn, c);
+            mx = std::max(mx, c);
+          }
+        if (mx < 0) mn = 0;
+        if (mx - mn > 65534 || mn > INT32_MAX) {
+          ok = false;
+          return;
+        }
+        p.cbase[base / H + j] = (int32_t)mn;
+        for (int64_t r = r0; r < r1; ++r)
+          if ((int64_t)ip[r] + j < (int64_t)ip[r + 1]) {
+            const int64_t q = base + j * H + (r - r0);
+            p.delta[q] = (uint16_t)((int64_t)ix[ip[r] + j] - mn);
+            p.val[q] = dv[ip[r] + j];
+          }
+      }
+    }
+  };
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 2048) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(fill, ns * t / nt, ns * (t + 1) / nt);
+  for (auto &x : th) x.join();
+  return ok.load();
+}
+
 namespace {
 template <typename I, typename MV>
 void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
@@ -800,6 +872,28 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipStreamSynchronize(st));
     }
   }
+  // paired-row SELL-128 image for general single-RHS SpMVs (KRY_SPMV_PAIR=0 disables)
+  const char *penv = getenv("KRY_SPMV_PAIR");
+  if (!A->dia && A->cb_nb == 0 && !(penv && atoi(penv) == 0)) {
+    PairHost<MV> ph;
+    if (pair_build(n, ip, ix, dv, A->nslots, ph)) {
+      A->sp = true;
+      A->sp_nslices = (int64_t)ph.width.size();
+      A->sp_nslots = ph.sptr.back();
+      A->sp_max_width = ph.max_width;
+      A->sp_sptr = dev_alloc(ph.sptr.size() * 8);
+      A->sp_width = dev_alloc(ph.width.size() * 4 + 4);
+      A->sp_cbase = dev_alloc(ph.cbase.size() * 4);
+      A->sp_delta = dev_alloc(ph.delta.size() * 2);
+      A->sp_val = dev_alloc(ph.val.size() * sizeof(MV));
+      KRY_HIP(hipMemcpyAsync(A->sp_sptr, ph.sptr.data(), ph.sptr.size() * 8, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->sp_width, ph.width.data(), ph.width.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->sp_cbase, ph.cbase.data(), ph.cbase.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->sp_delta, ph.delta.data(), ph.delta.size() * 2, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->sp_val, ph.val.data(), ph.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipStreamSynchronize(st));
+    }
+  }
   if (A->nirregular > 0) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
     A->indices = dev_alloc((nnz + 1) * sizeof(I));
@@ -817,7 +911,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 static void csr_free(kry_csr *A) {
   void *bufs[] = {A->sptr,   A->swidth,   A->sidx,     A->sval,     A->indptr,    A->indices,
                   A->data,   A->sdelta,   A->scbase,   A->cb_gptr,  A->cb_roff,   A->cb_col,
-                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val};
+                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val,
+                  A->sp_sptr, A->sp_width, A->sp_cbase, A->sp_delta, A->sp_val};
   for (void *b : bufs) dev_free(b);
 }
 

@@ -26,6 +26,8 @@ constexpr int kSlice = 64;           // SELL slice height = one wavefront
 // of the wave owns rows 2l and 2l + 1 of its slice
 constexpr int kDiaSlice = 128;
 constexpr int kDiaPad = 32;  // slot-column descriptors past the last one (unconditional reads of a round)
+// paired-row SELL-128 image (kry_csr::sp_*): lane l owns rows 2l, 2l + 1
+constexpr int kPairSlice = 128;
 constexpr int kCbRows = 256;         // rows per column-blocked segment (one per thread)
 constexpr int kCbCap = 1024;         // products staged in LDS per chunk
 constexpr int kNumXcd = 8;

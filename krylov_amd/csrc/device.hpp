@@ -813,6 +813,113 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
   }
 }
 
+// ------------------------------------ paired-row SELL-128 SpMV (k = 1)
+// The general-CSR image for one right-hand side (kry_csr::sp_*): slices of
+// 128 rows, slot column j of a slice holds the j-th stored entry of every row
+// (padding: delta 0xFFFF, value 0), rows interleaved so that lane l of the
+// wave owns rows 2l and 2l + 1. Per slot column a lane makes one 16-B value
+// load, one 4-B load of its two uint16 column deltas over the slot column's
+// int32 base (wave-uniform: scalar load) and one 16-B x load at its first
+// column: when the second row's column is the next one (banded and stencil
+// rows, where the slice's rows share their offsets) that load serves both;
+// otherwise the second value is an 8-B load behind one wave-level branch per
+// round, skipped by waves whose lanes all paired. Against SELL-64 that is
+// half the memory instructions per nonzero with the same 10 bytes
+// (tools/sellp_bench: 0.297 against 0.352 ms on the metric matrix). Each row
+// is summed from 0 in stored order, a hole or padding slot dropped by a
+// select, never added: bitwise csr_matvec, for unsorted rows, duplicates
+// and explicit zeros too. One slice per wave (grid over the slices).
+template <typename V, typename MV, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_pair_kernel(const int64_t *__restrict__ sptr,
+                                                           const int *__restrict__ swidth,
+                                                           const int *__restrict__ cbase,
+                                                           const uint32_t *__restrict__ dpair,
+                                                           const MV *__restrict__ val, int64_t nslices, int64_t n,
+                                                           Src src, Epi epi, double *__restrict__ part,
+                                                           const Ctrl *ctrl, int step) {
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const auto bs = src.template bind<1>(0);
+  double dacc = 0.0;
+  for (int64_t s = (int64_t)g * 4 + wid; s < nslices; s += W) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * kPairSlice + 2 * lane;
+    const int *cb = cbase + base / kPairSlice;  // wave-uniform: scalar loads (padded by kDiaPad)
+    const uint32_t *cd = dpair + base / 2 + lane;
+    const MV *cv = val + base + 2 * lane;
+    V acc0 = V(0), acc1 = V(0);
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      int b[UNR];
+      uint32_t d[UNR];
+      MV a[UNR][2];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        b[u] = cb[j0 + u];
+        if (j0 + u < w) {
+          d[u] = __builtin_nontemporal_load(cd + (int64_t)(j0 + u) * (kPairSlice / 2));
+          pload_nt<MV>(cv + (int64_t)(j0 + u) * kPairSlice, a[u]);
+        } else {
+          d[u] = 0xFFFFFFFFu;
+          a[u][0] = MV(0);
+          a[u][1] = MV(0);
+        }
+      }
+      V x0[UNR], x1[UNR];
+      bool v0[UNR], v1[UNR], need[UNR];
+      int64_t c1[UNR];
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t lo = d[u] & 0xFFFFu, hi = d[u] >> 16;
+        v0[u] = lo != 0xFFFFu;
+        v1[u] = hi != 0xFFFFu;
+        const int64_t c0 = (int64_t)b[u] + lo;
+        c1[u] = (int64_t)b[u] + hi;
+        const bool pr = v0[u] && v1[u] && c1[u] == c0 + 1;
+        V xp[2];
+        bs.pair(v0[u] ? c0 : (v1[u] ? c1[u] : 0), xp);  // at worst x[n]: inside the allocation slack
+        x0[u] = xp[0];
+        x1[u] = pr ? xp[1] : xp[0];
+        need[u] = v0[u] && v1[u] && !pr;
+        any = any || need[u];
+      }
+      if (__any(any)) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (need[u]) x1[u] = bs(c1[u], 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const V p0 = (V)a[u][0] * x0[u];
+        const V p1 = (V)a[u][1] * x1[u];
+        const V t0 = acc0 + p0;
+        const V t1 = acc1 + p1;
+        acc0 = v0[u] ? t0 : acc0;
+        acc1 = v1[u] ? t1 : acc1;
+      }
+    }
+    if (row + 1 < n) {
+      V xi[2];
+      bs.pair(row, xi);
+      const V o[2] = {acc0, acc1};
+      dacc += epi.rows2(row, o, xi);
+    } else if (row < n) {
+      dacc += epi(row, 0, acc0, bs(row, 0));
+    }
+  }
+  if (part != nullptr) {
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[g] = red[0];
+  }
+}
+
 // ------------------------------ diagonal-offset SpMV, block RHS (k = 2..8)
 // The same SELL-128/DIA image for k right-hand sides stored row-major
 // (n x k): for a slot column of offset o the x rows of the slice's rows are
@@ -1424,6 +1531,19 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                  int step, hipStream_t st) {
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
+  if (k == 1 && A->sp) {
+    // one slice per wave (tools/sellp_bench: 0.32 ms against 0.36 ms at 8192
+    // blocks of 2.4 slices per wave on the metric matrix); partial buffers
+    // hold kMaxGridBlk rows for k = 1
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGridBlk, (A->sp_nslices + 3) / 4));
+    hipLaunchKernelGGL((spmv_pair_kernel<V, MV, 8, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
+                       static_cast<const int64_t *>(A->sp_sptr), static_cast<const int *>(A->sp_width),
+                       static_cast<const int *>(A->sp_cbase), static_cast<const uint32_t *>(A->sp_delta),
+                       static_cast<const MV *>(A->sp_val), A->sp_nslices, A->n, src, epi, part, ctrl, step);
+    KRY_HIP(hipGetLastError());
+    if (grid_out) *grid_out = grid;
+    return;
+  }
   if constexpr (sizeof(I) == 4) {
     if (k == 1 && A->dia) {
       // Wide images (more than 8 slot columns, the metric's 15): one slice

@@ -79,6 +79,21 @@ struct kry_csr {
   void *dia_off = nullptr;    // int32, dia_nslots / kDiaSlice (+ kDiaPad)
   void *dia_mask = nullptr;   // uint64 x 2 per slot column: bit l of word q = row 2l + q present
   void *dia_val = nullptr;    // dtype, dia_nslots (+ pad), row order within a slot column; holes are 0
+  // paired-row SELL-128 image (general matrices, k = 1; spmv_pair_kernel):
+  // slice s covers rows [128 s, 128 s + 128); slot column j of the slice
+  // holds the j-th stored entry of every row, row r at position r - 128 s,
+  // as a value and a uint16 delta over the slot column's int32 base
+  // (0xFFFF = padding). Built when neither the DIA nor the column-blocked
+  // image serves k = 1, every slot column spans <= 65534 columns and the
+  // slots stay within 1.25x the SELL-64 image's.
+  bool sp = false;
+  int64_t sp_nslices = 0, sp_nslots = 0;
+  int sp_max_width = 0;
+  void *sp_sptr = nullptr;   // int64, sp_nslices + 1 (slots; kPairSlice per slot column)
+  void *sp_width = nullptr;  // int32, sp_nslices
+  void *sp_cbase = nullptr;  // int32, sp_nslots / kPairSlice (+ kDiaPad)
+  void *sp_delta = nullptr;  // uint16, sp_nslots (+ pad)
+  void *sp_val = nullptr;    // dtype, sp_nslots (+ pad)
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;

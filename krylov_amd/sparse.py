@@ -72,11 +72,12 @@ class CsrOperator:
 
     def layout(self):
         """The device image: {"slices", "slots", "irregular", "compact",
-        "col_blocks", "dia", "dia_slots"}."""
-        info = np.zeros(7, dtype=np.int64)
-        check(lib.kry_csr_info_n(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 7))
+        "col_blocks", "dia", "dia_slots", "pair", "pair_slots"} (kry_csr_info_n)."""
+        info = np.zeros(9, dtype=np.int64)
+        check(lib.kry_csr_info_n(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 9))
         return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3]),
-                "col_blocks": int(info[4]), "dia": bool(info[5]), "dia_slots": int(info[6])}
+                "col_blocks": int(info[4]), "dia": bool(info[5]), "dia_slots": int(info[6]), "pair": bool(info[7]),
+                "pair_slots": int(info[8])}
 
     def matvec_device(self, x, y):
         """y = A x for DeviceVectors (no host traffic)."""

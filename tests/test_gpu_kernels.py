@@ -114,10 +114,11 @@ def test_sell64_k1_regular_compact_bitwise(monkeypatch, dtype):
     """SELL-64 at k = 1 on a compact image of regular slices (no DIA image):
     rows of 0-16 banded entries, an empty slice, a 16-wide slice, a partial
     last slice; bitwise SciPy csr_matvec. (The solvers on this path:
-    tests/test_gpu_dia.py with KRY_SPMV_DIA=0.)"""
+    tests/test_gpu_dia.py with KRY_SPMV_DIA=0 and KRY_SPMV_PAIR=0.)"""
     import krylov_amd
 
     monkeypatch.setenv("KRY_SPMV_DIA", "0")
+    monkeypatch.setenv("KRY_SPMV_PAIR", "0")
     rng = np.random.default_rng(7)
     n = 64 * 37 + 5
     lens = rng.integers(0, 17, n)
@@ -135,8 +136,137 @@ def test_sell64_k1_regular_compact_bitwise(monkeypatch, dtype):
     op = krylov_amd.CsrOperator(A)
     lay = op.layout()
     assert lay["compact"] and not lay["dia"] and lay["irregular"] == 0 and lay["col_blocks"] == 0
+    assert not lay["pair"]
     x = rng.standard_normal(n).astype(dtype)
     np.testing.assert_array_equal(np.asarray(op @ x).view(np.uint8), (A @ x).view(np.uint8))
+
+
+def _pair_adversarial(dtype, seed=11):
+    """A general CSR for the paired-row SELL-128 image: n not a multiple of
+    128 or of 2, rows of 0-20 entries, an empty slice, unsorted rows,
+    duplicate and explicit-zero entries, values and x spanning 1e+-20
+    (1e+-8 in float32, where products stay finite); even
+    rows 2l and odd rows 2l + 1 share their offsets in some slices (one 16-B
+    x load serves both) and not in others (the second load)."""
+    rng = np.random.default_rng(seed)
+    n = 128 * 29 + 67
+    lens = rng.integers(0, 21, n)
+    lens[128:256] = 0  # an empty slice
+    rows, cols = [], []
+    for i in range(n):
+        if (i // 128) % 3 == 0:  # stencil-like: pairs of rows share offsets
+            offs = np.sort(rng.choice(np.arange(-900, 900), lens[i - (i & 1)], replace=False))
+            c = np.clip(i + offs, 0, n - 1)[: lens[i]]
+        else:
+            c = rng.integers(max(0, i - 3000), min(n, i + 3000), lens[i])
+            if i % 5 == 0:
+                c = np.sort(c)
+        if i % 7 == 0 and c.shape[0] > 1:
+            c[-1] = c[0]  # a duplicate (kept, added twice as csr_matvec does)
+        rows.append(np.full(c.shape[0], i))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    e = 20 if dtype == np.float64 else 8
+    vals = (rng.standard_normal(rows.shape[0]) * 10.0 ** rng.integers(-e, e, rows.shape[0])).astype(dtype)
+    vals[::17] = 0.0  # explicit zeros
+    indptr = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=n))]).astype(np.int32)
+    A = scipy.sparse.csr_matrix((vals, cols.astype(np.int32), indptr), shape=(n, n))  # stored order kept
+    x = (rng.standard_normal(n) * 10.0 ** rng.integers(-e, e, n)).astype(dtype)
+    return A, x
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_pair_image_bitwise_adversarial(dtype):
+    """The paired-row SELL-128 kernel (general CSR, k = 1): bitwise SciPy
+    csr_matvec on unsorted rows, duplicates, explicit zeros, empty and
+    partial slices, paired and unpaired x loads; block RHS on the same
+    operator stay on SELL-64 and bitwise csr_matvecs."""
+    import krylov_amd
+
+    A, x = _pair_adversarial(dtype)
+    assert not A.has_sorted_indices
+    op = krylov_amd.CsrOperator(A)
+    lay = op.layout()
+    assert lay["pair"] and not lay["dia"] and lay["col_blocks"] == 0
+    assert lay["pair_slots"] % 128 == 0 and lay["pair_slots"] <= 1.25 * lay["slots"] + 4 * 128 * 20
+    np.testing.assert_array_equal(np.asarray(op @ x).view(np.uint8), (A @ x).view(np.uint8))
+    X = np.stack([x, x[::-1].copy()], axis=1)
+    np.testing.assert_array_equal(np.asarray(op @ X).view(np.uint8), (A @ X).view(np.uint8))
+
+
+def test_pair_image_unreferenced_nan_never_added():
+    """x entries no row references hold NaN: the paired 16-B load reads the
+    neighbour of a column without using it, and padding slots are dropped by
+    a select, so y stays finite and bitwise."""
+    import krylov_amd
+
+    A, x = _pair_adversarial(np.float64, seed=5)
+    used = np.zeros(A.shape[0], dtype=bool)
+    used[A.indices] = True
+    x = x.copy()
+    x[~used] = np.nan
+    assert (~used).sum() > 0
+    op = krylov_amd.CsrOperator(A)
+    assert op.layout()["pair"]
+    y = op @ x
+    ref = A @ x
+    assert np.isfinite(ref).all()
+    np.testing.assert_array_equal(y.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_pair_image_int64_through_abi(dtype):
+    """int64 indices handed straight to kry_csr_create get the paired image
+    too (the deltas are relative; n < 2^31) and stay bitwise."""
+    import ctypes
+
+    from krylov_amd import _lib
+    from krylov_amd.device import DeviceVector, get_context
+
+    A, x = _pair_adversarial(dtype, seed=3)
+    ctx = get_context()
+    ip, ix = A.indptr.astype(np.int64), A.indices.astype(np.int64)
+    dv = np.ascontiguousarray(A.data)
+    n = A.shape[0]
+    h = ctypes.c_void_p()
+    _lib.check(_lib.lib.kry_csr_create(ctx.handle, n, ix.shape[0], _lib.ptr(ip), _lib.ptr(ix), _lib.ptr(dv),
+                                       _lib.dtype_code(dv.dtype), _lib.KRY_I64, ctypes.byref(h)))
+    try:
+        info = np.zeros(9, dtype=np.int64)
+        _lib.check(_lib.lib.kry_csr_info_n(h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 9))
+        assert info[7] == 1 and info[3] == 0
+        xv = DeviceVector.from_host(ctx, x)
+        y = DeviceVector(ctx, n, 1, dv.dtype)
+        _lib.check(_lib.lib.kry_spmv(ctx.handle, h, xv.handle, y.handle))
+        got = y.to_host().reshape(-1)
+        np.testing.assert_array_equal(got.view(np.uint8), (A @ x).view(np.uint8))
+    finally:
+        _lib.lib.kry_csr_destroy(h)
+
+
+def test_pair_image_selection(monkeypatch):
+    """Stencils keep the DIA image, cfg3-like scattered matrices the
+    column-blocked one, random patterns whose slot columns span more than
+    65534 columns keep SELL-64; KRY_SPMV_PAIR=0 disables the paired image
+    and both images give the same bits."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    S = problems.stencil15_3d(24)
+    lay = krylov_amd.CsrOperator(S).layout()
+    assert lay["dia"] and not lay["pair"]
+    R = problems.random_nonsym(200_000, seed=1)
+    assert not krylov_amd.CsrOperator(R).layout()["pair"]
+    monkeypatch.setenv("KRY_SPMV_DIA", "0")
+    x = np.random.default_rng(0).standard_normal(S.shape[0])
+    op = krylov_amd.CsrOperator(S)
+    assert op.layout()["pair"]
+    y = op @ x
+    monkeypatch.setenv("KRY_SPMV_PAIR", "0")
+    op0 = krylov_amd.CsrOperator(S)
+    assert not op0.layout()["pair"]
+    np.testing.assert_array_equal(op0 @ x, y)
+    np.testing.assert_array_equal(y, S @ x)
 
 
 def _scattered_csr(n, lens, seed, sort=True, dtype=np.float64):

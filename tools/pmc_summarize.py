@@ -56,7 +56,10 @@ def main(out):
     scale = 8.0 * slots / cal_fetch
     alg = bench.spmv_S(n, nnz)
     kernels = {}
-    for key, parts in (("dia", ("spmv_dia_kernel", "EpiApDot")), ("sell", ("spmv_sell_kernel", "EpiApDot"))):
+    for key, parts in (("dia", ("spmv_dia_kernel", "EpiApDot")), ("pair", ("spmv_pair_kernel", "EpiApDot")),
+                       ("sell", ("spmv_sell_kernel", "EpiApDot"))):
+        if not any(all(p in k for p in parts) for k in bf):
+            continue
         fetch, name = find(bf, *parts)
         write, _ = find(bw, *parts)
         traffic = fetch * scale + write
@@ -76,7 +79,8 @@ def main(out):
         "dia_slots": slots,
         "n": n,
         "nnz": nnz,
-        "program": "tools/spmv_legs.py 64 (64 metric CG iterations on each image)",
+        "program": "tools/spmv_legs.py 64 (64 metric CG iterations on each image: DIA, paired-row SELL-128, "
+                   "compact SELL-64)",
     }
     print(json.dumps(res, indent=1))
 

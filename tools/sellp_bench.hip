@@ -135,13 +135,14 @@ static bool build_sellp(int64_t n, const std::vector<int> &ip, const std::vector
 typedef double d2v __attribute__((ext_vector_type(2)));
 
 // MODE bits: 1 never pair (two 8-B gathers per lane and slot column);
-// 2 nontemporal delta loads; 4 one slice per wave (grid over the slices)
+// 2 nontemporal delta loads; 4 one slice per wave (grid over the slices);
+// 8 the unpaired second loads of a round behind one wave-level branch
 template <int UNR, int MODE, class Src, class Epi>
 __global__ __launch_bounds__(256) void sellp_kernel(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
                                                     const int *__restrict__ cbase, const uint32_t *__restrict__ dpair,
                                                     const double *__restrict__ val, int64_t nslices, int64_t n, Src src,
                                                     Epi epi, double *__restrict__ part) {
-  constexpr bool NOPAIR = (MODE & 1) != 0, NTD = (MODE & 2) != 0, ONE = (MODE & 4) != 0;
+  constexpr bool NOPAIR = (MODE & 1) != 0, NTD = (MODE & 2) != 0, ONE = (MODE & 4) != 0, WB = (MODE & 8) != 0;
   __shared__ double red[256];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -174,7 +175,9 @@ __global__ __launch_bounds__(256) void sellp_kernel(const int64_t *__restrict__ 
         }
       }
       double x0[UNR], x1[UNR];
-      bool v0[UNR], v1[UNR];
+      bool v0[UNR], v1[UNR], need[UNR];
+      int64_t c1s[UNR];
+      bool anyneed = false;
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const uint32_t lo = d[u] & 0xFFFFu, hi = d[u] >> 16;
@@ -190,8 +193,16 @@ __global__ __launch_bounds__(256) void sellp_kernel(const int64_t *__restrict__ 
           bs.pair(v0[u] ? c0 : (v1[u] ? c1 : 0), xp);
           x0[u] = xp[0];
           x1[u] = pr ? xp[1] : xp[0];
-          if (v0[u] && v1[u] && !pr) x1[u] = bs(c1, 0);
+          need[u] = v0[u] && v1[u] && !pr;
+          c1s[u] = c1;
+          anyneed = anyneed || need[u];
+          if (!WB && need[u]) x1[u] = bs(c1, 0);
         }
+      }
+      if (WB && !NOPAIR && __any(anyneed)) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (need[u]) x1[u] = bs(c1s[u], 0);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -334,15 +345,19 @@ int main(int argc, char **argv) {
     check(nm);                                                                                                        \
   }
     const int64_t one = (P.nslices + 3) / 4;
-    PK(16, 0, 8192, "sellp UNR 16 paired");
     PK(8, 0, 8192, "sellp UNR 8 paired");
     PK(16, 1, 8192, "sellp UNR 16 no pairing");
-    PK(16, 2, 8192, "sellp UNR 16 paired, nt deltas");
+    PK(8, 1, 8192, "sellp UNR 8 no pairing");
     if (one <= 65536) {
-      PK(16, 4, one, "sellp UNR 16 paired, 1 slice/wave");
       PK(8, 4, one, "sellp UNR 8 paired, 1 slice/wave");
+      PK(8, 5, one, "sellp UNR 8 no pairing, 1 slice/wave");
+      PK(8, 12, one, "sellp UNR 8 paired, wave branch, 1 slice/wave");
+      PK(8, 6, one, "sellp UNR 8 paired, nt deltas, 1 slice/wave");
+      PK(4, 4, one, "sellp UNR 4 paired, 1 slice/wave");
+      PK(4, 5, one, "sellp UNR 4 no pairing, 1 slice/wave");
+      PK(16, 5, one, "sellp UNR 16 no pairing, 1 slice/wave");
     }
-    PK(16, 0, 16384, "sellp UNR 16 paired");
+    PK(8, 0, 4096, "sellp UNR 8 paired");
   }
   KC(kry_vec_destroy(xv));
   KC(kry_vec_destroy(yv));
