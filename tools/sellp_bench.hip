@@ -245,6 +245,9 @@ int main(int argc, char **argv) {
   kry_csr *Adia, *Asell;
   KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &Adia));
   setenv("KRY_SPMV_DIA", "0", 1);
+  kry_csr *Apair;
+  KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &Apair));
+  setenv("KRY_SPMV_PAIR", "0", 1);
   KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &Asell));
   printf("library images: dia=%d sell compact=%d sell slots=%ld\n", (int)Adia->dia, (int)Asell->compact,
          (long)Asell->nslots);
@@ -332,6 +335,12 @@ int main(int argc, char **argv) {
                                        nullptr, 0, st);
     });
     check("library SELL-64");
+    timeit("library pair (spmv_pair_kernel, EpiApDot)", img_p, [&] {
+      int G;
+      launch_spmv<double, double, int>(Apair, 1, SrcPlain<double>{x, 1}, EpiApDot<double>{y, nullptr, 1}, part, &G,
+                                       nullptr, 0, st);
+    });
+    check("library pair");
 #define PK(UNR, MODE, GRID, NAME)                                                                                     \
   {                                                                                                                   \
     char nm[96];                                                                                                      \
@@ -345,24 +354,22 @@ int main(int argc, char **argv) {
     check(nm);                                                                                                        \
   }
     const int64_t one = (P.nslices + 3) / 4;
-    PK(8, 0, 8192, "sellp UNR 8 paired");
-    PK(16, 1, 8192, "sellp UNR 16 no pairing");
-    PK(8, 1, 8192, "sellp UNR 8 no pairing");
     if (one <= 65536) {
-      PK(8, 4, one, "sellp UNR 8 paired, 1 slice/wave");
-      PK(8, 5, one, "sellp UNR 8 no pairing, 1 slice/wave");
-      PK(8, 12, one, "sellp UNR 8 paired, wave branch, 1 slice/wave");
       PK(8, 6, one, "sellp UNR 8 paired, nt deltas, 1 slice/wave");
-      PK(4, 4, one, "sellp UNR 4 paired, 1 slice/wave");
-      PK(4, 5, one, "sellp UNR 4 no pairing, 1 slice/wave");
-      PK(16, 5, one, "sellp UNR 16 no pairing, 1 slice/wave");
+      PK(8, 14, one, "sellp UNR 8 paired, nt deltas, wave branch, 1 slice/wave");
+      PK(8, 7, one, "sellp UNR 8 no pairing, nt deltas, 1 slice/wave");
+      PK(16, 6, one, "sellp UNR 16 paired, nt deltas, 1 slice/wave");
+      PK(16, 14, one, "sellp UNR 16 paired, nt deltas, wave branch, 1 slice/wave");
+      PK(16, 7, one, "sellp UNR 16 no pairing, nt deltas, 1 slice/wave");
+      PK(4, 14, one, "sellp UNR 4 paired, nt deltas, wave branch, 1 slice/wave");
+      PK(12, 14, one, "sellp UNR 12 paired, nt deltas, wave branch, 1 slice/wave");
     }
-    PK(8, 0, 4096, "sellp UNR 8 paired");
   }
   KC(kry_vec_destroy(xv));
   KC(kry_vec_destroy(yv));
   KC(kry_csr_destroy(Adia));
   KC(kry_csr_destroy(Asell));
+  KC(kry_csr_destroy(Apair));
   KC(kry_ctx_destroy(ctx));
   return 0;
 }
