@@ -351,7 +351,7 @@ def run_minres_cfg5(steps=100):
             "config": "cfg5 shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights (vectors f64 as in the reference)"}
 
 
-PMC_SUMMARY = "r03_pmc_traffic.json"
+PMC_SUMMARY = "r03b_pmc_traffic.json"
 
 
 def pmc_traffic(n, nnz, kernel):
