@@ -6,6 +6,7 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <chrono>
 #include <unordered_map>
 
 #include "device.hpp"
@@ -794,10 +795,28 @@ static bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_
 }
 
 namespace {
+// KRY_UPLOAD_TRACE=1: wall-clock split of kry_csr_create's phases, to stderr
+struct UploadTrace {
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  UploadTrace() {
+    const char *e = getenv("KRY_UPLOAD_TRACE");
+    on = e && atoi(e) != 0;
+    t = std::chrono::steady_clock::now();
+  }
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "kry_csr_create %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+
 template <typename I, typename MV>
 void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   hipStream_t st = A->ctx->stream;
   const int64_t n = A->n, nnz = A->nnz;
+  UploadTrace tr;
   KRY_REQUIRE(ip[0] == 0 && (int64_t)ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
   for (int64_t r = 0; r < n; ++r)
     KRY_REQUIRE(ip[r + 1] >= ip[r], KRY_EINVAL, "indptr must be non-decreasing");
@@ -809,6 +828,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   std::vector<I> sidx;
   std::vector<MV> sval;
   sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
+  tr.mark("SELL-64 plan + fill");
   A->sptr = dev_alloc(sptr.size() * 8);
   A->swidth = dev_alloc(width.size() * 4 + 4);
   // compact image unless disabled (KRY_SELL_COMPACT=0) or impossible
@@ -830,6 +850,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
   if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
   KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+  if (tr.on) KRY_HIP(hipStreamSynchronize(st));
+  tr.mark("compact image + H2D");
   // diagonal-offset image for structured single-RHS SpMVs (KRY_SPMV_DIA=0 disables)
   const char *denv = getenv("KRY_SPMV_DIA");
   if (!(denv && atoi(denv) == 0)) {
@@ -851,6 +873,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->dia_val, dh.val.data(), dh.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
     }
+    tr.mark("DIA image + H2D");
   }
   // column-blocked image for scattered single-RHS SpMVs (KRY_SPMV_CB=0 disables)
   const char *cbenv = getenv("KRY_SPMV_CB");
@@ -871,6 +894,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->cb_val, cb.val.data(), cb.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
     }
+    tr.mark("column-blocked image + H2D");
   }
   // paired-row SELL-128 image for general single-RHS SpMVs (KRY_SPMV_PAIR=0 disables)
   const char *penv = getenv("KRY_SPMV_PAIR");
@@ -893,6 +917,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->sp_val, ph.val.data(), ph.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
     }
+    tr.mark("paired image + H2D");
   }
   if (A->nirregular > 0) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
@@ -905,6 +930,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
     }
   }
   KRY_HIP(hipStreamSynchronize(st));  // host staging vectors die at return
+  tr.mark("CSR copy + final sync");
 }
 }  // namespace
 
