@@ -79,6 +79,13 @@ struct kry_cg {
   int fusep = -1;
   bool fusep_used = false;  // the current chunk ran it
   bool fusep_last = false;  // ... the last kry_cg_run chunk
+  // block right-hand sides on the separate passes: yk += alpha p (cg.py:196)
+  // deferred and applied ydefer steps at a time (cg_pdefer_kernel, then
+  // cg_yflush at the chunk's end), p_i in pring[i % (ydefer + 1)] within a
+  // chunk (pring[0] is p). ydefer = -1 undecided, 0 not used.
+  int ydefer = -1;
+  void *pring[8] = {};
+  double *alpha_ring = nullptr;  // ydefer x k: alpha of step j at row j % ydefer
 };
 
 namespace {
@@ -86,6 +93,7 @@ namespace {
 enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_RHO_OLD = 6, S_COUNT = 7 };
 
 constexpr int kCgUpdateGrid = 1024;  // update-pass blocks: the <r, r> partials every yp block re-reduces
+constexpr int kCgYDefer = 7;         // deferred yk updates per flush (KRY_CG_YDEFER; 3 when memory is short)
 
 template <typename V>
 struct OpCgUpdate {
@@ -365,6 +373,168 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
   }
 }
 
+// The yp pass with yk += alpha p deferred (block right-hand sides, separate
+// passes): step i computes omega from the <r, r> partials exactly as
+// cg_yp_kernel does, records alpha_i in alpha_ring, and writes p_{i+1} = r +
+// omega p_i (cg.py:178) into the next ring buffer; every D-th step it also
+// applies the D deferred updates yk += alpha_j p_j (cg.py:196), j = i - D + 1
+// .. i, in that order (the same sequence of roundings as one update per
+// step: bitwise the same yk). Per D steps the passes read and write yk once
+// instead of D times: 3 vectors per step and D + 4 on the flushing one,
+// against 5 per step.
+template <typename V>
+struct PRing {
+  V *s[8];
+};
+
+template <typename V, typename S>
+__global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *__restrict__ y, PRing<V> ring, int D,
+                                                           const V *__restrict__ r, const double *__restrict__ part,
+                                                           int P, double *scal, double *alpha_ring, double *hist,
+                                                           Ctrl *ctrl, int step, double *gbuf, int col_offset,
+                                                           int total_k) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  __shared__ double red[kBlock];
+  __shared__ double sh_a[8][kMaxCols];  // alpha of the flushed steps, oldest first
+  __shared__ double sh_om[kMaxCols], rn[kMaxCols];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const bool flush = (step + 1) % D == 0;
+  const int nf = flush ? D : 0;
+  reduce_partials(part, P, k, red);
+  if (tid < k) {
+    const S rr = (S)red[tid];
+    const S old = (S)scal[S_RHO_OLD * k + tid];
+    const S om = rr / safe<S>(old);
+    sh_om[tid] = (double)om;
+    const double a = scal[S_ALPHA * k + tid];
+    for (int q = 0; q + 1 < nf; ++q) sh_a[q][tid] = alpha_ring[(int64_t)((step - nf + 1 + q) % D) * k + tid];
+    if (nf) sh_a[nf - 1][tid] = a;
+    const S nrm = sqrt(rr);
+    rn[tid] = (double)nrm;
+    if (g == 0) {
+      alpha_ring[(int64_t)(step % D) * k + tid] = a;
+      scal[S_RHO_PREV * k + tid] = (double)old;
+      scal[S_RHO * k + tid] = (double)rr;
+      scal[S_OMEGA * k + tid] = (double)om;
+      if (!gbuf) hist[(int64_t)step * k + tid] = (double)nrm;
+    }
+  }
+  __syncthreads();
+  const V *pi = ring.s[step % (D + 1)];
+  V *pn = ring.s[(step + 1) % (D + 1)];
+  const int64_t ngrp = (N + W - 1) / W;
+  const int64_t per = ((ngrp + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+  const int64_t v0 = per * g;
+  const int64_t v1 = v0 + per < ngrp ? v0 + per : ngrp;
+  for (int64_t gi = v0 + tid; gi < v1; gi += kBlock) {
+    const int64_t e = gi * W;
+    V pv[W], rv[W];
+    VIO<V>::load(pi, e, N, pv);
+    VIO<V>::load(r, e, N, rv);
+    if (flush) {
+      V yv[W];
+      VIO<V>::load_nt(y, e, N, yv);
+      for (int q = 0; q < nf; ++q) {
+        V pj[W];
+        if (q + 1 < nf) VIO<V>::load_nt(ring.s[(step - nf + 1 + q) % (D + 1)], e, N, pj);
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const V a = (V)sh_a[q][(int)((e + u) & (k - 1))];
+          const V t1 = a * (q + 1 < nf ? pj[u] : pv[u]);
+          yv[u] = yv[u] + t1;  // yk += alpha_j p_j (cg.py:196), j ascending
+        }
+      }
+      VIO<V>::store_nt(y, e, N, yv);
+    }
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      const V om = (V)sh_om[(int)((e + u) & (k - 1))];
+      const V t = om * pv[u];
+      pv[u] = rv[u] + t;  // p = r + omega p (cg.py:178)
+    }
+    VIO<V>::store(pn, e, N, pv);
+  }
+  if (g == 0) {
+    if (gbuf) {
+      for (int t = tid; t < total_k; t += kBlock) {
+        const int lc = t - col_offset;
+        gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
+      }
+    } else if (all_le(rn, scal + S_CRIT * k, k, &flag) && tid == 0) {
+      ctrl->stop_at = step + 1;
+    }
+  }
+}
+
+// The end of a chunk on the deferred path: m = min(stop_at, steps) steps ran;
+// the updates of steps (m / D) D .. m - 1 are still pending (yk += alpha_j
+// p_j in order), and p_m sits in ring buffer m % (D + 1), copied to p
+// (pring[0]) for the next chunk. Not halted by ctrl (it reads it).
+template <typename V>
+struct OpCgYFlush {
+  V *y;
+  PRing<V> ring;
+  int D;
+  const double *alpha_ring;
+  const Ctrl *ctrl;
+  int steps, k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    const int m = ctrl->stop_at < steps ? ctrl->stop_at : steps;
+    const int j0 = m / D * D;
+    if (j0 < m) {
+      V yv[W];
+      VIO<V>::load_nt(y, e, N, yv);
+      for (int j = j0; j < m; ++j) {
+        V pj[W];
+        VIO<V>::load(ring.s[j % (D + 1)], e, N, pj);
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+          const V a = (V)alpha_ring[(int64_t)(j % D) * k + (int)((e + u) & (k - 1))];
+          const V t1 = a * pj[u];
+          yv[u] = yv[u] + t1;
+        }
+      }
+      VIO<V>::store_nt(y, e, N, yv);
+    }
+    if (m % (D + 1) != 0) {
+      V pv[W];
+      VIO<V>::load(ring.s[m % (D + 1)], e, N, pv);
+      VIO<V>::store(ring.s[0], e, N, pv);
+    }
+  }
+};
+
+// yk += alpha_j p_j for j = j0 .. j1 - 1 in order (cg.py:196): the deferred
+// updates of a flushing step of the one-launch update path.
+template <typename V>
+struct OpCgYSteps {
+  V *y;
+  PRing<V> ring;
+  int D;
+  const double *alpha_ring;
+  int j0, j1, k;
+  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
+    constexpr int W = Vec16<V>::W;
+    V yv[W];
+    VIO<V>::load_nt(y, e, N, yv);
+    for (int j = j0; j < j1; ++j) {
+      V pj[W];
+      VIO<V>::load_nt(ring.s[j % (D + 1)], e, N, pj);
+#pragma unroll
+      for (int u = 0; u < W; ++u) {
+        const V a = (V)alpha_ring[(int64_t)(j % D) * k + (int)((e + u) & (k - 1))];
+        const V t1 = a * pj[u];
+        yv[u] = yv[u] + t1;
+      }
+    }
+    VIO<V>::store_nt(y, e, N, yv);
+  }
+};
+
 // ------------------------------------- one-launch CG update (large n, k = 1)
 // Replaces the alpha kernel, the r pass and the fused rho / y / p pass of an
 // iteration for one right-hand side, no M / Ml, Euclidean inner and n up to
@@ -386,13 +556,18 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 constexpr int kUpdBlock = 512;
 constexpr int kUpdU = 2;  // granules per streamed chunk
 constexpr size_t kUpdWords = 16 + 2 * 2 * 256 * 2;  // abort word area + two parity regions of G <= 256 granule pairs
-template <typename V, typename S, int NV>
+// DEF (deferred yk, see cg_pdefer_kernel): y is neither read nor written,
+// p_{i+1} goes to pout (the next ring buffer) and alpha to alpha_ring[step %
+// D]; 5 vectors per iteration, the yk updates applied D steps at a time by
+// OpCgYSteps.
+template <typename V, typename S, int NV, bool DEF>
 __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restrict__ y, V *__restrict__ r,
                                                            V *__restrict__ p, const V *__restrict__ Ap,
                                                            const double *__restrict__ partA, int PA, double *scal,
                                                            double *hist, Ctrl *ctrl, int step, double *gbuf,
                                                            int col_offset, int total_k, unsigned *words,
-                                                           int fault_step) {
+                                                           int fault_step, V *__restrict__ pout,
+                                                           double *__restrict__ alpha_ring, int D) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int U = kUpdU;
@@ -415,7 +590,8 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
   const int64_t seg = (int64_t)NV * kUpdBlock * W;
   const int64_t e0 = (int64_t)blockIdx.x * seg;
-  const BufSeg<V, kUpdBlock> sr(r, e0, N, seg), sa(Ap, e0, N, seg), sy(y, e0, N, seg), sp(p, e0, N, seg);
+  const BufSeg<V, kUpdBlock> sr(r, e0, N, seg), sa(Ap, e0, N, seg), sy(y, e0, N, seg), sp(p, e0, N, seg),
+      spo(pout, e0, N, seg);
   V ca[2][U][W], cb[2][U][W];
   auto ld2 = [&](const BufSeg<V, kUpdBlock> &s1, const BufSeg<V, kUpdBlock> &s2, int c, V(&d1)[U][W],
                  V(&d2)[U][W]) {
@@ -455,7 +631,12 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16) + (size_t)(step & 1) * 2 * 256;
   const unsigned tag = (unsigned)step + 1u;
   if (tid == 0) publish_partial(gran + 2 * blockIdx.x, tag, bp);
-  ld2(sp, sy, 0, ca[0], cb[0]);  // chunk 0 of p and y travels during the exchange
+  auto ld1 = [&](int c, V(&d1)[U][W]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) sp.template load<W>(c * U + u, d1[u]);
+  };
+  if constexpr (DEF) ld1(0, ca[0]);
+  else ld2(sp, sy, 0, ca[0], cb[0]);  // chunk 0 of p and y travels during the exchange
   if (tid < 64) {
     // every block commits or every block aborts (decide_exchange): no block
     // stores its segment after another gave up
@@ -475,25 +656,35 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   for (int c = 0; c < NC; ++c) {
     const int b = c & 1;
     __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NC) ld2(sp, sy, c + 1, ca[b ^ 1], cb[b ^ 1]);
+    if (c + 1 < NC) {
+      if constexpr (DEF) ld1(c + 1, ca[b ^ 1]);
+      else ld2(sp, sy, c + 1, ca[b ^ 1], cb[b ^ 1]);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int g = c * U + u;
       V yv[W], pv[W];
 #pragma unroll
       for (int v = 0; v < W; ++v) {
-        const V t1 = a * ca[b][u][v];
-        yv[v] = cb[b][u][v] + t1;
+        if constexpr (!DEF) {
+          const V t1 = a * ca[b][u][v];
+          yv[v] = cb[b][u][v] + t1;
+        }
         const V t = o * ca[b][u][v];
         pv[v] = rr[g][v] + t;
       }
-      sy.template store<W, 2>(g, yv);
-      sp.template store<W>(g, pv);
+      if constexpr (DEF) {
+        spo.template store<W>(g, pv);
+      } else {
+        sy.template store<W, 2>(g, yv);
+        sp.template store<W>(g, pv);
+      }
       sr.template store<W>(g, rr[g]);
     }
   }
   if (blockIdx.x == 0) {
     if (tid == 0) {
+      if (DEF) alpha_ring[step % D] = (double)alpha;
       scal[S_ALPHA] = (double)alpha;
       scal[S_RHO_OLD] = (double)rho;
       scal[S_RHO_PREV] = (double)rho;
@@ -975,21 +1166,22 @@ bool cgp_launch(kry_cg *s, int max_steps, bool decide_only = false) {
 // most 512 * 40 granules per block at one block per CU (decided once per
 // solver; KRY_CG_UPD=0 disables). Returns false when not launched.
 template <typename V, typename S, int NV>
-void *cgu_kern() {
-  return reinterpret_cast<void *>(cg_upd_kernel<V, S, NV>);
+void *cgu_kern(bool def) {
+  return def ? reinterpret_cast<void *>(cg_upd_kernel<V, S, NV, true>)
+             : reinterpret_cast<void *>(cg_upd_kernel<V, S, NV, false>);
 }
 template <typename V>
-bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) {
+bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf, const PRing<V> &ring, int D) {
   constexpr int W = Vec16<V>::W;
   using S = V;
   const int64_t N = s->n;
-  auto kern = [&](int nv) -> void * {
+  auto kern = [&](int nv, bool def = false) -> void * {
     switch (nv) {
-      case 8: return cgu_kern<V, S, 8>();
-      case 16: return cgu_kern<V, S, 16>();
-      case 24: return cgu_kern<V, S, 24>();
-      case 32: return cgu_kern<V, S, 32>();
-      default: return cgu_kern<V, S, 40>();
+      case 8: return cgu_kern<V, S, 8>(def);
+      case 16: return cgu_kern<V, S, 16>(def);
+      case 24: return cgu_kern<V, S, 24>(def);
+      case 32: return cgu_kern<V, S, 32>(def);
+      default: return cgu_kern<V, S, 40>(def);
     }
   };
   if (s->upd_nv < 0) {
@@ -1022,15 +1214,20 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
   int fault_step = fe ? atoi(fe) : -1;
   const char *fl = getenv("KRY_CGU_FAULT_LATE");  // ... or joins late (decide_exchange tests)
   if (fault_step >= 0 && fl) fault_step |= (atoi(fl) & 0x7fff) << 16;
-  V *y = static_cast<V *>(s->y), *r = static_cast<V *>(s->r), *p = static_cast<V *>(s->p);
+  V *y = static_cast<V *>(s->y), *r = static_cast<V *>(s->r);
+  V *p = D ? ring.s[step % (D + 1)] : static_cast<V *>(s->p);
+  V *pout = D ? ring.s[(step + 1) % (D + 1)] : p;
+  double *alpha_ring = s->alpha_ring;
+  int Dv = D ? D : 1;
   const V *Ap = static_cast<const V *>(s->Ap);
   double *scal = s->scal, *hist = s->hist;
   Ctrl *ctrl = s->ctrl;
   int col_offset = s->col_offset, total_k = s->total_k;
   unsigned *words = s->upd_words;
   int64_t n = N;
-  void *args[] = {&n, &y, &r, &p, &Ap, &partA, &PA, &scal, &hist, &ctrl, &step, &gbuf, &col_offset, &total_k,
-                  &words, &fault_step};
+  void *args[] = {&n,    &y,        &r,          &p,       &Ap,    &partA,       &PA,        &scal,
+                  &hist, &ctrl,     &step,       &gbuf,    &col_offset, &total_k, &words,  &fault_step,
+                  &pout, &alpha_ring, &Dv};
   hipError_t le;
   {
     // A plain launch: a cooperative one costs ~8 us more stream time on each
@@ -1039,7 +1236,12 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf) 
     // exchange's bounded spin with rollback covers a block that still does
     // not become resident.
     ProfScope ps(s->ctx, PROF_UPDATE);
-    le = hipLaunchKernel(kern(nv), dim3(G), dim3(kUpdBlock), args, 0, st);
+    le = hipLaunchKernel(kern(nv, D != 0), dim3(G), dim3(kUpdBlock), args, 0, st);
+  }
+  if (le == hipSuccess && D && (step + 1) % D == 0) {  // the D deferred yk updates of steps step - D + 1 .. step
+    ProfScope ps(s->ctx, PROF_OTHER);
+    launch_elementwise<V>(N, 1, OpCgYSteps<V>{y, ring, D, s->alpha_ring, step - D + 1, step + 1, 1}, nullptr, ctrl,
+                          step, st);
   }
   if (le != hipSuccess) {
     (void)hipGetLastError();
@@ -1164,8 +1366,34 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     return false;
   }
   double *partA = s->part, *partB = s->part + part_rows(k) * k;
+  // deferred yk updates on the block path (KRY_CG_YDEFER = D, 0 = off)
+  if (s->ydefer < 0) {
+    s->ydefer = 0;
+    const char *e = getenv("KRY_CG_YDEFER");
+    const size_t vb = ((size_t)s->n * k + 15) / 16 * 16 * dsize(s->dtype);
+    size_t fr = 0, tot = 0;
+    KRY_HIP(hipMemGetInfo(&fr, &tot));
+    // the default: only for vectors larger than half the 256 MB MALL (a
+    // smaller y / p stay cache-resident between the passes, and reading the
+    // ring's older p vectors back costs more than the y pass it saves: metric
+    // CG, 80 MB vectors, 3,016 -> 2,874 it/s with D = 7; cfg4, 640 MB, 690 ->
+    // 748 it/s), with D ring buffers within a quarter of the free memory
+    const bool big = vb > (size_t(128) << 20);
+    int D = e ? atoi(e) : !big ? 0 : (kCgYDefer * vb <= fr / 4 ? kCgYDefer : (3 * vb <= fr / 4 ? 3 : 0));
+    if (D >= 1 && D <= 7 && k <= 8 && !s->M) {
+      for (int q = 1; q <= D; ++q) s->pring[q] = dev_alloc(vb);
+      s->alpha_ring = static_cast<double *>(dev_alloc((size_t)D * k * 8));
+      s->ydefer = D;
+    }
+  }
+  const int D = (!s->M && k <= 8) ? s->ydefer : 0;
+  PRing<V> ring{};
+  if (D) {
+    ring.s[0] = static_cast<V *>(s->p);
+    for (int q = 1; q <= D; ++q) ring.s[q] = static_cast<V *>(s->pring[q]);
+  }
   for (int step = 0; step < max_steps; ++step) {
-    V *p = static_cast<V *>(s->p);
+    V *p = D ? ring.s[step % (D + 1)] : static_cast<V *>(s->p);
     int PA, PB;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
@@ -1180,7 +1408,7 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       }
     }
     double *gb = s->comm ? s->gbuf : nullptr;
-    if (!s->M && !s->Ml && k == 1 && cgu_launch<V>(s, partA, PA, step, gb)) {
+    if (!s->M && !s->Ml && k == 1 && cgu_launch<V>(s, partA, PA, step, gb, ring, D)) {
       // alpha, r, rho, omega, y and p in one launch (cg_upd_kernel)
     } else if (!s->M && k <= 8) {  // alpha kernel, r pass, then the fused rho / y / p pass
       launch_alpha(s, partA, PA, partB, step);
@@ -1194,7 +1422,16 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       ProfScope ps(s->ctx, PROF_OTHER);
       constexpr int W = Vec16<V>::W;
       const int G = grid_for((N + W - 1) / W, kBlock * 2);
-      if (s->scalar_f32)
+      if (D) {
+        if (s->scalar_f32)
+          hipLaunchKernelGGL((cg_pdefer_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
+                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
+                             step, gb, s->col_offset, s->total_k);
+        else
+          hipLaunchKernelGGL((cg_pdefer_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
+                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
+                             step, gb, s->col_offset, s->total_k);
+      } else if (s->scalar_f32)
         hipLaunchKernelGGL((cg_yp_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
                            static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
                            s->col_offset, s->total_k);
@@ -1244,6 +1481,12 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       KRY_HIP(hipGetLastError());
     }
   }
+  if (D) {  // the pending yk updates, and p_m back into p (skipped when no step ran)
+    ProfScope ps(s->ctx, PROF_OTHER);
+    launch_elementwise<V>(N, k,
+                          OpCgYFlush<V>{static_cast<V *>(s->y), ring, D, s->alpha_ring, s->ctrl, max_steps, k},
+                          nullptr, s->ctrl, 0, st);
+  }
   return false;
 }
 
@@ -1283,7 +1526,8 @@ static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
                   s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
                   s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
-                  s->cgp_scal, s->cgp_words, s->upd_words, s->p_alt};
+                  s->cgp_scal, s->cgp_words, s->upd_words, s->p_alt, s->alpha_ring,
+                  s->pring[1], s->pring[2], s->pring[3], s->pring[4], s->pring[5], s->pring[6], s->pring[7]};
   for (void *b : bufs) dev_free(b);
 }
 

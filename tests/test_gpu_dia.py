@@ -300,3 +300,107 @@ def test_block_cg_fused_p_pass_bitwise(case, k, monkeypatch):
     assert info1.numsteps == info0.numsteps and info1.success == info0.success
     _bits_equal(np.asarray(info1.resnorms), np.asarray(info0.resnorms))
     _bits_equal(info1.xk, info0.xk)
+
+
+@pytest.mark.parametrize("D", [1, 3, 7])
+@pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general"])
+def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
+    """Block CG with yk += alpha p deferred and applied D steps at a time
+    (cg_pdefer_kernel, p cycling through D + 1 buffers, OpCgYFlush at each
+    chunk's end) against one update per step (KRY_CG_YDEFER=0): the same
+    roundings in the same order, so the history, the iterate and the step
+    count are bitwise equal, for chunks of 1, 7, 32, 1 and 19 steps (ends
+    that fall before, on and after a flush), a solve stopping in the middle
+    of a chunk (tol), a weighted inner product and a general (non-DIA)
+    matrix."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+
+    inner = None
+    k = 4
+    if case == "poisson2d_300_f64":
+        A = problems.poisson2d(300)
+        k = 8
+    elif case == "lap3d_f32":
+        A, _ = problems.shifted_lap3d_weighted(24)
+    elif case == "banded_general":
+        n = 20_000
+        rng = np.random.default_rng(9)
+        offs = [-301, -17, -1, 0, 1, 17, 301]
+        diags = [rng.uniform(-1.0, 0.0, n - abs(o)) for o in offs]
+        A = scipy.sparse.diags(diags, offs, format="csr")
+        A = (A + A.T).tocsr()
+        A = A + scipy.sparse.diags(np.asarray(abs(A).sum(axis=1)).ravel() + 1.0)
+        A = A.tocsr()
+        A.sort_indices()
+        k = 2
+    else:
+        A = problems.poisson2d(200)
+        inner = krylov_amd.WeightedInner(np.random.default_rng(4).uniform(1.0, 2.0, A.shape[0]))
+    dt = np.float32 if A.dtype == np.float32 else np.float64
+    B = np.random.default_rng(k).standard_normal((A.shape[0], k)).astype(dt)
+    B[:, -1] *= 1e-2  # columns converge at different steps
+    op = krylov_amd.CsrOperator(A)
+
+    def solve(d):
+        monkeypatch.setenv("KRY_CG_YDEFER", str(d))
+        st = _CGState(_helpers.Problem(op, B, None, inner))
+        st.start()
+        st.set_criterion(np.zeros(k))
+        hs = [st.run(n) for n in (1, 7, 32, 1, 19)]
+        h, x = np.concatenate(hs), st.get(0)
+        _, info = krylov_amd.cg(op, B, inner=inner, tol=1e-6)
+        return h, x, info
+
+    h1, x1, info1 = solve(D)
+    h0, x0, info0 = solve(0)
+    _bits_equal(h1, h0)
+    _bits_equal(x1, x0)
+    assert info1.numsteps == info0.numsteps and info1.success == info0.success
+    _bits_equal(np.asarray(info1.resnorms), np.asarray(info0.resnorms))
+    _bits_equal(info1.xk, info0.xk)
+
+
+@pytest.mark.parametrize("path", ["upd", "passes", "upd_general"])
+def test_single_rhs_cg_deferred_y_bitwise(path, monkeypatch):
+    """One right-hand side with yk deferred 7 steps at a time: the one-launch
+    update kernel skipping y (cg_upd_kernel<..., DEF>, OpCgYSteps on every
+    7th step) and the separate passes (KRY_CG_UPD=0: cg_pdefer_kernel at
+    k = 1), on the DIA image and on a general matrix (paired image), against
+    KRY_CG_YDEFER=0: histories, iterates and step counts bitwise equal, for
+    chunks ending before, on and after a flush and a solve stopping
+    mid-chunk."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    if path == "passes":
+        monkeypatch.setenv("KRY_CG_UPD", "0")
+    if path == "upd_general":
+        monkeypatch.setenv("KRY_SPMV_DIA", "0")
+    A = problems.stencil15_3d(40)
+    op = krylov_amd.CsrOperator(A)
+    assert op.layout()["pair"] == (path == "upd_general")
+    b = np.random.default_rng(2).standard_normal(A.shape[0])
+
+    def solve(d):
+        monkeypatch.setenv("KRY_CG_YDEFER", str(d))
+        st = _CGState(_helpers.Problem(op, b, None, None))
+        st.start()
+        st.set_criterion(np.zeros(1))
+        hs = [st.run(n) for n in (1, 7, 32, 1, 19, 6)]
+        upd = st.update_path()
+        h, x = np.concatenate(hs), st.get(0)
+        _, info = krylov_amd.cg(op, b, tol=1e-7)
+        return h, x, info, upd
+
+    h1, x1, info1, upd1 = solve(7)
+    h0, x0, info0, upd0 = solve(0)
+    assert upd1[0] == upd0[0] == (0 if path == "passes" else 1)
+    _bits_equal(h1, h0)
+    _bits_equal(x1, x0)
+    assert info1.numsteps == info0.numsteps and info1.success == info0.success
+    _bits_equal(np.asarray(info1.resnorms), np.asarray(info0.resnorms))
+    _bits_equal(info1.xk, info0.xk)
