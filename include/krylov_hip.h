@@ -103,6 +103,16 @@ int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices,
  * that offset). Call once with null arrays to size them. */
 int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
                  int32_t *widths, int32_t *offsets, uint64_t *masks);
+/* Host-only view of the paired-row SELL-128 plan (no device needed; the
+ * image kry_csr_create builds for a general matrix, kry_version() >= 102):
+ * info[0..3] = built (0 = refused: a slot column spans more than 65534
+ * columns, n >= 2^31, or more than 1.25x the SELL-64 slots), slices, slots,
+ * widest slice; when built and the arrays are non-null: widths[slices],
+ * cbase[slots / 128] (each slot column's smallest column), deltas[slots]
+ * (column - base at slot 128 * (sptr[s] / 128 + j) + row - 128 s, 0xFFFF =
+ * padding). Call once with null arrays to size them. */
+int kry_pair_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                  int32_t *widths, int32_t *cbase, uint16_t *deltas);
 /* The device image kry_csr_create built, size-checked: writes the first
  * min(len, KRY_CSR_INFO_LEN) of info[0..8] = slices, slots, irregular slices,
  * compact (1 when the column indices are stored as uint16 deltas over

@@ -58,6 +58,7 @@ _SIGNATURES = {
     "kry_csr_destroy": [_vp],
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
     "kry_dia_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
+    "kry_pair_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
     "kry_csr_info": [_vp, _ip64],
     "kry_csr_info_n": [_vp, _ip64, _i32],
     "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
@@ -216,6 +217,28 @@ def dia_plan(indptr, indices):
                            ptr(offsets), ptr(masks)))
     return {"slices": int(info[1]), "slots": int(info[2]), "max_width": int(info[3]), "widths": widths,
             "offsets": offsets, "masks": masks}
+
+
+def pair_plan(indptr, indices):
+    """Host-only paired-row SELL-128 plan (kry_pair_plan): None if the image
+    would not be built, else {"slices", "slots", "max_width", "widths",
+    "cbase", "deltas"}."""
+    indptr = np.ascontiguousarray(indptr)
+    indices = np.ascontiguousarray(indices, dtype=indptr.dtype)
+    n, nnz = indptr.shape[0] - 1, indices.shape[0]
+    info = np.zeros(4, dtype=np.int64)
+    ip64 = info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    check(lib.kry_pair_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, None, None, None))
+    if not info[0]:
+        return None
+    slots = int(info[2])
+    widths = np.zeros(int(info[1]), dtype=np.int32)
+    cbase = np.zeros(slots // 128, dtype=np.int32)
+    deltas = np.zeros(slots, dtype=np.uint16)
+    check(lib.kry_pair_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, ptr(widths),
+                            ptr(cbase), ptr(deltas)))
+    return {"slices": int(info[1]), "slots": slots, "max_width": int(info[3]), "widths": widths, "cbase": cbase,
+            "deltas": deltas}
 
 
 def csr_layout(indptr):

@@ -247,6 +247,56 @@ ProfScope::~ProfScope() {
   ctx->ev_used++;
 }
 
+// ------------------------------------------------- host staging buffers
+// Image staging vectors: no zero-initialisation on resize (std::vector's
+// value-initialisation writes every page from one thread), filled in
+// parallel instead, so the first touch of the pages is spread over threads.
+template <class T>
+struct NoInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInit<U>;
+  };
+  NoInit() = default;
+  template <class U>
+  NoInit(const NoInit<U> &) {}
+  template <class U, class... A>
+  void construct(U *q, A &&...a) {
+    if constexpr (sizeof...(A) == 0) ::new ((void *)q) U;
+    else ::new ((void *)q) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using hvec = std::vector<T, NoInit<T>>;
+
+// A staging vector's pages are returned on a detached thread once its H2D
+// copies have completed (the caller has synchronised the stream): unmapping
+// ~1 GB takes ~0.1 s that kry_csr_create then does not wait for.
+template <class T>
+static void release_later(hvec<T> &v) {
+  if (v.capacity() < (size_t(64) << 20) / sizeof(T)) {
+    hvec<T>().swap(v);
+    return;
+  }
+  auto *h = new hvec<T>();
+  h->swap(v);
+  std::thread([h] { delete h; }).detach();
+}
+
+template <class T>
+static void par_fill(hvec<T> &v, size_t n, T val) {
+  v.resize(n);
+  const unsigned nt = n < (size_t(1) << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (nt == 1) {
+    std::fill(v.begin(), v.end(), val);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] { std::fill(v.data() + n * t / nt, v.data() + n * (t + 1) / nt, val); });
+  for (auto &x : th) x.join();
+}
+
 // ---------------------------------------------------------- SELL-64 layout
 // Host-side plan: slice s = rows [64 s, 64 s + 64); width = longest row;
 // a slice is irregular (CSR walk) when 64 * width > 2 * nnz_slice + 1024.
@@ -275,11 +325,11 @@ static void sell_plan(int64_t n, const I *ip, std::vector<int64_t> *sptr, std::v
 
 template <typename I, typename MV>
 static void sell_fill(int64_t n, const I *ip, const I *ix, const MV *dv, const std::vector<int64_t> &sptr,
-                      const std::vector<int32_t> &width, std::vector<I> &sidx, std::vector<MV> &sval) {
+                      const std::vector<int32_t> &width, hvec<I> &sidx, hvec<MV> &sval) {
   const int64_t ns = (int64_t)width.size();
   const int64_t slots = sptr[ns];
-  sidx.assign(slots + 256, I(-1));
-  sval.assign(slots + 256, MV(0));
+  par_fill(sidx, slots + 256, I(-1));
+  par_fill(sval, slots + 256, MV(0));
   auto work = [&](int64_t sa, int64_t sb) {
     for (int64_t s = sa; s < sb; ++s) {
       if (width[s] < 0) continue;
@@ -471,10 +521,10 @@ int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, i
 // index per nonzero instead of 4. Returns false (nothing built) otherwise.
 template <typename I>
 static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int32_t> &width,
-                         const std::vector<I> &sidx, std::vector<uint16_t> &sdelta, std::vector<int32_t> &scbase) {
+                         const hvec<I> &sidx, hvec<uint16_t> &sdelta, std::vector<int32_t> &scbase) {
   const int64_t ns = (int64_t)width.size();
   const int64_t slots = sptr[ns];
-  sdelta.assign(slots + 256, 0xFFFF);
+  par_fill(sdelta, slots + 256, (uint16_t)0xFFFF);
   scbase.assign(slots / kSlice + 16, 0);
   std::atomic<bool> ok{true};
   auto work = [&](int64_t sa, int64_t sb) {
@@ -521,8 +571,8 @@ struct DiaHost {
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
   std::vector<int32_t> off;
-  std::vector<uint64_t> mask;
-  std::vector<MV> val;
+  hvec<uint64_t> mask;
+  hvec<MV> val;
   int max_width = 0;
 };
 
@@ -575,8 +625,8 @@ static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t
   if (slots * 4 > sell_slots * 5 + (int64_t)4 * H * d.max_width) return false;
   const int64_t cols = slots / H;
   d.off.assign(cols + kDiaPad, 0);
-  d.mask.assign(2 * (cols + kDiaPad), 0);
-  d.val.assign(slots + 2 * H, MV(0));
+  par_fill(d.mask, 2 * (cols + kDiaPad), (uint64_t)0);
+  par_fill(d.val, slots + 2 * H, MV(0));
   auto pass2 = [&](int64_t sa, int64_t sb) {
     for (int64_t s = sa; s < sb; ++s) {
       const std::vector<int32_t> &o = offs[s];
@@ -611,7 +661,8 @@ static void dia_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int6
                           int32_t *offsets, uint64_t *masks) {
   int64_t ns = 0, sell_slots = 0, irr = 0;
   sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
-  std::vector<double> zeros((size_t)std::max<int64_t>(nnz, 1), 0.0);
+  hvec<double> zeros;
+  par_fill(zeros, (size_t)std::max<int64_t>(nnz, 1), 0.0);
   DiaHost<double> d;
   const bool built = dia_build(n, ip, ix, zeros.data(), sell_slots, d);
   info[0] = built ? 1 : 0;
@@ -633,9 +684,9 @@ template <typename MV>
 struct CbHost {
   int64_t nb = 0, cols = 0, ng = 0;
   std::vector<int64_t> gptr;
-  std::vector<uint16_t> roff;
-  std::vector<int32_t> col;
-  std::vector<MV> val;
+  hvec<uint16_t> roff;
+  hvec<int32_t> col;
+  hvec<MV> val;
 };
 
 template <typename I, typename MV>
@@ -671,7 +722,8 @@ static bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<M
   if (!sorted || nnz == 0 || nfar * 4 < nnz) return false;
   const int64_t ng = (n + kCbRows - 1) / kCbRows;
   // per (block, row) counts -> per (block, group) segment lengths
-  std::vector<uint16_t> roff(nb * n + 256, 0);
+  hvec<uint16_t> roff;
+  par_fill(roff, nb * n + 256, (uint16_t)0);
   std::vector<int64_t> seg(nb * ng, 0);
   std::atomic<bool> fits{true};
   auto pass1 = [&](int64_t g0, int64_t g1) {
@@ -699,8 +751,8 @@ static bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<M
   if (!fits) return false;
   cb.gptr.assign(nb * ng + 1, 0);
   for (int64_t i = 0; i < nb * ng; ++i) cb.gptr[i + 1] = cb.gptr[i] + seg[i];
-  cb.col.assign(nnz + 256, 0);
-  cb.val.assign(nnz + 256, MV(0));
+  par_fill(cb.col, nnz + 256, (int32_t)0);
+  par_fill(cb.val, nnz + 256, MV(0));
   auto pass2 = [&](int64_t g0, int64_t g1) {
     std::vector<int64_t> pos(nb);
     for (int64_t g = g0; g < g1; ++g) {
@@ -734,8 +786,8 @@ struct PairHost {
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
   std::vector<int32_t> cbase;
-  std::vector<uint16_t> delta;
-  std::vector<MV> val;
+  hvec<uint16_t> delta;
+  hvec<MV> val;
   int max_width = 0;
 };
 
@@ -757,8 +809,8 @@ static bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_
   const int64_t slots = p.sptr[ns];
   if (slots == 0 || slots * 4 > sell_slots * 5 + (int64_t)4 * H * p.max_width) return false;
   p.cbase.assign(slots / H + kDiaPad, 0);
-  p.delta.assign(slots + 2 * H, 0xFFFF);
-  p.val.assign(slots + 2 * H, MV(0));
+  par_fill(p.delta, slots + 2 * H, (uint16_t)0xFFFF);
+  par_fill(p.val, slots + 2 * H, MV(0));
   std::atomic<bool> ok{true};
   auto fill = [&](int64_t sa, int64_t sb) {
     for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
@@ -794,6 +846,29 @@ static bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_
   return ok.load();
 }
 
+// Host-only view of the paired-row plan (kry_pair_plan): the image
+// kry_csr_create would build for these CSR arrays when neither the DIA nor the
+// column-blocked image is built, without a device.
+template <typename I>
+static void pair_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
+                           int32_t *cbase, uint16_t *deltas) {
+  int64_t ns = 0, sell_slots = 0, irr = 0;
+  sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
+  hvec<double> zeros;
+  par_fill(zeros, (size_t)std::max<int64_t>(nnz, 1), 0.0);
+  PairHost<double> p;
+  const bool built = pair_build(n, ip, ix, zeros.data(), sell_slots, p);
+  info[0] = built ? 1 : 0;
+  info[1] = built ? (int64_t)p.width.size() : 0;
+  info[2] = built ? p.sptr.back() : 0;
+  info[3] = built ? p.max_width : 0;
+  if (!built) return;
+  if (widths) std::copy(p.width.begin(), p.width.end(), widths);
+  const int64_t slots = p.sptr.back();
+  if (cbase) std::copy(p.cbase.begin(), p.cbase.begin() + slots / kPairSlice, cbase);
+  if (deltas) std::copy(p.delta.begin(), p.delta.begin() + slots, deltas);
+}
+
 namespace {
 // KRY_UPLOAD_TRACE=1: wall-clock split of kry_csr_create's phases, to stderr
 struct UploadTrace {
@@ -825,15 +900,15 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
   A->max_width = 0;
   for (int32_t w : width) A->max_width = std::max(A->max_width, w);
-  std::vector<I> sidx;
-  std::vector<MV> sval;
+  hvec<I> sidx;
+  hvec<MV> sval;
   sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
   tr.mark("SELL-64 plan + fill");
   A->sptr = dev_alloc(sptr.size() * 8);
   A->swidth = dev_alloc(width.size() * 4 + 4);
   // compact image unless disabled (KRY_SELL_COMPACT=0) or impossible
   const char *cenv = getenv("KRY_SELL_COMPACT");
-  std::vector<uint16_t> sdelta;
+  hvec<uint16_t> sdelta;
   std::vector<int32_t> scbase;
   A->compact = sizeof(I) == 4 && !(cenv && atoi(cenv) == 0) && A->nslots > 0 &&
                compact_fill(sptr, width, sidx, sdelta, scbase);
@@ -850,7 +925,10 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
   if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
   KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
-  if (tr.on) KRY_HIP(hipStreamSynchronize(st));
+  KRY_HIP(hipStreamSynchronize(st));
+  release_later(sidx);
+  release_later(sval);
+  release_later(sdelta);
   tr.mark("compact image + H2D");
   // diagonal-offset image for structured single-RHS SpMVs (KRY_SPMV_DIA=0 disables)
   const char *denv = getenv("KRY_SPMV_DIA");
@@ -872,6 +950,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->dia_mask, dh.mask.data(), dh.mask.size() * 8, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->dia_val, dh.val.data(), dh.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
+      release_later(dh.val);
     }
     tr.mark("DIA image + H2D");
   }
@@ -893,6 +972,9 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->cb_col, cb.col.data(), cb.col.size() * 4, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->cb_val, cb.val.data(), cb.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
+      release_later(cb.val);
+      release_later(cb.col);
+      release_later(cb.roff);
     }
     tr.mark("column-blocked image + H2D");
   }
@@ -916,6 +998,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       KRY_HIP(hipMemcpyAsync(A->sp_delta, ph.delta.data(), ph.delta.size() * 2, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->sp_val, ph.val.data(), ph.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
       KRY_HIP(hipStreamSynchronize(st));
+      release_later(ph.val);
+      release_later(ph.delta);
     }
     tr.mark("paired image + H2D");
   }
@@ -954,6 +1038,21 @@ int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices
   else if (itype == KRY_I64)
     dia_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
                   offsets, masks);
+  else
+    throw Error{KRY_EINVAL, "bad itype"};
+  KRY_API_END
+}
+
+int kry_pair_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                  int32_t *widths, int32_t *cbase, uint16_t *deltas) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
+  if (itype == KRY_I32)
+    pair_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, widths,
+                   cbase, deltas);
+  else if (itype == KRY_I64)
+    pair_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
+                   cbase, deltas);
   else
     throw Error{KRY_EINVAL, "bad itype"};
   KRY_API_END

@@ -255,3 +255,90 @@ def test_dia_plan_matches_restatement(case):
     for key in ("widths", "offsets", "masks"):
         np.testing.assert_array_equal(got[key], want[key])
     assert case not in ("unsorted", "scattered")
+
+
+def _pair_plan_py(indptr, indices):
+    """Restatement of the paired-row SELL-128 plan (kry_pair_plan): slices of
+    128 rows, width = the longest row; slot column j holds every row's j-th
+    stored entry (stored order, unsorted rows and duplicates as they are) as
+    column - base, base = the slot column's smallest column, 0xFFFF where the
+    row is shorter; refused when a slot column spans more than 65534
+    columns, or when the slots exceed 1.25x the SELL-64 slots plus one slice
+    of padding."""
+    n = indptr.shape[0] - 1
+    if n == 0 or n >= 2**31:
+        return None
+    ns = (n + 127) // 128
+    lens = np.diff(indptr.astype(np.int64))
+    widths = np.array([lens[128 * s:128 * s + 128].max() for s in range(ns)], dtype=np.int32)
+    maxw = int(widths.max())
+    slots = 128 * int(widths.sum())
+    sell_slots = _layout_py(indptr)[1]
+    if slots == 0 or slots * 4 > sell_slots * 5 + 4 * 128 * maxw:
+        return None
+    cbase, deltas = [], []
+    for s in range(ns):
+        r0, r1 = 128 * s, min(n, 128 * s + 128)
+        for j in range(widths[s]):
+            col = np.full(128, -1, dtype=np.int64)
+            for r in range(r0, r1):
+                if j < lens[r]:
+                    col[r - r0] = indices[indptr[r] + j]
+            have = col >= 0
+            base = int(col[have].min()) if have.any() else 0
+            if have.any() and int(col[have].max()) - base > 65534:
+                return None
+            d = np.where(have, col - base, 0xFFFF).astype(np.uint16)
+            cbase.append(base)
+            deltas.append(d)
+    return {"slices": ns, "slots": slots, "max_width": maxw, "widths": widths,
+            "cbase": np.array(cbase, dtype=np.int32), "deltas": np.concatenate(deltas)}
+
+
+@pytest.mark.parametrize("case", ["banded_holes", "ragged_129", "one_row", "unsorted_dups", "wide_span",
+                                  "uneven", "int64"])
+def test_pair_plan_matches_restatement(case):
+    """The host side of the paired-row image (widths, bases, deltas, and when
+    it is refused) against a NumPy restatement, without a device
+    (kry_pair_plan)."""
+    from krylov_amd import _lib
+
+    itype = np.int32
+    if case == "banded_holes":
+        A = _banded(3000, [-70, -3, -1, 0, 2, 9, 70], 1, drop=0.2)
+    elif case == "ragged_129":
+        A = _banded(129, [-1, 0, 1], 2, drop=0.0)
+    elif case == "one_row":
+        A = scipy.sparse.csr_matrix(np.array([[2.0]]))
+    elif case == "unsorted_dups":
+        rng = np.random.default_rng(5)
+        n = 700
+        lens = rng.integers(0, 9, n)
+        ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        rows = np.repeat(np.arange(n), lens)
+        ix = np.clip(rows + rng.integers(-40, 40, rows.size), 0, n - 1).astype(np.int32)
+        A = scipy.sparse.csr_matrix((np.ones(ix.size), ix, ip), shape=(n, n))
+    elif case == "wide_span":  # one slot column spans 65535 columns: refused
+        n = 70_000
+        A = scipy.sparse.csr_matrix((np.ones(2), ([0, 1], [0, 65535])), shape=(n, n))
+    elif case == "uneven":  # one long row in a slice of short ones: past 1.25x, refused
+        n = 512
+        rows = np.concatenate([np.zeros(400, dtype=int), np.arange(1, n)])
+        cols = np.concatenate([np.arange(400), np.arange(1, n)])
+        A = scipy.sparse.csr_matrix((np.ones(rows.size), (rows, cols)), shape=(n, n))
+    else:
+        A = _banded(1000, [-5, 0, 5], 3, drop=0.1)
+        itype = np.int64
+    ip = A.indptr.astype(itype)
+    ix = A.indices.astype(itype)
+    got = _lib.pair_plan(ip, ix)
+    want = _pair_plan_py(ip, ix)
+    if want is None:
+        assert got is None
+        assert case in ("wide_span", "uneven")
+        return
+    assert got is not None
+    for key in ("slices", "slots", "max_width"):
+        assert got[key] == want[key], key
+    for key in ("widths", "cbase", "deltas"):
+        np.testing.assert_array_equal(got[key], want[key])
