@@ -590,14 +590,22 @@ static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t
     for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
       const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H);
       o.clear();
-      for (int64_t r = r0; r < r1; ++r)
+      for (int64_t r = r0; r < r1; ++r) {
+        // a row whose offsets repeat the previous row's adds nothing new to
+        // the list (stencil rows, away from the grid's faces): checked
+        // against it entry by entry, not pushed
+        const int64_t len = (int64_t)ip[r + 1] - (int64_t)ip[r];
+        bool same = r > r0 && len == (int64_t)ip[r] - (int64_t)ip[r - 1];
         for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
           if (e > ip[r] && ix[e] <= ix[e - 1]) {  // unsorted or duplicate: stored order is not offset order
             ok = false;
             return;
           }
-          o.push_back((int32_t)((int64_t)ix[e] - r));
+          same = same && (int64_t)ix[e] - r == (int64_t)ix[e - len] - (r - 1);
         }
+        if (!same)
+          for (int64_t e = ip[r]; e < ip[r + 1]; ++e) o.push_back((int32_t)((int64_t)ix[e] - r));
+      }
       std::sort(o.begin(), o.end());
       o.erase(std::unique(o.begin(), o.end()), o.end());
       if ((int64_t)o.size() * H > 2 * ((int64_t)ip[r1] - (int64_t)ip[r0]) + 2048) {
