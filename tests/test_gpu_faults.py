@@ -279,3 +279,34 @@ def test_exchange_timeout_is_time_bounded(monkeypatch):
     faulted = timed()
     print(f"\nclean {1e3 * clean:.2f} ms, faulted {1e3 * faulted:.2f} ms (extra {1e3 * (faulted - clean):.2f} ms)")
     assert faulted - clean < 0.1
+
+
+@pytest.mark.parametrize("fault_step", [3, 6, 7])
+def test_cg_update_kernel_dropout_with_deferred_y(monkeypatch, fault_step):
+    """The one-launch update with yk deferred 7 steps (KRY_CG_YDEFER=7): a
+    timed-out exchange at a step before, on and after a flush point leaves
+    the pending updates to the chunk's end flush, which also moves p back
+    into place for the launch-per-pass rerun; the faulted solve equals the
+    clean deferred one to 1e-10 (the rerun's separate passes sum the inner
+    products in another order, as in the per-step fallback test above), and
+    the clean one equals the per-step form bit for bit."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
+    monkeypatch.setenv("KRY_CG_YDEFER", "7")
+    R = problems.poisson2d(300)
+    A = krylov_amd.CsrOperator(R)
+    b = np.random.default_rng(17).standard_normal(R.shape[0])
+    _, clean = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.setenv("KRY_CGU_FAULT", str(fault_step))
+    _, faulted = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    monkeypatch.delenv("KRY_CGU_FAULT")
+    monkeypatch.setenv("KRY_CG_YDEFER", "0")
+    _, plain = krylov_amd.cg(A, b, tol=1e-9, maxiter=500)
+    assert plain.numsteps == clean.numsteps == faulted.numsteps
+    np.testing.assert_array_equal(np.asarray(plain.resnorms).view(np.uint8), np.asarray(clean.resnorms).view(np.uint8))
+    np.testing.assert_array_equal(plain.xk.view(np.uint8), clean.xk.view(np.uint8))
+    f, c = np.asarray(faulted.resnorms), np.asarray(clean.resnorms)
+    np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-10)
+    np.testing.assert_allclose(faulted.xk, clean.xk, rtol=1e-10, atol=1e-12 * np.abs(clean.xk).max())
