@@ -536,6 +536,18 @@ int main(int argc, char **argv) {
     });                                                                                                             \
     check(NAME);                                                                                                    \
   }
+    if (getenv("DIA_BLK_NTV")) {  // value-load policy and shuffles at one slice per wave
+      for (int rep = 0; rep < 2; ++rep) {
+        gr = full;
+        SM(2, 0, "slot-major CPL 2, 1 slice/wave", true);
+        SM(2, 2, "slot-major CPL 2, nt values, 1 slice/wave", true);
+        SM(2, 16, "slot-major CPL 2, shuffled values, 1 slice/wave", true);
+        SM(2, 18, "slot-major CPL 2, shuffled nt values, 1 slice/wave", true);
+        SM(2, 10, "slot-major CPL 2, nt values + diagonal p, 1 slice/wave", true);
+        SM(2, 26, "slot-major CPL 2, shuf nt + diag p, 1 slice/wave", true);
+      }
+      return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
       gr = full;
       SM(2, 0, "slot-major CPL 2, 1 slice/wave", true);
