@@ -248,11 +248,17 @@ int kry_cg_path(kry_cg *s, int32_t *info);
  * kry_cg_run chunk used it; info[1] = chunks whose remaining steps were rerun
  * with separate passes after its exchange timed out (it writes nothing
  * before the exchange completes). KRY_CG_UPD=0 disables it; KRY_CGU_FAULT=t
- * makes the last block drop out at step t of a chunk (tests). info[0] = 2:
- * the last chunk ran the block path (2 <= k <= 8 on the diagonal-offset
- * image) with each step's y / p pass folded into the next step's SpMV
- * (KRY_CG_FUSEP=1 enables it; measured slower, off by default). */
+ * makes the last block drop out at step t of a chunk (tests). */
 int kry_cg_update_path(kry_cg *s, int32_t *info);
+/* Deferred yk updates (yk += alpha p, cg.py:196, applied D steps at a time;
+ * bitwise the per-step updates): *D = the steps per flush this solver uses
+ * (0 = one update per step; decided at the first kry_cg_run), *bytes = the
+ * device memory its D ring buffers of p and the alpha ring hold until
+ * kry_cg_destroy. Default: D = 7 when an n x k vector exceeds 128 MB and
+ * the ring fits an eighth of the device's total memory (3 if only that
+ * fits), else 0; KRY_CG_YDEFER = D overrides; an allocation failure falls
+ * back to D = 0. */
+int kry_cg_defer_info(kry_cg *s, int32_t *D, int64_t *bytes);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);
 int kry_cg_scalars(kry_cg *s, double *out);
@@ -287,6 +293,10 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done,
 int kry_gmres_solution(kry_gmres *s);
 int kry_gmres_residual(kry_gmres *s, double *resnorm);
 int kry_gmres_get(kry_gmres *s, int which, void *host);
+/* xk (after kry_gmres_solution) copied into a device vector of the solver's
+ * shape, on the context stream: restarted GMRES(m) chains x0 = xk of the last
+ * cycle (gmres.py:41-54 called again with x0) without leaving the device. */
+int kry_gmres_xk_device(kry_gmres *s, kry_vec *out);
 /* info[0] = 1 while Arnoldi steps run their MGS passes as one persistent
  * launch (gm_mgsp_kernel), 0 launch per pass (not eligible, or switched off
  * after a timeout); info[1] = chunks finished launch per pass after a
@@ -332,9 +342,16 @@ int kry_minres_get(kry_minres *s, int which, void *host);
 
 /* ---- multi-GPU: RHS columns sharded one block per GPU ----
  * One RCCL communicator per process/GPU. After attaching, each CG iteration
- * performs exactly one ncclAllReduce(sum, f64, count = total_k) on the
+ * performs exactly one ncclAllReduce(sum, f64, count = total_k + 1) on the
  * zero-padded residual-norm vector so every rank applies the reference's
- * global stop rule np.all(resnorms[-1] <= criterion) (cg.py:156). */
+ * global stop rule np.all(resnorms[-1] <= criterion) (cg.py:156).
+ * The last slot of every per-step allreduce (CG, GMRES, MINRES) is a fault
+ * count: a rank whose in-launch exchange timed out at a step (a block that
+ * never became resident) posts a fault there instead of its norms, so EVERY
+ * rank stops the chunk before that step, after the same collectives: the
+ * faulting rank's run returns KRY_EDEVICE, every other rank's KRY_ECOMM, and
+ * no rank blocks in a later allreduce. KRY_COMM_PEER_FAULT=s makes step s of
+ * a run call receive a fault as if a peer had posted it (tests on one GPU). */
 int kry_comm_unique_id(void *id128);
 int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id128,
                     kry_comm **out);
@@ -344,8 +361,9 @@ int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);
 int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k);
 /* GMRES / MINRES: the same sharding (gmres.py:193 and minres.py:162 stop rules,
  * arnoldi.py:187 / 270-272 invariance over all columns): one
- * ncclAllReduce(sum, f64, count = total_k + 1) per step of the zero-padded
- * residual norms plus a count of ranks with a non-invariant column. After
+ * ncclAllReduce(sum, f64, count = total_k + 2) per step of the zero-padded
+ * residual norms, a count of ranks with a non-invariant column and the fault
+ * count. After
  * attaching, set_criterion takes total_k values and each run history row
  * holds total_k values. */
 int kry_gmres_attach_comm(kry_gmres *s, kry_comm *c, int32_t col_offset, int32_t total_k);

@@ -77,6 +77,7 @@ _SIGNATURES = {
     "kry_cg_preferred_chunk": [_vp, _ip32],
     "kry_cg_path": [_vp, _ip32],
     "kry_cg_update_path": [_vp, _ip32],
+    "kry_cg_defer_info": [_vp, _ip32, _ip64],
     "kry_minres_update_path": [_vp, _ip32],
     "kry_cg_residual": [_vp, _dp],
     "kry_cg_get": [_vp, _int, _vp],
@@ -95,6 +96,7 @@ _SIGNATURES = {
     "kry_gmres_solution": [_vp],
     "kry_gmres_residual": [_vp, _dp],
     "kry_gmres_get": [_vp, _int, _vp],
+    "kry_gmres_xk_device": [_vp, _vp],
     "kry_gmres_path": [_vp, _ip32],
     "kry_minres_create": [_vp, _vp, _i32, _int, _pvp],
     "kry_minres_destroy": [_vp],
@@ -275,6 +277,22 @@ def own(obj, destroy, handle, context=False):
     return fin
 
 
+def _release(fin):
+    """Run a finalizer and close its owner: every attribute of the owner that
+    holds the released handle becomes None, so a later call through a live
+    object (a hook that runs after this one, a daemon thread) passes NULL and
+    the library refuses it (KRY_EINVAL, "null argument") instead of touching
+    freed memory."""
+    info = fin.peek()  # (owner, func, args, kwargs), None once it ran
+    fin()
+    if info is None:
+        return
+    owner, handle = info[0], info[2][0]
+    for name, val in list(getattr(owner, "__dict__", {}).items()):
+        if val is handle:
+            setattr(owner, name, None)
+
+
 def _shutdown():
     with _owned_lock:
         owned = list(_owned)
@@ -286,10 +304,10 @@ def _shutdown():
             lib.kry_ctx_synchronize(info[2][0])
     for f, c in reversed(owned):
         if not c:
-            f()
+            _release(f)
     lib.kry_mem_release()
     for f in reversed(ctxs):
-        f()
+        _release(f)
     maps = os.environ.get("KRY_EXIT_MAPS")  # diagnostics: the address map at exit (tools/gpu_exit_bisect.sh)
     if maps:
         with open("/proc/self/maps") as src, open(maps, "w") as dst:

@@ -64,12 +64,18 @@ class _CGState:
 
     def update_path(self):
         """(path, fallbacks) of the launch-per-pass form (kry_cg_update_path):
-        path 1 (== True) = the one-launch update (k = 1), 2 = the block path
-        with the y / p pass folded into the next SpMV, 0 (== False) = separate
-        passes."""
+        path 1 (== True) = the one-launch update (k = 1), 0 (== False) =
+        separate passes."""
         info = (ctypes.c_int32 * 2)()
         check(lib.kry_cg_update_path(self.h, info))
         return int(info[0]), int(info[1])
+
+    def defer_info(self):
+        """(D, bytes): yk updates applied D steps at a time (0 = every step)
+        and the device memory its ring buffers hold (kry_cg_defer_info)."""
+        d, nb = ctypes.c_int32(), ctypes.c_int64()
+        check(lib.kry_cg_defer_info(self.h, ctypes.byref(d), ctypes.byref(nb)))
+        return int(d.value), int(nb.value)
 
     def residual_norm2(self):
         out = np.zeros(self.prob.kpad)

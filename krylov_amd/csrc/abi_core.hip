@@ -414,8 +414,11 @@ __global__ void lartg_kernel(int64_t count, const T *f, const T *g, T *c, T *s, 
 extern "C" {
 
 // 101: kry_csr_info_n (size-checked image info); kry_csr_info back to its
-// version-100 five values. 102: kry_csr_info_n reports the paired-row image
-int kry_version(void) { return 102; }
+// version-100 five values. 102: kry_csr_info_n reports the paired-row image.
+// 103: the per-step allreduces of the sharded solvers carry a fault count
+// (CG total_k + 1, GMRES / MINRES total_k + 2 values); kry_cg_defer_info,
+// kry_gmres_xk_device.
+int kry_version(void) { return 103; }
 
 const char *kry_last_error(void) { return kry::g_last_error.c_str(); }
 

@@ -51,7 +51,7 @@ struct kry_cg {
   // multi-GPU
   kry_comm *comm = nullptr;
   int col_offset = 0, total_k = 0;
-  double *gbuf = nullptr;  // total_k (allreduced residual norms)
+  double *gbuf = nullptr;  // total_k + 1 (allreduced residual norms, fault count)
   double *gcrit = nullptr; // total_k
   // persistent small-n loop (cg_persist_kernel): its scratch r, two p
   // buffers, the y output, the scalar staging slots, barrier and granule
@@ -72,13 +72,6 @@ struct kry_cg {
   int upd_fallbacks = 0;
   bool upd_used = false;  // an update kernel was launched in the current chunk
   bool upd_last = false;  // ... in the last kry_cg_run chunk
-  // block right-hand sides on the DIA image: the y / p pass folded into the
-  // next SpMV (EpiCgApY); p alternates between p and p_alt within a chunk.
-  // fusep = -1 undecided, 0 not used, 1 used
-  void *p_alt = nullptr;
-  int fusep = -1;
-  bool fusep_used = false;  // the current chunk ran it
-  bool fusep_last = false;  // ... the last kry_cg_run chunk
   // block right-hand sides on the separate passes: yk += alpha p (cg.py:196)
   // deferred and applied ydefer steps at a time (cg_pdefer_kernel, then
   // cg_yflush at the chunk's end), p_i in pring[i % (ydefer + 1)] within a
@@ -86,6 +79,7 @@ struct kry_cg {
   int ydefer = -1;
   void *pring[8] = {};
   double *alpha_ring = nullptr;  // ydefer x k: alpha of step j at row j % ydefer
+  int64_t ydefer_bytes = 0;      // what the rings hold (kry_cg_defer_info)
 };
 
 namespace {
@@ -176,41 +170,6 @@ struct OpCgP {
   }
 };
 
-// The end of a chunk of the fused-p block path: the deferred update of the
-// last step that ran, m - 1 (m = min(stop_at, steps) >= 1; the launch is
-// skipped when no step ran): yk += alpha p_{m-1} (cg.py:196) and p_m = r_m +
-// omega p_{m-1} (cg.py:178) into the solver's own p buffer, p_{m-1} being in
-// p0 (m - 1 even) or p1 (odd). Leaves the state a separate y / p pass leaves.
-template <typename V>
-struct OpCgYPFinal {
-  V *y, *p0;
-  const V *p1, *r;
-  const double *alpha, *omega;
-  const Ctrl *ctrl;
-  int steps, k;
-  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
-    constexpr int W = Vec16<V>::W;
-    const int m = ctrl->stop_at < steps ? ctrl->stop_at : steps;
-    const V *src = ((m - 1) & 1) ? p1 : p0;
-    V yv[W], pv[W], rv[W];
-    VIO<V>::load_nt(y, e, N, yv);
-    VIO<V>::load(src, e, N, pv);
-    VIO<V>::load(r, e, N, rv);
-#pragma unroll
-    for (int v = 0; v < W; ++v) {
-      const int c = (int)((e + v) & (k - 1));
-      const V a = (V)alpha[c];
-      const V t1 = a * pv[v];
-      yv[v] = yv[v] + t1;
-      const V om = (V)omega[c];
-      const V t = om * pv[v];
-      pv[v] = rv[v] + t;
-    }
-    VIO<V>::store_nt(y, e, N, yv);
-    VIO<V>::store(p0, e, N, pv);
-  }
-};
-
 // rho0 = <r0, r0> -> rho slot (cg.py:116, 131).
 template <typename S>
 __global__ void cg_start_finalize(const double *part, int P, int k, double *scal) {
@@ -283,7 +242,7 @@ __global__ void cg_rho_kernel(const double *part, int P, int k, double *scal, do
   __syncthreads();
   if (gbuf) {
     // zero-padded residual-norm vector for the RCCL allreduce
-    for (int t = threadIdx.x; t < total_k; t += blockDim.x) {
+    for (int t = threadIdx.x; t <= total_k; t += blockDim.x) {  // + the fault slot (0)
       const int lc = t - col_offset;
       gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
     }
@@ -292,10 +251,12 @@ __global__ void cg_rho_kernel(const double *part, int P, int k, double *scal, do
   if (all_le(rn, scal + S_CRIT * k, k, &flag) && threadIdx.x == 0) ctrl->stop_at = step + 1;
 }
 
-// global stop test on the allreduced residual norms
+// global stop test on the allreduced residual norms (slot total_k: the fault
+// count, post_fault)
 __global__ void cg_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
                                 int step) {
   if (halted(ctrl, step)) return;
+  if (peer_fault(gbuf, total_k + 1, ctrl, step)) return;
   __shared__ int flag;
   for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
   if (all_le(gbuf, gcrit, total_k, &flag) && threadIdx.x == 0) ctrl->stop_at = step + 1;
@@ -363,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
   }
   if (g == 0) {
     if (gbuf) {
-      for (int t = tid; t < total_k; t += kBlock) {
+      for (int t = tid; t <= total_k; t += kBlock) {  // + the fault slot (0)
         const int lc = t - col_offset;
         gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
       }
@@ -459,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
   }
   if (g == 0) {
     if (gbuf) {
-      for (int t = tid; t < total_k; t += kBlock) {
+      for (int t = tid; t <= total_k; t += kBlock) {  // + the fault slot (0)
         const int lc = t - col_offset;
         gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
       }
@@ -646,6 +607,7 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   __syncthreads();
   if (!__builtin_amdgcn_readfirstlane(flag)) {
     if (tid == 0) atomicMin(&ctrl->stop_at, step);
+    if (gbuf && blockIdx.x == 0) post_fault(gbuf, total_k + 1);  // sharded: tell the other ranks
     return;
   }
   const S rrs = (S)shv[0];
@@ -696,7 +658,7 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
     }
     __syncthreads();
     if (gbuf) {
-      for (int t = tid; t < total_k; t += kUpdBlock) gbuf[t] = t == col_offset ? red[0] : 0.0;
+      for (int t = tid; t <= total_k; t += kUpdBlock) gbuf[t] = t == col_offset ? red[0] : 0.0;  // + fault slot
     } else if (all_le(red, scal + S_CRIT, 1, &flag) && tid == 0) {
       ctrl->stop_at = step + 1;
     }
@@ -1252,16 +1214,6 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf, 
   return true;
 }
 
-// Block right-hand sides (2 <= k <= 8) on the diagonal-offset image, no M /
-// Ml: the y / p pass of step s - 1 runs inside the SpMV of step s (SrcCgP +
-// EpiCgApY), so an iteration is SpMV (reads r, p, y; writes p', Ap, y), the
-// alpha kernel, the r pass (r -= alpha Ap, <r, r>) and the one-block rho
-// kernel (omega, history, stop test): 9 vectors per iteration instead of 10,
-// bitwise the same iterates. Measured SLOWER, so off unless KRY_CG_FUSEP=1:
-// on cfg4 (Poisson 3163^2, k = 8) the SpMV that gathers r and p_{s-1} and
-// updates y takes 1.30 ms against 0.44 ms for the plain one, 1.71 against
-// 1.32 ms per iteration (profiles/r03_cfg4_fusep.txt): the doubled x-run
-// traffic through L2 costs far more than the 640 MB pass it saves.
 // alpha = rho / <p, Ap> from the SpMV's PA partial rows (cg_alpha_kernel),
 // through partial_stage_kernel first when there are many; `scratch` (k x
 // kAlphaStage doubles) is free until the r pass writes its partials there.
@@ -1286,74 +1238,6 @@ static void launch_alpha(kry_cg *s, const double *partA, int PA, double *scratch
   KRY_HIP(hipGetLastError());
 }
 
-template <typename V, typename MV, typename I>
-bool fusep_eligible(kry_cg *s) {
-  if (s->fusep < 0) {
-    const char *e = getenv("KRY_CG_FUSEP");
-    constexpr int CPLB = 16 / (int)sizeof(V);
-    s->fusep = ((e && atoi(e) == 1) && sizeof(I) == 4 && s->A->dia && s->k >= CPLB && s->k >= 2 && s->k <= 8 &&
-                !s->M && !s->Ml && !dia_blk_off())
-                   ? 1
-                   : 0;
-    if (s->fusep) {
-      const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * sizeof(V);
-      s->p_alt = dev_alloc(vb);
-    }
-  }
-  return s->fusep == 1;
-}
-
-template <typename V, typename MV, typename I>
-void cg_run_fusep(kry_cg *s, int max_steps) {
-  hipStream_t st = s->ctx->stream;
-  const int k = s->k;
-  const int64_t N = s->n * (int64_t)k;
-  double *partA = s->part, *partB = s->part + part_rows(k) * k;
-  V *P[2] = {static_cast<V *>(s->p), static_cast<V *>(s->p_alt)};
-  V *r = static_cast<V *>(s->r), *y = static_cast<V *>(s->y), *Ap = static_cast<V *>(s->Ap);
-  double *gb = s->comm ? s->gbuf : nullptr;
-  for (int step = 0; step < max_steps; ++step) {
-    int PA, PB;
-    {
-      ProfScope ps(s->ctx, PROF_SPMV);
-      if (step == 0)  // p is the solver's own (the previous chunk ended with its y / p update)
-        launch_spmv<V, MV, I>(s->A, k, SrcPlain<V>{P[0], k}, EpiApDot<V>{Ap, s->w, k}, partA, &PA, s->ctrl, step,
-                              st);
-      else
-        launch_spmv<V, MV, I>(s->A, k, SrcCgP<V>{r, P[(step - 1) & 1], s->scal + S_OMEGA * k, k, 0},
-                              EpiCgApY<V>{Ap, P[step & 1], P[(step - 1) & 1], y, s->scal + S_ALPHA * k, s->w, k},
-                              partA, &PA, s->ctrl, step, st);
-    }
-    launch_alpha(s, partA, PA, partB, step);
-    {
-      ProfScope ps(s->ctx, PROF_UPDATE);
-      PB = launch_elementwise<V>(N, k, OpCgR<V>{r, Ap, s->scal + S_ALPHA * k, s->w, k}, partB, s->ctrl, step, st,
-                                 kCgUpdateGrid);
-    }
-    if (s->scalar_f32)
-      hipLaunchKernelGGL(cg_rho_kernel<float>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist, s->ctrl,
-                         step, gb, s->col_offset, s->total_k);
-    else
-      hipLaunchKernelGGL(cg_rho_kernel<double>, dim3(1), dim3(kBlock), 0, st, partB, PB, k, s->scal, s->hist,
-                         s->ctrl, step, gb, s->col_offset, s->total_k);
-    KRY_HIP(hipGetLastError());
-    if (s->comm) {
-      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k, ncclDouble, ncclSum, s->comm->comm, st);
-      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-      hipLaunchKernelGGL(cg_global_check, dim3(1), dim3(kBlock), 0, st, s->gbuf, s->gcrit, s->total_k, s->hist,
-                         s->ctrl, step);
-      KRY_HIP(hipGetLastError());
-    }
-  }
-  // the deferred y / p update of the last step that ran (none ran: stop_at = 0, skipped)
-  ProfScope ps(s->ctx, PROF_OTHER);
-  launch_elementwise<V>(N, k,
-                        OpCgYPFinal<V>{y, P[0], P[1], r, s->scal + S_ALPHA * k, s->scal + S_OMEGA * k, s->ctrl,
-                                       max_steps, k},
-                        nullptr, s->ctrl, 0, st);
-  s->fusep_used = true;
-}
-
 // Returns true when the chunk ran as one persistent launch.
 template <typename V, typename MV, typename I>
 bool cg_run_impl(kry_cg *s, int max_steps) {
@@ -1361,10 +1245,6 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
   if (cgp_launch<V, MV, I>(s, max_steps)) return true;
-  if (fusep_eligible<V, MV, I>(s)) {
-    cg_run_fusep<V, MV, I>(s, max_steps);
-    return false;
-  }
   double *partA = s->part, *partB = s->part + part_rows(k) * k;
   // deferred yk updates on the block path (KRY_CG_YDEFER = D, 0 = off)
   if (s->ydefer < 0) {
@@ -1377,13 +1257,25 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     // smaller y / p stay cache-resident between the passes, and reading the
     // ring's older p vectors back costs more than the y pass it saves: metric
     // CG, 80 MB vectors, 3,016 -> 2,874 it/s with D = 7; cfg4, 640 MB, 690 ->
-    // 748 it/s), with D ring buffers within a quarter of the free memory
+    // 748 it/s), with the D ring buffers within an eighth of the device's
+    // TOTAL memory (a fixed policy: the path does not depend on what other
+    // allocations happen to leave free); an allocation failure falls back to
+    // one update per step
     const bool big = vb > (size_t(128) << 20);
-    int D = e ? atoi(e) : !big ? 0 : (kCgYDefer * vb <= fr / 4 ? kCgYDefer : (3 * vb <= fr / 4 ? 3 : 0));
+    int D = e ? atoi(e) : !big ? 0 : (kCgYDefer * vb <= tot / 8 ? kCgYDefer : (3 * vb <= tot / 8 ? 3 : 0));
     if (D >= 1 && D <= 7 && k <= 8 && !s->M) {
-      for (int q = 1; q <= D; ++q) s->pring[q] = dev_alloc(vb);
-      s->alpha_ring = static_cast<double *>(dev_alloc((size_t)D * k * 8));
-      s->ydefer = D;
+      try {
+        for (int q = 1; q <= D; ++q) s->pring[q] = dev_alloc(vb);
+        s->alpha_ring = static_cast<double *>(dev_alloc((size_t)D * k * 8));
+        s->ydefer = D;
+        s->ydefer_bytes = (int64_t)D * (int64_t)vb + (int64_t)D * k * 8;
+      } catch (const Error &err) {
+        if (err.code != KRY_ENOMEM) throw;
+        for (int q = 1; q <= D; ++q) {
+          dev_free(s->pring[q]);
+          s->pring[q] = nullptr;
+        }
+      }
     }
   }
   const int D = (!s->M && k <= 8) ? s->ydefer : 0;
@@ -1473,8 +1365,10 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       }
     }
     if (s->comm) {
-      // exactly one collective per iteration: the residual-norm vector
-      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k, ncclDouble, ncclSum, s->comm->comm, st);
+      // exactly one collective per iteration: the residual-norm vector and the
+      // fault count (post_fault)
+      inject_peer_fault(s->gbuf, s->total_k + 1, step, st);
+      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
       KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
       hipLaunchKernelGGL(cg_global_check, dim3(1), dim3(kBlock), 0, st, s->gbuf, s->gcrit, s->total_k, s->hist,
                          s->ctrl, step);
@@ -1526,7 +1420,7 @@ static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
                   s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
                   s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
-                  s->cgp_scal, s->cgp_words, s->upd_words, s->p_alt, s->alpha_ring,
+                  s->cgp_scal, s->cgp_words, s->upd_words, s->alpha_ring,
                   s->pring[1], s->pring[2], s->pring[3], s->pring[4], s->pring[5], s->pring[6], s->pring[7]};
   for (void *b : bufs) dev_free(b);
 }
@@ -1647,7 +1541,6 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     reset_ctrl(s->ctrl, st);
     bool persistent = false;
     s->upd_used = false;
-    s->fusep_used = false;
     dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) {
       persistent = cg_run_impl<decltype(v0), decltype(m0), decltype(i0)>(s, steps);
     });
@@ -1666,15 +1559,19 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     upd = s->upd_used;
   } else if (persistent) {
     cgp_commit(s, done);
+  } else if (s->comm && c.status == KRY_ECOMM) {
+    throw Error{KRY_ECOMM, "CG: another rank's in-launch exchange failed at step " + std::to_string(done) +
+                               " of this run call; every rank stopped before it"};
   } else if (upd && c.status == KRY_EDEVICE && s->comm) {
     // under a communicator every step posts one allreduce on every rank: a
     // rank that reran part of its chunk alone would pair its collectives with
-    // other iterations of the other ranks (wrong global stop decisions, then
-    // a hang), so a timed-out exchange is a hard error here
+    // other iterations of the other ranks, so a timed-out exchange is a hard
+    // error here; the step's allreduce carried the fault to every rank
+    // (post_fault), which all stopped before it
     s->upd_nv = 0;
     ++s->upd_fallbacks;
     throw Error{KRY_EDEVICE, "CG: the one-launch update's exchange timed out at step " + std::to_string(done) +
-                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
+                                 " (a block was not resident); every rank of the communicator stopped before it"};
   } else if (upd && c.status == KRY_EDEVICE) {
     // a one-launch update timed out at step `done` and wrote nothing: the
     // steps before it stand; rerun the rest of the chunk launch per pass,
@@ -1689,7 +1586,6 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   KRY_REQUIRE(c.status == 0, KRY_EDEVICE, "CG: device error status " + std::to_string(c.status));
   s->cgp_last = persistent;
   s->upd_last = upd;
-  s->fusep_last = s->fusep_used;
   s->it += done;
   *steps_done = done;
   KRY_API_END
@@ -1721,8 +1617,16 @@ int kry_cg_path(kry_cg *s, int32_t *info) {
 int kry_cg_update_path(kry_cg *s, int32_t *info) {
   KRY_API_BEGIN
   KRY_REQUIRE(s && info, KRY_EINVAL, "null argument");
-  info[0] = s->upd_last ? 1 : (s->fusep_last ? 2 : 0);
+  info[0] = s->upd_last ? 1 : 0;
   info[1] = s->upd_fallbacks;
+  KRY_API_END
+}
+
+int kry_cg_defer_info(kry_cg *s, int32_t *D, int64_t *bytes) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s && D && bytes, KRY_EINVAL, "null argument");
+  *D = s->ydefer > 0 ? s->ydefer : 0;
+  *bytes = s->ydefer > 0 ? s->ydefer_bytes : 0;
   KRY_API_END
 }
 
@@ -1806,7 +1710,7 @@ int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total
   dev_free(s->gcrit);
   s->gbuf = nullptr;
   s->gcrit = nullptr;
-  s->gbuf = static_cast<double *>(dev_alloc((size_t)total_k * 8));
+  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 1) * 8));  // + the fault count
   s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
   dev_free(s->hist);
   s->hist = nullptr;

@@ -130,69 +130,6 @@ struct SrcPlain {
   }
 };
 
-// p = r + omega * p_old (cg.py:178); first iteration p = r (cg.py:138).
-template <typename V>
-struct SrcCgP {
-  const V *r;
-  const V *pold;
-  const double *omega;
-  int k;
-  int first;
-  __device__ __forceinline__ V operator()(int64_t j, int c) const {
-    const V rj = r[j * k + c];
-    if (first) return rj;
-    const V om = (V)omega[c];
-    const V t = om * pold[j * k + c];
-    return rj + t;
-  }
-  template <int KT>
-  struct Bound {
-    const V *r, *pold;
-    V om[KT];
-    int k, c0, first;
-    __device__ __forceinline__ V operator()(int64_t j, int c) const {
-      const V rj = r[j * k + c0 + c];
-      if (first) return rj;
-      const V t = om[c] * pold[j * k + c0 + c];
-      return rj + t;
-    }
-    __device__ __forceinline__ void pair(int64_t j, V (&o)[2]) const {
-      pload<V>(r + j, o);
-      if (first) return;
-      V q[2];
-      pload<V>(pold + j, q);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const V t = om[0] * q[c];
-        o[c] = o[c] + t;
-      }
-    }
-    __device__ __forceinline__ void row(int64_t j, V (&o)[KT]) const {
-      vload_row<V, KT>(r + j * k + c0, o);
-      if (first) return;
-      V q[KT];
-      vload_row<V, KT>(pold + j * k + c0, q);
-#pragma unroll
-      for (int c = 0; c < KT; ++c) {
-        const V t = om[c] * q[c];
-        o[c] = o[c] + t;
-      }
-    }
-  };
-  template <int KT>
-  __device__ __forceinline__ Bound<KT> bind(int c0) const {
-    Bound<KT> b;
-    b.r = r;
-    b.pold = pold;
-    b.k = k;
-    b.c0 = c0;
-    b.first = first;
-#pragma unroll
-    for (int c = 0; c < KT; ++c) b.om[c] = first ? V(0) : (V)omega[c0 + c];
-    return b;
-  }
-};
-
 // x = w / hsafe (GMRES: the next basis vector V_{k+1} = w / guard(h[k+1]),
 // arnoldi.py:191-196, formed on the fly at every gather of the next SpMV).
 template <typename V>
@@ -403,92 +340,6 @@ struct EpiResidual {
     ri[1] = ri[1] - s[1];
     pstore<V>(r + i, ri);
     return dterm2(w, i, (double)ri[0], (double)ri[0], (double)ri[1], (double)ri[1]);
-  }
-};
-
-// CG: Ap = A p, write p (materialised by SrcCgP), <p, Ap> (cg.py:178-183).
-template <typename V>
-struct EpiCgAp {
-  V *Ap;
-  V *pnew;
-  SrcCgP<V> src;
-  const double *w;
-  int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
-    const V pi = xi;  // p_i, materialised by the bound source at row i
-    pnew[i * k + c] = pi;
-    __builtin_nontemporal_store(s, Ap + i * k + c);  // read once, by the update pass
-    const double pv = (double)pi;
-    return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
-  }
-  template <int C>
-  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
-    vstore_row<V, C>(pnew + i * k + c0, xi);
-    vstore_row<V, C, true>(Ap + i * k + c0, s);
-#pragma unroll
-    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
-  }
-  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
-    pstore<V>(pnew + i, xi);
-    pstore<V, true>(Ap + i, s);
-    return dterm2(w, i, (double)xi[0], (double)s[0], (double)xi[1], (double)s[1]);
-  }
-};
-
-// CG, block right-hand sides with the p pass folded into the next SpMV
-// (cg_run_impl, fused_p): the source materialises p_s = r_s + omega p_{s-1}
-// (SrcCgP, cg.py:178) at every gather; the owner row writes p_s to the other
-// p buffer, stores Ap_s, and applies the previous step's deferred
-// y += alpha_{s-1} p_{s-1} (cg.py:196) to its row. Same operations in the same
-// order as the separate y / p pass: bitwise the same iterates, one pass over
-// y and p (5 vectors) fewer per iteration for one more gathered vector (r).
-template <typename V>
-struct EpiCgApY {
-  V *Ap;
-  V *pnew;
-  const V *pold;
-  V *y;
-  const double *alpha;  // alpha_{s-1}, per column
-  const double *w;
-  int k;
-  __device__ __forceinline__ double operator()(int64_t i, int c, V s, V xi) const {
-    pnew[i * k + c] = xi;
-    __builtin_nontemporal_store(s, Ap + i * k + c);
-    const V t = (V)alpha[c] * pold[i * k + c];
-    y[i * k + c] = y[i * k + c] + t;
-    const double pv = (double)xi;
-    return w ? dterm_w(pv, w[i], (double)s) : dterm(pv, (double)s);
-  }
-  template <int C>
-  __device__ __forceinline__ void row(int64_t i, int c0, const V (&s)[C], const V (&xi)[C], double (&d)[C]) const {
-    vstore_row<V, C>(pnew + i * k + c0, xi);
-    vstore_row<V, C, true>(Ap + i * k + c0, s);
-    V yv[C], po[C];
-    vload_row<V, C>(y + i * k + c0, yv);
-    vload_row<V, C>(pold + i * k + c0, po);
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const V t = (V)alpha[c0 + c] * po[c];
-      yv[c] = yv[c] + t;
-    }
-    vstore_row<V, C, true>(y + i * k + c0, yv);
-#pragma unroll
-    for (int c = 0; c < C; ++c) d[c] += w ? dterm_w((double)xi[c], w[i], (double)s[c]) : dterm((double)xi[c], (double)s[c]);
-  }
-  __device__ __forceinline__ double rows2(int64_t i, const V (&s)[2], const V (&xi)[2]) const {
-    pstore<V>(pnew + i, xi);
-    pstore<V, true>(Ap + i, s);
-    V yv[2], po[2];
-    pload<V>(y + i, yv);
-    pload<V>(pold + i, po);
-    const V a = (V)alpha[0];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const V t = a * po[c];
-      yv[c] = yv[c] + t;
-    }
-    pstore<V, true>(y + i, yv);
-    return dterm2(w, i, (double)xi[0], (double)s[0], (double)xi[1], (double)s[1]);
   }
 };
 

@@ -62,7 +62,7 @@ struct kry_gmres {
   // RHS sharding (kry_gmres_attach_comm): one allreduce per step of the
   // zero-padded residual-norm vector + a non-invariant count, global stop
   kry_comm *comm = nullptr;
-  double *gbuf = nullptr;   // total_k + 1
+  double *gbuf = nullptr;   // total_k + 2 (norms, non-invariant count, fault count)
   double *gcrit = nullptr;  // total_k
   int col_offset = 0, total_k = 0;
   int mgsp_E = -1;  // persistent MGS: -1 undecided, 0 not used, else elements per thread
@@ -796,7 +796,11 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
     py1 = y[(int64_t)(col + 1) * k + c];
     pc0 = h[c];
   }
-  if (halted(ctrl, step)) return;
+  if (halted(ctrl, step)) {
+    // sharded: this step's MGS exchange timed out here, tell the other ranks
+    if (gbuf && local_fault_at(ctrl, step)) post_fault(gbuf, total_k + 2);
+    return;
+  }
   if (!hgiven) reduce_partials(part, P, k, red);  // else h[k+1] is already in h (Householder)
   if (c < k) {
     const S hk1 = hgiven ? (S)h[(int64_t)(col + 1) * k + c] : sqrt((S)red[c]);
@@ -878,7 +882,10 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
       const int lc = t - col_offset;
       gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
     }
-    if (threadIdx.x == 0) gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+    if (threadIdx.x == 0) {
+      gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+      gbuf[total_k + 1] = 0.0;          // the fault count (post_fault)
+    }
     return;
   }
   const bool conv = all_le(rn, scal + G_CRIT * k, k, &flag);
@@ -894,6 +901,7 @@ __global__ void gm_qr_kernel(const double *part, int P, int k, double *scal, dou
 __global__ void gm_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
                                 int step) {
   if (halted(ctrl, step)) return;
+  if (peer_fault(gbuf, total_k + 2, ctrl, step)) return;
   __shared__ int flag;
   for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
   const bool inv = gbuf[total_k] == 0.0;
@@ -1428,7 +1436,8 @@ void gm_qr_step(kry_gmres *s, const double *pin, int P, int col, int step) {
                      s->total_k, s->Hs);
   KRY_HIP(hipGetLastError());
   if (!s->comm) return;
-  ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+  inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
+  ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
   KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
   hipLaunchKernelGGL(gm_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                      (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
@@ -1783,13 +1792,17 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   };
   Ctrl c;
   int done = run_chunk(max_steps, resnorms, &c);
+  if (s->comm && c.status == KRY_ECOMM)
+    throw Error{KRY_ECOMM, "GMRES: another rank's in-launch exchange failed at step " + std::to_string(done) +
+                               " of this run call; every rank stopped before it"};
   if (c.status == KRY_EDEVICE && s->mgsp_E > 0 && s->comm) {
     // one allreduce per step on every rank: no rank may rerun part of a chunk
-    // alone (see kry_cg_run)
+    // alone (see kry_cg_run); the step's allreduce carried the fault to every
+    // rank (post_fault), which all stopped before it
     s->mgsp_E = 0;
     ++s->mgsp_fallbacks;
     throw Error{KRY_EDEVICE, "GMRES: the persistent MGS exchange timed out at step " + std::to_string(done) +
-                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
+                                 " (a block was not resident); every rank of the communicator stopped before it"};
   }
   if (c.status == KRY_EDEVICE && s->mgsp_E > 0) {
     // the persistent MGS kernel timed out at step `done` (a block was not
@@ -1826,6 +1839,18 @@ int kry_gmres_solution(kry_gmres *s) {
   if (c.status == KRY_ESINGULAR) throw Error{KRY_ESINGULAR, "singular matrix: resolution failed at a zero diagonal"};
   if (c.status == KRY_ENONFINITE) throw Error{KRY_ENONFINITE, "array must not contain infs or NaNs"};
   s->have_solution = true;
+  KRY_API_END
+}
+
+// xk (after kry_gmres_solution) into a device vector: the restart chain's
+// next x0 without a round trip through the host (gmres_restarted).
+int kry_gmres_xk_device(kry_gmres *s, kry_vec *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(s, KRY_EINVAL, "null solver");
+  KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
+  check_vec(out, s->n, s->k, s->dtype, "out");
+  KRY_HIP(hipSetDevice(s->ctx->device));
+  KRY_HIP(hipMemcpyAsync(out->d, s->xk, out->bytes(), hipMemcpyDeviceToDevice, s->ctx->stream));
   KRY_API_END
 }
 
@@ -1905,7 +1930,7 @@ int kry_gmres_attach_comm(kry_gmres *s, kry_comm *c, int32_t col_offset, int32_t
   dev_free(s->gcrit);
   s->gbuf = nullptr;
   s->gcrit = nullptr;
-  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 1) * 8));
+  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 2) * 8));  // + non-invariant and fault counts
   s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
   dev_free(s->hist);
   s->hist = nullptr;

@@ -42,7 +42,7 @@ struct kry_minres {
   Ctrl *ctrl = nullptr;
   // RHS sharding (kry_minres_attach_comm), as in GMRES
   kry_comm *comm = nullptr;
-  double *gbuf = nullptr;   // total_k + 1
+  double *gbuf = nullptr;   // total_k + 2 (norms, non-invariant count, fault count)
   double *gcrit = nullptr;  // total_k
   int col_offset = 0, total_k = 0;
   int chunk_cap = 0;
@@ -252,7 +252,10 @@ __global__ void mr_qr_kernel(const double *part, int P, int k, double *scal, int
       const int lc = t - col_offset;
       gbuf[t] = (lc >= 0 && lc < k) ? rn[lc] : 0.0;
     }
-    if (threadIdx.x == 0) gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+    if (threadIdx.x == 0) {
+      gbuf[total_k] = inv ? 0.0 : 1.0;  // ranks with a non-invariant column
+      gbuf[total_k + 1] = 0.0;          // the fault count (post_fault)
+    }
     return;
   }
   const bool conv = all_le(rn, scal + M_CRIT * k, k, &flag);
@@ -378,6 +381,7 @@ __global__ __launch_bounds__(kMrBlock) void mr_upd_kernel(int64_t N, const doubl
   __syncthreads();
   if (!__builtin_amdgcn_readfirstlane(flag)) {
     if (tid == 0) atomicMin(&ctrl->stop_at, step);
+    if (gbuf && blockIdx.x == 0) post_fault(gbuf, total_k + 2);  // sharded: tell the other ranks
     return;
   }
   // mr_qr_kernel's scalar recurrence (minres.py:193-228), same in every block
@@ -453,7 +457,10 @@ __global__ __launch_bounds__(kMrBlock) void mr_upd_kernel(int64_t N, const doubl
     __syncthreads();
     if (gbuf) {
       for (int t = tid; t < total_k; t += kMrBlock) gbuf[t] = t == col_offset ? red[0] : 0.0;
-      if (tid == 0) gbuf[total_k] = inv ? 0.0 : 1.0;
+      if (tid == 0) {
+        gbuf[total_k] = inv ? 0.0 : 1.0;
+        gbuf[total_k + 1] = 0.0;  // the fault count (post_fault)
+      }
     } else {
       const bool conv = all_le(red, scal + M_CRIT, 1, &flag);
       if (tid == 0) {
@@ -474,6 +481,7 @@ void *mru_kern() {
 __global__ void mr_global_check(const double *gbuf, const double *gcrit, int total_k, double *hist, Ctrl *ctrl,
                                 int step) {
   if (halted(ctrl, step)) return;
+  if (peer_fault(gbuf, total_k + 2, ctrl, step)) return;
   __shared__ int flag;
   for (int t = threadIdx.x; t < total_k; t += blockDim.x) hist[(int64_t)step * total_k + t] = gbuf[t];
   const bool inv = gbuf[total_k] == 0.0;
@@ -655,7 +663,8 @@ void mr_run_typed(kry_minres *s, int max_steps) {
     if constexpr (std::is_same<V, double>::value) {
       if (mru_launch(s, w, p, s->W[f], s->W[f ^ 1], pnew, partA, PA, step, i)) {
         if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
-          ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+          inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
+          ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
           KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
           hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                              (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
@@ -675,7 +684,8 @@ void mr_run_typed(kry_minres *s, int max_steps) {
                        s->total_k);
     KRY_HIP(hipGetLastError());
     if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
-      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
+      inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
+      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
       KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
       hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                          (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
@@ -897,13 +907,17 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   Ctrl c;
   int done = run_steps(max_steps, resnorms, &c);
   const bool upd = s->upd_used;
+  if (s->comm && c.status == KRY_ECOMM)
+    throw Error{KRY_ECOMM, "MINRES: another rank's in-launch exchange failed at step " + std::to_string(done) +
+                               " of this run call; every rank stopped before it"};
   if (upd && c.status == KRY_EDEVICE && s->comm) {
     // one allreduce per step on every rank: no rank may rerun part of a chunk
-    // alone (see kry_cg_run)
+    // alone (see kry_cg_run); the step's allreduce carried the fault to every
+    // rank (post_fault), which all stopped before it
     s->upd_nv = 0;
     ++s->upd_fallbacks;
     throw Error{KRY_EDEVICE, "MINRES: the one-launch step tail's exchange timed out at step " + std::to_string(done) +
-                                 " (a block was not resident); under a communicator the rank cannot rerun alone"};
+                                 " (a block was not resident); every rank of the communicator stopped before it"};
   }
   if (upd && c.status == KRY_EDEVICE) {
     // the one-launch step tail timed out at step `done` and wrote nothing:
@@ -986,7 +1000,7 @@ int kry_minres_attach_comm(kry_minres *s, kry_comm *c, int32_t col_offset, int32
   dev_free(s->gcrit);
   s->gbuf = nullptr;
   s->gcrit = nullptr;
-  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 1) * 8));
+  s->gbuf = static_cast<double *>(dev_alloc(((size_t)total_k + 2) * 8));  // + non-invariant and fault counts
   s->gcrit = static_cast<double *>(dev_alloc((size_t)total_k * 8));
   dev_free(s->hist);
   s->hist = nullptr;

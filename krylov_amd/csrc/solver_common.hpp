@@ -271,6 +271,45 @@ __device__ __forceinline__ S safe(S d) {
   return d != S(0) ? d : S(1);
 }
 
+// ------------------------------------------ sharded runs: fault agreement
+// Under a communicator every step posts one allreduce of the global vector on
+// every rank, and its LAST slot is a fault count. A rank whose in-launch
+// exchange timed out at `step` (that kernel left ctrl->stop_at = step and
+// ctrl->status = KRY_EDEVICE, and stored nothing) posts zeros and a fault in
+// place of its norms; every rank's global check of that step sees the count,
+// stops the chunk at `step` (the step does not count) and raises KRY_ECOMM.
+// So every rank leaves the chunk after the same collectives and reports the
+// failure: the healthy ranks never block in the next chunk's allreduce, and
+// none of them reads the faulting rank's stale slots as a step's norms.
+// nslots = the allreduced length (fault slot = nslots - 1). One block.
+__device__ inline void post_fault(double *gbuf, int nslots) {
+  for (int t = threadIdx.x; t < nslots; t += blockDim.x) gbuf[t] = t == nslots - 1 ? 1.0 : 0.0;
+}
+// This rank's step `step` was abandoned by a timed-out exchange (read by the
+// kernel that would have posted the step's norms).
+__device__ inline bool local_fault_at(const Ctrl *ctrl, int step) {
+  return ctrl->stop_at == step && ctrl->status == (int32_t)KRY_EDEVICE;
+}
+// In a global check: a rank posted a fault for this step. Stops the chunk
+// before the step and records KRY_ECOMM (block-uniform answer).
+__device__ inline bool peer_fault(const double *gbuf, int nslots, Ctrl *ctrl, int step) {
+  if (gbuf[nslots - 1] == 0.0) return false;
+  if (threadIdx.x == 0) {
+    ctrl->stop_at = step;
+    if (ctrl->status == 0) ctrl->status = (int32_t)KRY_ECOMM;
+  }
+  return true;
+}
+
+// Test hook for the receiving side on one GPU (a 1-rank communicator has no
+// peer that could fail): KRY_COMM_PEER_FAULT = s makes step s's allreduce
+// carry a fault count, as if another rank had posted one (s counts the steps
+// of a run call, like the other fault switches).
+inline void inject_peer_fault(double *gbuf, int nslots, int step, hipStream_t st) {
+  const char *e = getenv("KRY_COMM_PEER_FAULT");
+  if (e && atoi(e) == step) KRY_HIP(hipMemsetAsync(gbuf + nslots - 1, 0x3f, 8, st));
+}
+
 // Column-wise convergence test np.all(resnorm <= criterion) over `count`
 // columns held in slots[0..count) by the first `count` threads. All threads
 // of the block must call it; returns the same answer in every thread.

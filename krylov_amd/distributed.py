@@ -65,6 +65,22 @@ class ShardComm:
         return cls(rank, world, uid, device=device)
 
     @classmethod
+    def solo(cls, rank, world, device=None):
+        """Rank ``rank`` of ``world`` rehearsed on ONE GPU: a 1-rank RCCL
+        communicator (its allreduce is the identity) with the layout of rank
+        ``rank`` of ``world``. The solvers then attach at column offset
+        ``rank * kpad`` of ``world * kpad`` global slots and run every
+        per-step collective and global check of that rank; the other ranks'
+        slots of each global vector stay exactly 0 (no one posts them), so
+        this rank's slots must equal the unsharded solve of its columns bit
+        for bit. Used to execute the rank > 0 device code without a node."""
+        if not (0 <= int(rank) < int(world)):
+            raise ValueError(f"bad rank {rank} of {world}")
+        c = cls(0, 1, cls.unique_id(), device=device)
+        c.rank, c.world = int(rank), int(world)
+        return c
+
+    @classmethod
     def from_file(cls, path, rank, world, device=None, timeout=120.0):
         """Create the communicator without PyTorch: rank 0 writes the unique id
         to ``path`` (a fresh file name on a file system every rank sees, e.g.

@@ -60,10 +60,13 @@ class _GmresState:
         if prob.has_precond():
             check(lib.kry_gmres_set_preconditioners(h, *prob.op_handles("M", "Ml", "Mr")))
 
-    def start(self):
+    def start(self, x0_dev=None):
+        """r0 = b - A x0 on the device; x0 = the problem's own x0 or, for a
+        restart chain, ``x0_dev`` (a DeviceVector of the solve's shape)."""
         p = self.prob
         out = np.zeros(p.kpad)
-        check(lib.kry_gmres_start(self.h, p.b_dev.handle, p.x0_dev.handle if p.x0_dev else None,
+        x0 = x0_dev if x0_dev is not None else p.x0_dev
+        check(lib.kry_gmres_start(self.h, p.b_dev.handle, x0.handle if x0 is not None else None,
                                   p.w_dev.handle if p.w_dev else None, _lib.dptr(out)))
         return out
 
@@ -93,6 +96,10 @@ class _GmresState:
         out = np.zeros(self.prob.kpad)
         check(lib.kry_gmres_residual(self.h, _lib.dptr(out)))
         return out
+
+    def xk_into(self, vec):
+        """xk (after solution()) into a DeviceVector, device to device."""
+        check(lib.kry_gmres_xk_device(self.h, vec.handle))
 
     def xk(self):
         p = self.prob
@@ -158,17 +165,18 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
 
     ``ortho``: "mgs", "mgsK" (K MGS sweeps) or "householder" (Householder
     Arnoldi, arnoldi.py:33-104, one right-hand side, default inner, no M)."""
-    return _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback)
+    sweeps = _sweeps(ortho, inner, M, b)
+    prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
+    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+    st = _GmresState(prob, maxiter, sweeps)
+    success, xk, k, resnorms = _cycle(prob, st, maxiter, tol, atol, callback)
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=_num_operations(k))
 
 
-def _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback, tol_of_r0=None):
-    """``gmres`` proper. ``tol_of_r0`` (restarts only) maps the device's
-    initial residual norm ``||Ml (b - A x0)||`` to the ``tol`` this call is
-    given, for a caller that chooses ``tol`` from that norm (gmres_restarted):
-    the norm is then read once, not recomputed on the host."""
+def _sweeps(ortho, inner, M, b):
     if ortho.startswith("mgs"):
-        sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
-    elif ortho == "householder":
+        return 1 if len(ortho) == 3 else int(ortho[3:])
+    if ortho == "householder":
         # gmres.py:158-161 and householder.py:19-22: Euclidean inner product,
         # no M, one (quasi-1-D) right-hand side
         assert inner is None, "ortho='householder' needs the default inner product"
@@ -177,40 +185,60 @@ def _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback, tol_
         assert len(bs) == 1 or (len(bs) == 2 and bs[1] == 1), (
             "Householder only works for quasi-1D vectors for now. " f"Input vector has shape {bs}."
         )
-        sweeps = 0
-    else:
-        raise ValueError(f"unknown ortho {ortho!r}")
-    prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
-    maxiter = prob.A.shape[0] if maxiter is None else maxiter
+        return 0
+    raise ValueError(f"unknown ortho {ortho!r}")
 
-    st = _GmresState(prob, maxiter, sweeps)
-    rn0 = st.start()
+
+def _num_operations(k):
+    return {
+        "A": 1 + k,
+        "M": 2 + k,
+        "Ml": 2 + k,
+        "Mr": 1 + k,
+        "inner": 2 + k + k * (k + 1) / 2,
+        "axpy": 4 + 2 * k + k * (k + 1) / 2,
+    }
+
+
+def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_dev=None, host_x=True):
+    """One ``gmres`` call's loop (gmres.py:150-251) on the device state ``st``.
+
+    ``tol_of_r0`` (restarts) maps the device's initial residual norm
+    ``||Ml (b - A x0)||`` to this call's ``tol``, so the norm is read once.
+    ``x_dev`` (restarts): x0 is this DeviceVector instead of the problem's
+    host x0, and the cycle leaves its xk in it (device to device); the host
+    copy of xk is made only if ``host_x`` (else the returned xk is None).
+    Returns ``(success, xk, numsteps, resnorms)``."""
+    rn0 = st.start(x_dev)
     resnorms = [prob.colvals(rn0)]
     if callback is not None:
         # the reference passes Ml_r0 = Ml (b - A x0) here (gmres.py:143-144)
-        callback(prob.x0_or_zeros(), prob.apply_host("Ml", prob.b - prob.A @ prob.x0_or_zeros()))
+        x0h = prob.x0_or_zeros() if x_dev is None else prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
+        callback(x0h, prob.apply_host("Ml", prob.b - prob.A @ x0h))
     if tol_of_r0 is not None:
         tol = tol_of_r0(resnorms[0])
     criterion = np.maximum(tol * resnorms[0], atol)
     st.set_criterion(prob.pad_cols(criterion, np.inf))
 
     steps_done = 0
-    xk = None
+    solved = False  # st holds x0 + V R^-1 y of the steps done so far
     k = 0
     success = False
 
-    def current_x():
-        if steps_done == 0:
+    def solve():
+        nonlocal solved
+        if not solved:
+            st.solution()
+            solved = True
+
+    def host_x0():
+        if x_dev is None:
             return prob.x0_or_zeros()  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
-        st.solution()
-        return st.xk()
+        return prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
 
     while True:
         if np.all(resnorms[-1] <= criterion):
-            if xk is None:
-                xk = current_x()
-            if steps_done == 0:
-                st.solution()
+            solve()  # with no step done this is x0 (the explicit residual's input)
             resnorms[-1] = prob.colvals(np.sqrt(np.asarray(st.residual_norm2()[: prob.kc]).astype(prob.inner_dtype)))
             if np.all(resnorms[-1] <= criterion):
                 success = True
@@ -219,29 +247,26 @@ def _gmres(A, b, M, Ml, Mr, inner, ortho, x0, tol, atol, maxiter, callback, tol_
             break
         steps = 1 if callback is not None else min(_helpers.CHUNK, maxiter - k)
         hist, _ = st.run(steps)
-        xk = None
+        solved = False
         for row in hist:
             resnorms.append(prob.colvals(row))
             k += 1
             steps_done += 1
         if callback is not None and len(hist):
-            xk = current_x()
-            callback(xk, np.array(resnorms[-1]))
+            solve()
+            callback(st.xk(), np.array(resnorms[-1]))
 
-    if xk is None:
-        xk = current_x()
-    num_operations = {
-        "A": 1 + k,
-        "M": 2 + k,
-        "Ml": 2 + k,
-        "Mr": 1 + k,
-        "inner": 2 + k + k * (k + 1) / 2,
-        "axpy": 4 + 2 * k + k * (k + 1) / 2,
-    }
-    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)
+    if steps_done == 0:
+        xk = host_x0() if host_x else None  # x0 itself; x_dev already holds it
+    else:
+        solve()
+        if x_dev is not None:
+            st.xk_into(x_dev)
+        xk = st.xk() if host_x else None
+    return success, xk, k, resnorms
 
 
-def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycles=100, ortho="mgs", M=None,
+def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycles=100, ortho="mgs", *, M=None,
                     Ml=None, Mr=None, inner=None, callback=None):
     """Restarted GMRES(restart): the reference's ``gmres`` (``gmres.py:41-54``,
     no restart parameter of its own) chained through ``x0``, one call of
@@ -253,34 +278,54 @@ def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycle
                   x_{c+1} = info.xk; stop after the first cycle with success
 
     so every cycle's criterion is ``tol * ||b||`` (relative to b, not to the
-    cycle's start) and the run stops when ``||b - A x|| <= tol ||b||``.
-    ``||b - A x_c||`` is the device's own initial residual norm of the cycle
-    (the norm of the Euclidean or ``WeightedInner`` inner product; with Ml,
-    of ``Ml (b - A x_c)``); ``||b||`` is the same norm of b, taken on the host
-    as ``np.linalg.norm`` (default inner) or ``sqrt(inner(b, b))``. The operator
-    is uploaded once.
+    cycle's start: a different ``tol`` meaning from ``gmres``'s) and the run
+    stops when ``||b - A x|| <= tol ||b||``. ``||b - A x_c||`` is the device's
+    own initial residual norm of the cycle (the norm of the Euclidean or
+    ``WeightedInner`` inner product; with Ml, of ``Ml (b - A x_c)``), and
+    ``||b||`` is taken in the same norm (with Ml: ``||Ml b||``), so the
+    criterion compares like with like. The preconditioned chains (M, Ml, Mr)
+    are parity unpinned: the reference's fixtures chain unpreconditioned
+    cycles only (the oracle chaining of tests/test_gpu_solvers.py covers Mr).
 
-    Returns ``(x, infos)``: the last iterate and one ``Info`` per cycle; the
-    chained history is ``sum(info.resnorms for info in infos)``.
+    The chain stays on the device: the operator, b and the solver state are
+    set up once, each cycle starts from the previous cycle's iterate in device
+    memory and leaves its own there, so a cycle moves no vector over PCIe; the
+    final iterate is downloaded once. M, Ml, Mr and inner are keyword-only.
+
+    Returns ``(x, infos)``: the last iterate and one ``Info`` per cycle (the
+    last cycle's ``xk`` is x; earlier cycles' iterates stay on the device, their
+    ``xk`` is None); the chained history is ``sum(info.resnorms for info in
+    infos)``.
     """
+    from .device import DeviceVector
     from .sparse import as_device_operator
 
+    sweeps = _sweeps(ortho, inner, M, b)
     Aop = as_device_operator(A)
     b = np.asarray(b)
+    prob = Problem(Aop, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
+    bn = prob.apply_host("Ml", b)
     if inner is None:
-        bnorm = np.linalg.norm(b, axis=0)
+        bnorm = np.linalg.norm(bn, axis=0)
     else:
-        bnorm = np.sqrt(np.asarray(inner(b, b)).real)
-    x = np.zeros_like(b) if x0 is None else np.asarray(x0)
+        bnorm = np.sqrt(np.asarray(inner(bn, bn)).real)
 
     def tol_of_r0(r0):
         return tol * bnorm / np.maximum(r0, 1e-300)
 
+    st = _GmresState(prob, restart, sweeps)
+    x_dev = DeviceVector(prob.ctx, prob.n, prob.kpad, prob.dtype)
+    x_dev.upload(prob.pad(np.zeros(b.shape, dtype=prob.dtype) if x0 is None else np.asarray(x0)))
     infos = []
-    for _ in range(max_cycles):
-        _, info = _gmres(Aop, b, M, Ml, Mr, inner, ortho, x, tol, atol, restart, callback, tol_of_r0=tol_of_r0)
-        infos.append(info)
-        x = info.xk
-        if info.success:
+    x = None
+    for c in range(max_cycles):
+        last = c == max_cycles - 1
+        success, xk, k, resnorms = _cycle(prob, st, restart, tol, atol, callback, tol_of_r0=tol_of_r0,
+                                          x_dev=x_dev, host_x=last)
+        if success and xk is None:
+            xk = prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
+        infos.append(Info(success, xk, k, resnorms, num_operations=_num_operations(k)))
+        x = xk
+        if success:
             break
     return x, infos

@@ -162,6 +162,35 @@ def shifted_lap3d_weighted(m=200, sigma=0.5, seed=0):
     return A, w
 
 
+def permuted_sym(A, seed=0):
+    """``P A P^T`` for a uniformly random permutation (``default_rng(seed)``):
+    the same nonzeros and values, rows and columns relabelled, so a banded or
+    stencil matrix becomes one with scattered columns (the general-CSR SpMV
+    case). Row i of the result is row p[i] of A with column c renamed
+    pinv[c], sorted (canonical CSR, int32 indices kept)."""
+    n = A.shape[0]
+    p = np.random.default_rng(seed).permutation(n)
+    pinv = np.empty(n, dtype=np.int64)
+    pinv[p] = np.arange(n, dtype=np.int64)
+    ip = A.indptr.astype(np.int64)
+    lens = np.diff(ip)[p]
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    nnz = int(indptr[-1])
+    # source position of every output slot: row p[i]'s entries, in order
+    start = np.repeat(ip[p] - indptr[:-1], lens)
+    src = start + np.arange(nnz, dtype=np.int64)
+    cols = pinv[A.indices[src]]
+    # sort within rows: key = row * n + col (< 2^63 for n < 3e9)
+    rows = np.repeat(np.arange(n, dtype=np.int64), lens)
+    order = np.argsort(rows * n + cols, kind="stable")
+    del rows
+    indices = cols[order].astype(A.indices.dtype)
+    data = A.data[src[order]]
+    it = A.indptr.dtype if nnz < 2**31 else np.int64
+    return scipy.sparse.csr_matrix((data, indices, indptr.astype(it)), shape=A.shape)
+
+
 def diag100(n=100):
     """README / cfg1 problem: ``A = diag([1e-3, 2, ..., n])``, ``b = ones``."""
     return np.diag([1.0e-3] + list(range(2, n + 1))), np.ones(n)

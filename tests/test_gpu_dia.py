@@ -249,59 +249,6 @@ def test_dia_block_cg_matches_lane_group_and_oracle(golden, monkeypatch):
         np.testing.assert_allclose(np.asarray(got.resnorms)[:-1], ref[:-1], rtol=1e-10)
 
 
-@pytest.mark.parametrize("k", [2, 4, 8])
-@pytest.mark.parametrize("case", ["poisson2d_300_f64", "stencil15_24_f64", "lap3d_f32", "poisson_weighted"])
-def test_block_cg_fused_p_pass_bitwise(case, k, monkeypatch):
-    """Block CG with each step's y / p pass folded into the next step's SpMV
-    (cg_run_fusep: SrcCgP + EpiCgApY on the DIA block kernel, the deferred
-    update of a chunk's last step applied by OpCgYPFinal) against the separate
-    passes (KRY_CG_FUSEP=0; the fused form is opt-in, KRY_CG_FUSEP=1, being
-    measured slower): the same operations in the same order, so the
-    history, the iterate and the step count are bitwise equal, including a
-    solve that stops in the middle of a chunk (tol) and chunks of one step."""
-    import krylov_amd
-    from krylov_amd import _helpers, problems
-    from krylov_amd.cg import _CGState
-
-    inner = None
-    if case == "poisson2d_300_f64":
-        A = problems.poisson2d(300)
-    elif case == "stencil15_24_f64":
-        A = problems.stencil15_3d(24)
-    elif case == "lap3d_f32":
-        A, _ = problems.shifted_lap3d_weighted(24)
-        if k < 4:
-            pytest.skip("fp32 block DIA kernel needs k >= 4 (16-byte lanes)")
-    else:
-        A = problems.poisson2d(200)
-        inner = krylov_amd.WeightedInner(np.random.default_rng(4).uniform(1.0, 2.0, A.shape[0]))
-    dt = np.float32 if A.dtype == np.float32 else np.float64
-    B = np.random.default_rng(k).standard_normal((A.shape[0], k)).astype(dt)
-    B[:, -1] *= 1e-2  # columns converge at different steps
-    op = krylov_amd.CsrOperator(A)
-
-    monkeypatch.setenv("KRY_CG_FUSEP", "1")
-
-    def solve():
-        st = _CGState(_helpers.Problem(op, B, None, inner))
-        st.start()
-        st.set_criterion(np.zeros(k))
-        hs = [st.run(n) for n in (1, 7, 32, 1, 19)]
-        return np.concatenate(hs), st.get(0), st.update_path()
-
-    h1, x1, path1 = solve()
-    _, info1 = krylov_amd.cg(op, B, inner=inner, tol=1e-6)
-    monkeypatch.setenv("KRY_CG_FUSEP", "0")
-    h0, x0, path0 = solve()
-    _, info0 = krylov_amd.cg(op, B, inner=inner, tol=1e-6)
-    assert path1[0] == 2 and path0[0] == 0
-    _bits_equal(h1, h0)
-    _bits_equal(x1, x0)
-    assert info1.numsteps == info0.numsteps and info1.success == info0.success
-    _bits_equal(np.asarray(info1.resnorms), np.asarray(info0.resnorms))
-    _bits_equal(info1.xk, info0.xk)
-
-
 @pytest.mark.parametrize("D", [1, 3, 7])
 @pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general"])
 def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):

@@ -1639,13 +1639,6 @@ int main(int argc, char **argv) {
                                        nullptr, nullptr, 0, 0);
     });
     check(nm, d_ap, y2ref);
-    snprintf(nm, 96, "SELL %s fused p-update + SpMV (old CG)", tag);
-    SrcCgP<double> src{d_x, d_x, d_om, 1, 0};
-    report(nm, S + 16.0 * n, [&] {
-      launch_spmv<double, double, int>(M, 1, src, EpiCgAp<double>{d_ap, d_y, src, nullptr, 1}, part, nullptr,
-                                       nullptr, 0, 0);
-    });
-    check(nm, d_ap, y2ref);
   }
 #define PF(UNR, MINW, GRID)                                                                                  \
   {                                                                                                          \
