@@ -113,6 +113,16 @@ int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices
  * padding). Call once with null arrays to size them. */
 int kry_pair_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
                   int32_t *widths, int32_t *cbase, uint16_t *deltas);
+/* Host-only view of the column-blocked plan (no device needed; the image
+ * kry_csr_create builds for single-RHS SpMVs of a matrix with scattered
+ * columns when the diagonal-offset image is not built, kry_version() >= 103):
+ * info[0..3] = built (0 = refused: int64 indices, x under 8 MB, rows not
+ * sorted, fewer than a quarter of the entries more than half a block from the
+ * diagonal, or a segment over 65535 entries), column blocks nb, columns per
+ * block, 256-row groups ng; when built and gptr is non-null: gptr[nb * ng + 1],
+ * the first entry of segment (block b, group g) at gptr[b * ng + g]. */
+int kry_cb_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                int64_t *gptr);
 /* The device image kry_csr_create built, size-checked: writes the first
  * min(len, KRY_CSR_INFO_LEN) of info[0..8] = slices, slots, irregular slices,
  * compact (1 when the column indices are stored as uint16 deltas over

@@ -15,6 +15,12 @@ from .errors import exception_for
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
+# KRYLOV_LIB: load another build of the C-ABI instead, e.g. the host-only
+# sanitizer builds of the image builders (make -C krylov_amd/csrc sanitize;
+# tests/test_host_sanitize.py): entry points it lacks are then left unbound.
+HOST_ONLY = bool(os.environ.get("KRYLOV_LIB"))
+if HOST_ONLY:
+    LIB_PATH = os.environ["KRYLOV_LIB"]
 
 KRY_F32, KRY_F64 = 1, 2
 KRY_I32, KRY_I64 = 1, 2
@@ -59,6 +65,7 @@ _SIGNATURES = {
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
     "kry_dia_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
     "kry_pair_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
+    "kry_cb_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp],
     "kry_csr_info": [_vp, _ip64],
     "kry_csr_info_n": [_vp, _ip64, _i32],
     "kry_vec_create": [_vp, _i64, _i32, _int, _pvp],
@@ -133,11 +140,17 @@ _SIGNATURES = {
 }
 
 for _name, _args in _SIGNATURES.items():
-    _f = getattr(lib, _name)
+    try:
+        _f = getattr(lib, _name)
+    except AttributeError:
+        if HOST_ONLY:
+            continue
+        raise
     _f.argtypes = _args
     _f.restype = _int
-lib.kry_version.argtypes = []
-lib.kry_version.restype = _int
+if not HOST_ONLY:
+    lib.kry_version.argtypes = []
+    lib.kry_version.restype = _int
 lib.kry_last_error.argtypes = []
 lib.kry_last_error.restype = ctypes.c_char_p
 
@@ -243,6 +256,23 @@ def pair_plan(indptr, indices):
             "deltas": deltas}
 
 
+def cb_plan(indptr, indices):
+    """Host-only column-blocked plan (kry_cb_plan): None if the image would
+    not be built, else {"nb", "cols", "ng", "gptr"}."""
+    indptr = np.ascontiguousarray(indptr)
+    indices = np.ascontiguousarray(indices, dtype=indptr.dtype)
+    n, nnz = indptr.shape[0] - 1, indices.shape[0]
+    info = np.zeros(4, dtype=np.int64)
+    ip64 = info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    check(lib.kry_cb_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, None))
+    if not info[0]:
+        return None
+    nb, ng = int(info[1]), int(info[3])
+    gptr = np.zeros(nb * ng + 1, dtype=np.int64)
+    check(lib.kry_cb_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, ptr(gptr)))
+    return {"nb": nb, "cols": int(info[2]), "ng": ng, "gptr": gptr}
+
+
 def csr_layout(indptr):
     """SELL-64 plan of a CSR row pointer: (nslices, nslots, nirregular)."""
     indptr = np.ascontiguousarray(indptr)
@@ -294,6 +324,8 @@ def _release(fin):
 
 
 def _shutdown():
+    if HOST_ONLY:  # a host-only build owns no device objects
+        return
     with _owned_lock:
         owned = list(_owned)
         _owned.clear()

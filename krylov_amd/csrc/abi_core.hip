@@ -10,13 +10,11 @@
 #include <unordered_map>
 
 #include "device.hpp"
+#include "host_image.hpp"
 
 using namespace kry;
 
 namespace kry {
-
-static thread_local std::string g_last_error;
-void set_error(const std::string &msg) { g_last_error = msg; }
 
 // Every device buffer carries kAllocSlack bytes of readable slack before and
 // after it: the diagonal-offset SpMV loads x[j], x[j + 1] as one pair even
@@ -247,110 +245,6 @@ ProfScope::~ProfScope() {
   ctx->ev_used++;
 }
 
-// ------------------------------------------------- host staging buffers
-// Image staging vectors: no zero-initialisation on resize (std::vector's
-// value-initialisation writes every page from one thread), filled in
-// parallel instead, so the first touch of the pages is spread over threads.
-template <class T>
-struct NoInit : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInit<U>;
-  };
-  NoInit() = default;
-  template <class U>
-  NoInit(const NoInit<U> &) {}
-  template <class U, class... A>
-  void construct(U *q, A &&...a) {
-    if constexpr (sizeof...(A) == 0) ::new ((void *)q) U;
-    else ::new ((void *)q) U(std::forward<A>(a)...);
-  }
-};
-template <class T>
-using hvec = std::vector<T, NoInit<T>>;
-
-// A staging vector's pages are returned on a detached thread once its H2D
-// copies have completed (the caller has synchronised the stream): unmapping
-// ~1 GB takes ~0.1 s that kry_csr_create then does not wait for.
-template <class T>
-static void release_later(hvec<T> &v) {
-  if (v.capacity() < (size_t(64) << 20) / sizeof(T)) {
-    hvec<T>().swap(v);
-    return;
-  }
-  auto *h = new hvec<T>();
-  h->swap(v);
-  std::thread([h] { delete h; }).detach();
-}
-
-template <class T>
-static void par_fill(hvec<T> &v, size_t n, T val) {
-  v.resize(n);
-  const unsigned nt = n < (size_t(1) << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (nt == 1) {
-    std::fill(v.begin(), v.end(), val);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t)
-    th.emplace_back([&, t] { std::fill(v.data() + n * t / nt, v.data() + n * (t + 1) / nt, val); });
-  for (auto &x : th) x.join();
-}
-
-// ---------------------------------------------------------- SELL-64 layout
-// Host-side plan: slice s = rows [64 s, 64 s + 64); width = longest row;
-// a slice is irregular (CSR walk) when 64 * width > 2 * nnz_slice + 1024.
-template <typename I>
-static void sell_plan(int64_t n, const I *ip, std::vector<int64_t> *sptr, std::vector<int32_t> *width,
-                      int64_t *nslices, int64_t *nslots, int64_t *nirr) {
-  const int64_t ns = (n + kSlice - 1) / kSlice;
-  if (sptr) sptr->assign(ns + 1, 0);
-  if (width) width->assign(ns, 0);
-  int64_t slots = 0, irr = 0;
-  for (int64_t s = 0; s < ns; ++s) {
-    const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
-    int64_t w = 0;
-    for (int64_t r = r0; r < r1; ++r) w = std::max<int64_t>(w, (int64_t)ip[r + 1] - (int64_t)ip[r]);
-    const int64_t snnz = (int64_t)ip[r1] - (int64_t)ip[r0];
-    const bool irregular = kSlice * w > 2 * snnz + 1024 || w > (int64_t(1) << 30);
-    if (irregular) ++irr;
-    if (width) (*width)[s] = irregular ? -1 : (int32_t)w;
-    if (!irregular) slots += kSlice * w;
-    if (sptr) (*sptr)[s + 1] = slots;
-  }
-  *nslices = ns;
-  *nslots = slots;
-  *nirr = irr;
-}
-
-template <typename I, typename MV>
-static void sell_fill(int64_t n, const I *ip, const I *ix, const MV *dv, const std::vector<int64_t> &sptr,
-                      const std::vector<int32_t> &width, hvec<I> &sidx, hvec<MV> &sval) {
-  const int64_t ns = (int64_t)width.size();
-  const int64_t slots = sptr[ns];
-  par_fill(sidx, slots + 256, I(-1));
-  par_fill(sval, slots + 256, MV(0));
-  auto work = [&](int64_t sa, int64_t sb) {
-    for (int64_t s = sa; s < sb; ++s) {
-      if (width[s] < 0) continue;
-      const int64_t base = sptr[s];
-      const int64_t r0 = s * kSlice, r1 = std::min<int64_t>(n, r0 + kSlice);
-      for (int64_t r = r0; r < r1; ++r) {
-        const int64_t lane = r - r0;
-        int64_t j = 0;
-        for (int64_t e = ip[r]; e < ip[r + 1]; ++e, ++j) {
-          sidx[base + j * kSlice + lane] = ix[e];
-          sval[base + j * kSlice + lane] = dv[e];
-        }
-      }
-    }
-  };
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ns < 4096) nt = 1;
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
-  for (auto &x : th) x.join();
-}
 
 
 template <typename V>
@@ -419,8 +313,6 @@ extern "C" {
 // (CG total_k + 1, GMRES / MINRES total_k + 2 values); kry_cg_defer_info,
 // kry_gmres_xk_device.
 int kry_version(void) { return 103; }
-
-const char *kry_last_error(void) { return kry::g_last_error.c_str(); }
 
 int kry_device_count(int *count) {
   KRY_API_BEGIN
@@ -502,383 +394,7 @@ int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len) {
 
 int kry_csr_info(const kry_csr *A, int64_t *info) { return kry_csr_info_n(A, info, 5); }
 
-int kry_csr_layout(int64_t n, const void *indptr, int itype, int64_t *nslices, int64_t *nslots,
-                   int64_t *nirregular) {
-  KRY_API_BEGIN
-  KRY_REQUIRE(indptr && nslices && nslots && nirregular && n >= 0, KRY_EINVAL, "bad layout arguments");
-  if (itype == KRY_I32)
-    sell_plan(n, static_cast<const int32_t *>(indptr), nullptr, nullptr, nslices, nslots, nirregular);
-  else if (itype == KRY_I64)
-    sell_plan(n, static_cast<const int64_t *>(indptr), nullptr, nullptr, nslices, nslots, nirregular);
-  else
-    throw Error{KRY_EINVAL, "bad itype"};
-  KRY_API_END
-}
-
 }  // extern "C"
-
-// Compact column image: for every slot column (slice s, column j) the base is
-// the smallest column index among its lanes and every lane stores col - base
-// as uint16 (0xFFFF = padding). Possible when each slot column spans at most
-// 65534 columns (banded and stencil matrices); the gathers then read 2 B of
-// index per nonzero instead of 4. Returns false (nothing built) otherwise.
-template <typename I>
-static bool compact_fill(const std::vector<int64_t> &sptr, const std::vector<int32_t> &width,
-                         const hvec<I> &sidx, hvec<uint16_t> &sdelta, std::vector<int32_t> &scbase) {
-  const int64_t ns = (int64_t)width.size();
-  const int64_t slots = sptr[ns];
-  par_fill(sdelta, slots + 256, (uint16_t)0xFFFF);
-  scbase.assign(slots / kSlice + 16, 0);
-  std::atomic<bool> ok{true};
-  auto work = [&](int64_t sa, int64_t sb) {
-    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
-      const int64_t base = sptr[s];
-      for (int64_t j = 0; j < width[s]; ++j) {
-        const I *c = sidx.data() + base + j * kSlice;
-        int64_t mn = INT64_MAX, mx = -1;
-        for (int l = 0; l < kSlice; ++l)
-          if (c[l] >= 0) {
-            mn = std::min<int64_t>(mn, c[l]);
-            mx = std::max<int64_t>(mx, c[l]);
-          }
-        if (mx < 0) mn = 0;
-        if (mx - mn > 65534 || mn > INT32_MAX) {
-          ok = false;
-          return;
-        }
-        scbase[base / kSlice + j] = (int32_t)mn;
-        uint16_t *d = sdelta.data() + base + j * kSlice;
-        for (int l = 0; l < kSlice; ++l)
-          if (c[l] >= 0) d[l] = (uint16_t)(c[l] - mn);
-      }
-    }
-  };
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ns < 4096) nt = 1;
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
-  for (auto &x : th) x.join();
-  return ok.load();
-}
-
-// Diagonal-offset image (see kry_csr::dia_*). Pass 1 collects every slice's
-// sorted offset list (col - row over its entries) and checks that each row is
-// strictly sorted, so a row's entries occur in the slot order of their
-// offsets: the per-row summation order stays the stored order (bitwise
-// csr_matvec). Pass 2 places entry (row, col) in the slot column of offset
-// col - row and sets the row's mask bit. Returns false (nothing built) for
-// unsorted or duplicate entries, or when the image would hold more than
-// 1.25x the SELL image's slots (offsets not shared across the slice's rows).
-template <typename MV>
-struct DiaHost {
-  std::vector<int64_t> sptr;
-  std::vector<int32_t> width;
-  std::vector<int32_t> off;
-  hvec<uint64_t> mask;
-  hvec<MV> val;
-  int max_width = 0;
-};
-
-template <typename I, typename MV>
-static bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, DiaHost<MV> &d) {
-  if (sizeof(I) != 4 || n == 0) return false;
-  constexpr int H = kDiaSlice;
-  const int64_t ns = (n + H - 1) / H;
-  std::vector<std::vector<int32_t>> offs(ns);
-  std::atomic<bool> ok{true};
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ns < 2048) nt = 1;
-  auto pass1 = [&](int64_t sa, int64_t sb) {
-    std::vector<int32_t> o;
-    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
-      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H);
-      o.clear();
-      for (int64_t r = r0; r < r1; ++r) {
-        // a row whose offsets repeat the previous row's adds nothing new to
-        // the list (stencil rows, away from the grid's faces): checked
-        // against it entry by entry, not pushed
-        const int64_t len = (int64_t)ip[r + 1] - (int64_t)ip[r];
-        bool same = r > r0 && len == (int64_t)ip[r] - (int64_t)ip[r - 1];
-        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
-          if (e > ip[r] && ix[e] <= ix[e - 1]) {  // unsorted or duplicate: stored order is not offset order
-            ok = false;
-            return;
-          }
-          same = same && (int64_t)ix[e] - r == (int64_t)ix[e - len] - (r - 1);
-        }
-        if (!same)
-          for (int64_t e = ip[r]; e < ip[r + 1]; ++e) o.push_back((int32_t)((int64_t)ix[e] - r));
-      }
-      std::sort(o.begin(), o.end());
-      o.erase(std::unique(o.begin(), o.end()), o.end());
-      if ((int64_t)o.size() * H > 2 * ((int64_t)ip[r1] - (int64_t)ip[r0]) + 2048) {
-        ok = false;  // offsets not shared across the slice's rows
-        return;
-      }
-      offs[s] = o;
-    }
-  };
-  {
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass1, ns * t / nt, ns * (t + 1) / nt);
-    for (auto &x : th) x.join();
-  }
-  if (!ok) return false;
-  d.sptr.assign(ns + 1, 0);
-  d.width.assign(ns, 0);
-  for (int64_t s = 0; s < ns; ++s) {
-    d.width[s] = (int32_t)offs[s].size();
-    d.max_width = std::max(d.max_width, d.width[s]);
-    d.sptr[s + 1] = d.sptr[s] + (int64_t)H * d.width[s];
-  }
-  const int64_t slots = d.sptr[ns];
-  // the 128-row slices may hold up to one slice more padding than SELL-64's
-  if (slots * 4 > sell_slots * 5 + (int64_t)4 * H * d.max_width) return false;
-  const int64_t cols = slots / H;
-  d.off.assign(cols + kDiaPad, 0);
-  par_fill(d.mask, 2 * (cols + kDiaPad), (uint64_t)0);
-  par_fill(d.val, slots + 2 * H, MV(0));
-  auto pass2 = [&](int64_t sa, int64_t sb) {
-    for (int64_t s = sa; s < sb; ++s) {
-      const std::vector<int32_t> &o = offs[s];
-      const int64_t base = d.sptr[s], c0 = base / H;
-      for (size_t j = 0; j < o.size(); ++j) d.off[c0 + j] = o[j];
-      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H);
-      for (int64_t r = r0; r < r1; ++r) {
-        const int rl = (int)(r - r0);
-        size_t j = 0;
-        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
-          const int32_t off = (int32_t)((int64_t)ix[e] - r);
-          while (o[j] != off) ++j;  // the row's offsets ascend, as the list's do
-          d.mask[2 * (c0 + j) + (rl & 1)] |= uint64_t(1) << (rl >> 1);
-          d.val[base + (int64_t)j * H + rl] = dv[e];
-          ++j;
-        }
-      }
-    }
-  };
-  {
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass2, ns * t / nt, ns * (t + 1) / nt);
-    for (auto &x : th) x.join();
-  }
-  return true;
-}
-
-// Host-only view of the diagonal-offset plan (kry_dia_plan): the image
-// kry_csr_create would build for these CSR arrays, without a device.
-template <typename I>
-static void dia_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
-                          int32_t *offsets, uint64_t *masks) {
-  int64_t ns = 0, sell_slots = 0, irr = 0;
-  sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
-  hvec<double> zeros;
-  par_fill(zeros, (size_t)std::max<int64_t>(nnz, 1), 0.0);
-  DiaHost<double> d;
-  const bool built = dia_build(n, ip, ix, zeros.data(), sell_slots, d);
-  info[0] = built ? 1 : 0;
-  info[1] = built ? (int64_t)d.width.size() : 0;
-  info[2] = built ? d.sptr.back() : 0;
-  info[3] = built ? d.max_width : 0;
-  if (!built) return;
-  if (widths) std::copy(d.width.begin(), d.width.end(), widths);
-  const int64_t cols = d.sptr.back() / kDiaSlice;
-  if (offsets) std::copy(d.off.begin(), d.off.begin() + cols, offsets);
-  if (masks) std::copy(d.mask.begin(), d.mask.begin() + 2 * cols, masks);
-}
-
-// Column-blocked image (see kry_csr::cb_*). Returns false when not useful or
-// not possible: rows not sorted, x small enough to stay cache-resident, the
-// columns not scattered (most entries within half a block of the diagonal),
-// or a segment too long for uint16 offsets.
-template <typename MV>
-struct CbHost {
-  int64_t nb = 0, cols = 0, ng = 0;
-  std::vector<int64_t> gptr;
-  hvec<uint16_t> roff;
-  hvec<int32_t> col;
-  hvec<MV> val;
-};
-
-template <typename I, typename MV>
-static bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<MV> &cb) {
-  if (sizeof(I) != 4 || n * 8 < (int64_t(8) << 20)) return false;
-  const int64_t nnz = (int64_t)ip[n];
-  const char *cenv = getenv("KRY_CB_COLS");  // tuning override: columns per block
-  int64_t cols = cenv ? std::max<int64_t>(1024, atoll(cenv)) : std::max<int64_t>(int64_t(1) << 18, (n + 15) / 16);
-  const int64_t nb = (n + cols - 1) / cols;
-  if (nb < 2) return false;
-  // sorted rows and scattered columns
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  std::vector<int64_t> far(nt, 0);
-  std::atomic<bool> sorted{true};
-  {
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t)
-      th.emplace_back([&, t] {
-        const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
-        int64_t f = 0;
-        for (int64_t r = r0; r < r1; ++r)
-          for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
-            if (e > ip[r] && ix[e] < ix[e - 1]) sorted = false;
-            const int64_t d = (int64_t)ix[e] - r;
-            f += (d > cols / 2 || d < -cols / 2);
-          }
-        far[t] = f;
-      });
-    for (auto &x : th) x.join();
-  }
-  int64_t nfar = 0;
-  for (int64_t f : far) nfar += f;
-  if (!sorted || nnz == 0 || nfar * 4 < nnz) return false;
-  const int64_t ng = (n + kCbRows - 1) / kCbRows;
-  // per (block, row) counts -> per (block, group) segment lengths
-  hvec<uint16_t> roff;
-  par_fill(roff, nb * n + 256, (uint16_t)0);
-  std::vector<int64_t> seg(nb * ng, 0);
-  std::atomic<bool> fits{true};
-  auto pass1 = [&](int64_t g0, int64_t g1) {
-    std::vector<int64_t> cnt(nb);
-    for (int64_t g = g0; g < g1; ++g) {
-      std::fill(cnt.begin(), cnt.end(), 0);
-      const int64_t r0 = g * kCbRows, r1 = std::min<int64_t>(n, r0 + kCbRows);
-      for (int64_t r = r0; r < r1; ++r) {
-        for (int64_t b = 0; b < nb; ++b) {
-          if (cnt[b] > 65535) fits = false;
-          roff[b * n + r] = (uint16_t)cnt[b];
-        }
-        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) cnt[ix[e] / cols]++;
-      }
-      for (int64_t b = 0; b < nb; ++b) {
-        if (cnt[b] > 65535) fits = false;
-        seg[b * ng + g] = cnt[b];
-      }
-    }
-  };
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass1, ng * t / nt, ng * (t + 1) / nt);
-  for (auto &x : th) x.join();
-  th.clear();
-  if (!fits) return false;
-  cb.gptr.assign(nb * ng + 1, 0);
-  for (int64_t i = 0; i < nb * ng; ++i) cb.gptr[i + 1] = cb.gptr[i] + seg[i];
-  par_fill(cb.col, nnz + 256, (int32_t)0);
-  par_fill(cb.val, nnz + 256, MV(0));
-  auto pass2 = [&](int64_t g0, int64_t g1) {
-    std::vector<int64_t> pos(nb);
-    for (int64_t g = g0; g < g1; ++g) {
-      for (int64_t b = 0; b < nb; ++b) pos[b] = cb.gptr[b * ng + g];
-      const int64_t r0 = g * kCbRows, r1 = std::min<int64_t>(n, r0 + kCbRows);
-      for (int64_t r = r0; r < r1; ++r)
-        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
-          const int64_t p = pos[ix[e] / cols]++;
-          cb.col[p] = (int32_t)ix[e];
-          cb.val[p] = dv[e];
-        }
-    }
-  };
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(pass2, ng * t / nt, ng * (t + 1) / nt);
-  for (auto &x : th) x.join();
-  cb.nb = nb;
-  cb.cols = cols;
-  cb.ng = ng;
-  cb.roff = std::move(roff);
-  return true;
-}
-
-// Paired-row SELL-128 image (see kry_csr::sp_*). Pass 1: slice widths (the
-// longest row of each 128 rows); pass 2: per slot column the smallest column
-// as base and every entry's delta and value at row position r - 128 s.
-// Returns false (nothing built) when a slot column spans more than 65534
-// columns, a column does not fit int32, or the image would hold more than
-// 1.25x the SELL-64 image's slots (very uneven rows).
-template <typename MV>
-struct PairHost {
-  std::vector<int64_t> sptr;
-  std::vector<int32_t> width;
-  std::vector<int32_t> cbase;
-  hvec<uint16_t> delta;
-  hvec<MV> val;
-  int max_width = 0;
-};
-
-template <typename I, typename MV>
-static bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, PairHost<MV> &p) {
-  constexpr int H = kPairSlice;
-  if (n == 0 || n >= (int64_t(1) << 31)) return false;
-  const int64_t ns = (n + H - 1) / H;
-  p.width.assign(ns, 0);
-  p.sptr.assign(ns + 1, 0);
-  for (int64_t s = 0; s < ns; ++s) {
-    int64_t w = 0;
-    for (int64_t r = s * H; r < std::min<int64_t>(n, (s + 1) * H); ++r) w = std::max<int64_t>(w, ip[r + 1] - ip[r]);
-    if (w > INT32_MAX / H) return false;
-    p.width[s] = (int32_t)w;
-    p.max_width = std::max(p.max_width, (int)w);
-    p.sptr[s + 1] = p.sptr[s] + H * w;
-  }
-  const int64_t slots = p.sptr[ns];
-  if (slots == 0 || slots * 4 > sell_slots * 5 + (int64_t)4 * H * p.max_width) return false;
-  p.cbase.assign(slots / H + kDiaPad, 0);
-  par_fill(p.delta, slots + 2 * H, (uint16_t)0xFFFF);
-  par_fill(p.val, slots + 2 * H, MV(0));
-  std::atomic<bool> ok{true};
-  auto fill = [&](int64_t sa, int64_t sb) {
-    for (int64_t s = sa; s < sb && ok.load(std::memory_order_relaxed); ++s) {
-      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H), base = p.sptr[s];
-      for (int64_t j = 0; j < p.width[s]; ++j) {
-        int64_t mn = INT64_MAX, mx = -1;
-        for (int64_t r = r0; r < r1; ++r)
-          if ((int64_t)ip[r] + j < (int64_t)ip[r + 1]) {
-            const int64_t c = (int64_t)ix[ip[r] + j];
-            mn = std::min(mn, c);
-            mx = std::max(mx, c);
-          }
-        if (mx < 0) mn = 0;
-        if (mx - mn > 65534 || mn > INT32_MAX) {
-          ok = false;
-          return;
-        }
-        p.cbase[base / H + j] = (int32_t)mn;
-        for (int64_t r = r0; r < r1; ++r)
-          if ((int64_t)ip[r] + j < (int64_t)ip[r + 1]) {
-            const int64_t q = base + j * H + (r - r0);
-            p.delta[q] = (uint16_t)((int64_t)ix[ip[r] + j] - mn);
-            p.val[q] = dv[ip[r] + j];
-          }
-      }
-    }
-  };
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (ns < 2048) nt = 1;
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(fill, ns * t / nt, ns * (t + 1) / nt);
-  for (auto &x : th) x.join();
-  return ok.load();
-}
-
-// Host-only view of the paired-row plan (kry_pair_plan): the image
-// kry_csr_create would build for these CSR arrays when neither the DIA nor the
-// column-blocked image is built, without a device.
-template <typename I>
-static void pair_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
-                           int32_t *cbase, uint16_t *deltas) {
-  int64_t ns = 0, sell_slots = 0, irr = 0;
-  sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
-  hvec<double> zeros;
-  par_fill(zeros, (size_t)std::max<int64_t>(nnz, 1), 0.0);
-  PairHost<double> p;
-  const bool built = pair_build(n, ip, ix, zeros.data(), sell_slots, p);
-  info[0] = built ? 1 : 0;
-  info[1] = built ? (int64_t)p.width.size() : 0;
-  info[2] = built ? p.sptr.back() : 0;
-  info[3] = built ? p.max_width : 0;
-  if (!built) return;
-  if (widths) std::copy(p.width.begin(), p.width.end(), widths);
-  const int64_t slots = p.sptr.back();
-  if (cbase) std::copy(p.cbase.begin(), p.cbase.begin() + slots / kPairSlice, cbase);
-  if (deltas) std::copy(p.delta.begin(), p.delta.begin() + slots, deltas);
-}
 
 namespace {
 // KRY_UPLOAD_TRACE=1: wall-clock split of kry_csr_create's phases, to stderr
@@ -1038,36 +554,6 @@ static void csr_free(kry_csr *A) {
 }
 
 extern "C" {
-
-int kry_dia_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
-                 int32_t *widths, int32_t *offsets, uint64_t *masks) {
-  KRY_API_BEGIN
-  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
-  if (itype == KRY_I32)
-    dia_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, widths,
-                  offsets, masks);
-  else if (itype == KRY_I64)
-    dia_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
-                  offsets, masks);
-  else
-    throw Error{KRY_EINVAL, "bad itype"};
-  KRY_API_END
-}
-
-int kry_pair_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
-                  int32_t *widths, int32_t *cbase, uint16_t *deltas) {
-  KRY_API_BEGIN
-  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
-  if (itype == KRY_I32)
-    pair_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, widths,
-                   cbase, deltas);
-  else if (itype == KRY_I64)
-    pair_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
-                   cbase, deltas);
-  else
-    throw Error{KRY_EINVAL, "bad itype"};
-  KRY_API_END
-}
 
 int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
                    const void *data, int dtype, int itype, kry_csr **out) {

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/krylov_hip.h"
+#include "host_common.hpp"
 
 namespace kry {
 
@@ -21,24 +22,8 @@ constexpr int kMaxGrid = 8192;       // grid cap (and partial-buffer rows)
 constexpr int kMaxGridBlk = 32768;
 inline size_t part_rows(int k) { return k <= 8 ? (size_t)kMaxGridBlk : (size_t)kMaxGrid; }
 constexpr int kMaxCols = 256;        // RHS columns per device (power of two)
-constexpr int kSlice = 64;           // SELL slice height = one wavefront
-// diagonal-offset image (kry_csr::dia_*): slices of kDiaSlice rows, lane l
-// of the wave owns rows 2l and 2l + 1 of its slice
-constexpr int kDiaSlice = 128;
-constexpr int kDiaPad = 32;  // slot-column descriptors past the last one (unconditional reads of a round)
-// paired-row SELL-128 image (kry_csr::sp_*): lane l owns rows 2l, 2l + 1
-constexpr int kPairSlice = 128;
-constexpr int kCbRows = 256;         // rows per column-blocked segment (one per thread)
 constexpr int kCbCap = 1024;         // products staged in LDS per chunk
 constexpr int kNumXcd = 8;
-
-// ---------------------------------------------------------------- errors
-void set_error(const std::string &msg);
-
-struct Error {
-  int code;
-  std::string msg;
-};
 
 #define KRY_HIP(call)                                                          \
   do {                                                                         \
@@ -46,11 +31,6 @@ struct Error {
     if (e_ != hipSuccess)                                                      \
       throw ::kry::Error{e_ == hipErrorOutOfMemory ? KRY_ENOMEM : KRY_EDEVICE, \
                          std::string(#call) + ": " + hipGetErrorString(e_)};   \
-  } while (0)
-
-#define KRY_REQUIRE(cond, code, msg)                                           \
-  do {                                                                         \
-    if (!(cond)) throw ::kry::Error{(code), (msg)};                            \
   } while (0)
 
 // ------------------------------------------------------------- scalars

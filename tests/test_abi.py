@@ -342,3 +342,101 @@ def test_pair_plan_matches_restatement(case):
         assert got[key] == want[key], key
     for key in ("widths", "cbase", "deltas"):
         np.testing.assert_array_equal(got[key], want[key])
+
+
+def _cb_plan_py(indptr, indices):
+    """Restatement of the column-blocked plan (kry_cb_plan): int32 indices;
+    x over 8 MB (n >= 2^20); columns cut into blocks of max(2^18, ceil(n / 16))
+    columns (at least 2 blocks); refused unless every row is sorted and at
+    least a quarter of the entries lie more than half a block from the
+    diagonal; segment (block b, 256-row group g) holds the group's entries in
+    block b, in row order, its start at gptr[b * ng + g]; a segment over 65535
+    entries refuses the image."""
+    n = indptr.shape[0] - 1
+    if indptr.dtype != np.int32 or n * 8 < (8 << 20):
+        return None
+    cols = max(1 << 18, (n + 15) // 16)
+    nb = (n + cols - 1) // cols
+    if nb < 2:
+        return None
+    ip = indptr.astype(np.int64)
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(ip))
+    ix = indices.astype(np.int64)
+    same_row = rows[1:] == rows[:-1]
+    if np.any(same_row & (ix[1:] < ix[:-1])):
+        return None
+    d = ix - rows
+    if ix.size == 0 or 4 * int(np.count_nonzero((d > cols // 2) | (d < -(cols // 2)))) < ix.size:
+        return None
+    ng = (n + 255) // 256
+    cnt = np.bincount((ix // cols) * ng + rows // 256, minlength=nb * ng)
+    if cnt.max() > 65535:
+        return None
+    gptr = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    return {"nb": nb, "cols": cols, "ng": ng, "gptr": gptr}
+
+
+@pytest.mark.parametrize("case", ["scattered", "scattered_wide", "stencil", "unsorted", "small", "int64"])
+def test_cb_plan_matches_restatement(case):
+    """The host side of the column-blocked image (column blocks, segment
+    pointers, and when it is refused) against a NumPy restatement, without a
+    device (kry_cb_plan). Sizes are past the builder's threading thresholds,
+    so the sanitizer runs (tests/test_host_sanitize.py) see its threads."""
+    from krylov_amd import _lib, problems
+
+    n = 1_100_000
+    if case in ("scattered", "unsorted", "int64"):
+        A = problems.random_nonsym(n, per_row=5, seed=4)
+    elif case == "scattered_wide":
+        A = problems.random_nonsym(4_500_000, per_row=3, seed=5)
+    elif case == "stencil":
+        A = problems.poisson2d(1100)  # columns near the diagonal: refused
+    else:
+        A = problems.random_nonsym(200_000, per_row=5, seed=6)  # x fits the caches: refused
+    ip, ix = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+    if case == "unsorted":
+        ix = ix.copy()
+        a = ip[1234]
+        ix[a], ix[a + 1] = ix[a + 1], ix[a]
+    if case == "int64":
+        ip, ix = ip.astype(np.int64), ix.astype(np.int64)
+    got = _lib.cb_plan(ip, ix)
+    want = _cb_plan_py(ip, ix)
+    if want is None:
+        assert got is None
+        assert case in ("stencil", "unsorted", "small", "int64")
+        return
+    assert got is not None and case.startswith("scattered")
+    for key in ("nb", "cols", "ng"):
+        assert got[key] == want[key], key
+    np.testing.assert_array_equal(got["gptr"], want["gptr"])
+
+
+def test_plans_of_large_matrices_match():
+    """The threaded paths of the plan builders (more than 2048 slices): the
+    DIA plan of a 600^2 Poisson matrix against the restatement, and the
+    paired plan of a banded 300k-row matrix checked entry by entry (each
+    slot's base + delta is the stored column)."""
+    from krylov_amd import _lib, problems
+
+    A = problems.poisson2d(600)
+    got = _lib.dia_plan(A.indptr, A.indices)
+    want = _dia_plan_py(A.indptr, A.indices)
+    assert got is not None and want is not None
+    for key in ("slices", "slots", "max_width"):
+        assert got[key] == want[key], key
+    for key in ("widths", "offsets", "masks"):
+        np.testing.assert_array_equal(got[key], want[key])
+    B = _banded(300_000, [-700, -3, 0, 2, 9, 700], 7, drop=0.15)
+    p = _lib.pair_plan(B.indptr, B.indices)
+    assert p is not None
+    ip = B.indptr.astype(np.int64)
+    lens = np.diff(ip)
+    ns = (B.shape[0] + 127) // 128
+    np.testing.assert_array_equal(p["widths"], [lens[128 * s:128 * s + 128].max() for s in range(ns)])
+    sptr = np.concatenate([[0], 128 * np.cumsum(p["widths"].astype(np.int64))])
+    rows = np.repeat(np.arange(B.shape[0]), lens)
+    j = np.arange(B.nnz) - ip[rows]  # position in the row
+    slot = sptr[rows // 128] + 128 * j + rows % 128
+    np.testing.assert_array_equal(p["cbase"][slot // 128].astype(np.int64) + p["deltas"][slot], B.indices)
+    assert np.count_nonzero(p["deltas"] != 0xFFFF) == B.nnz

@@ -434,6 +434,133 @@ __global__ __launch_bounds__(256) void dia_shift(const int64_t *__restrict__ spt
   if (tid < K) part[(int64_t)g * K + tid] = red[tid];
 }
 
+// LDS window (round 4): the slot columns whose offsets lie within +-kNear of
+// the diagonal (Poisson: -1, 0, +1) read x from ONE window of the slice's x
+// rows [128 s + lo, 128 s + hi + 128), staged in LDS by global_load_lds (16 B
+// per lane, 1 KB per instruction) instead of three overlapping 1 KB runs per
+// row group through L1; the epilogue's p comes from the same window. MODE bit
+// 1: the slice's values staged in LDS too (one 1 KB DMA per slot column, then
+// ds_read_b64 per row group) instead of 8-B loads replicated over a row's
+// lanes. Far columns (+-m) load straight to registers as before. One slice per
+// wave. Bitwise the library kernel (same products, same order).
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+constexpr int kNear = 4;
+constexpr int kWinB = (128 + 2 * kNear) * 64;
+constexpr int kValMax = 8;
+template <int MODE>
+__global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                               const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                               const double *__restrict__ val, int64_t nslices, int64_t n,
+                                               const double *__restrict__ x, double *__restrict__ y,
+                                               double *__restrict__ part) {
+  constexpr int CPL = 2, LPR = K / CPL, RPG = 64 / LPR, NG = kDiaSlice / RPG;
+  constexpr bool VL = (MODE & 1) != 0;
+  constexpr int PERW = kWinB + (VL ? kValMax * 1024 : 0);
+  __shared__ __attribute__((aligned(16))) char lds[4 * PERW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
+  char *my = lds + wid * PERW;
+  const int64_t s = (int64_t)g * 4 + wid;
+  double dacc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
+  if (s < nslices) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s], cb = base / kDiaSlice;
+    int lo = 1 << 30, hi = -(1 << 30);
+    for (int j = 0; j < w; ++j) {
+      const int o = doff[cb + j];
+      if (o >= -kNear && o <= kNear) {
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+      }
+    }
+    const bool win = lo <= hi;
+    const int64_t r0 = s * kDiaSlice;
+    const int64_t nx = n * K;
+    if (win) {
+      const int nb = (hi - lo + kDiaSlice) * K * 8;
+      const int64_t e0 = (r0 + lo) * K;
+      for (int i = 0; i * 1024 < nb; ++i) {
+        int64_t e = e0 + (i * 1024 + lane * 16) / 8;
+        e = e < 0 ? 0 : (e > nx - 2 ? nx - 2 : e);  // rows outside x: holes, never added
+        __builtin_amdgcn_global_load_lds((glb_void *)(x + e), (lds_void *)(my + i * 1024), 16, 0, 0);
+      }
+    }
+    const bool vl = VL && w <= kValMax;
+    if (vl)
+      for (int j = 0; j < w; ++j)
+        __builtin_amdgcn_global_load_lds((glb_void *)(val + base + (int64_t)j * kDiaSlice + 2 * lane),
+                                         (lds_void *)(my + kWinB + j * 1024), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double acc[NG][CPL];
+#pragma unroll
+    for (int r = 0; r < NG; ++r)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[r][c] = 0.0;
+    for (int j = 0; j < w; ++j) {
+      const int off = doff[cb + j];
+      const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+      const bool near = win && off >= lo && off <= hi;
+      double a[NG], xv[NG][CPL];
+      bool on[NG];
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        on[r] = (((rl & 1) ? m1 : m0) >> (rl >> 1) & 1u) != 0;
+        a[r] = vl ? *reinterpret_cast<const double *>(my + kWinB + j * 1024 + rl * 8)
+                  : val[base + (int64_t)j * kDiaSlice + rl];
+        if (near) {
+          const d2v v = *reinterpret_cast<const d2v *>(my + (rl + off - lo) * K * 8 + c0 * 8);
+          xv[r][0] = v.x;
+          xv[r][1] = v.y;
+        } else {
+          ldx<CPL>(x + (on[r] ? r0 + rl + off : 0) * K + c0, xv[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NG; ++r)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const double p = a[r] * xv[r][c];
+          const double t = acc[r][c] + p;
+          acc[r][c] = on[r] ? t : acc[r][c];
+        }
+    }
+    const bool pin = win && lo <= 0 && hi >= 0;
+#pragma unroll
+    for (int r = 0; r < NG; ++r) {
+      const int rl = r * RPG + rl0;
+      const int64_t row = r0 + rl;
+      if (row < n) {
+        double q[CPL];
+        if (pin) {
+          const d2v v = *reinterpret_cast<const d2v *>(my + (rl - lo) * K * 8 + c0 * 8);
+          q[0] = v.x;
+          q[1] = v.y;
+        } else {
+          ldx<CPL>(x + row * K + c0, q);
+        }
+        d2v o;
+        o.x = acc[r][0];
+        o.y = acc[r][1];
+        __builtin_nontemporal_store(o, reinterpret_cast<d2v *>(y + row * K + c0));
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) dacc[c] += dterm(q[c], acc[r][c]);
+      }
+    }
+  }
+  __syncthreads();  // every wave is done with its window: the LDS serves the reduction
+  double *red = reinterpret_cast<double *>(lds);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) red[tid * CPL + c] = dacc[c];
+  block_tree_reduce(red, 256 * CPL, K);
+  if (tid < K) part[(int64_t)g * K + tid] = red[tid];
+}
+
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 3163;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -524,6 +651,25 @@ int main(int argc, char **argv) {
     });                                                                                                           \
     if (CHECK) check(nm);                                                                                         \
   }
+  if (getenv("DIA_BLK_LDS")) {  // round 4: the near-diagonal x window (and values) through LDS
+    const int full = (int)((A->dia_nslices + 3) / 4);
+    if (full > 65536) return 1;
+#define LD(MODE, NAME)                                                                                              \
+  {                                                                                                                 \
+    timeit(NAME, [&] {                                                                                              \
+      hipLaunchKernelGGL((dia_lds<MODE>), dim3(full), dim3(256), 0, st, (const int64_t *)A->dia_sptr,               \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,        \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);               \
+    });                                                                                                             \
+    check(NAME);                                                                                                    \
+  }
+    for (int rep = 0; rep < 2; ++rep) {
+      gr = full;
+      SM(2, 0, "slot-major CPL 2, 1 slice/wave", true);
+      LD(0, "LDS window (near x), values direct");
+      LD(1, "LDS window (near x) + LDS values");
+    }
+  } else
   if (getenv("DIA_BLK_SHIFT")) {  // shifted-window variants against the slot-major kernel
     const int full = (int)((A->dia_nslices + 3) / 4);
     if (full > 65536) return 1;
