@@ -54,14 +54,69 @@ def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
     return nnz * (mvb + ib) + (n + 1) * ib + 2 * n * k * vb
 
 
-def cg_iteration_bytes(n, nnz, k=1, vb=8, ib=4):
-    """SpMV + fused x/r/rho pass (6 vectors) + p pass (3)."""
-    return spmv_S(n, nnz, k, vb, ib) + 9 * n * k * vb
+def image_bytes_k1(layout, n, nnz, vectors=2):
+    """Bytes a k = 1 SpMV must move on the image launch_spmv picks:
+    (kernel, bytes, formula). `vectors` n-vectors of 8 B beside the matrix
+    (2: x read, y written; GMRES's epilogue also reads V_0: 3)."""
+    v = vectors * n * 8
+    vt = f"{vectors}*n*8"
+    if layout["dia"]:
+        ds = layout["dia_slots"]
+        return ("spmv_dia_kernel", ds * 8 + ds / 128 * 20 + v,
+                f"dia_slots*8 + dia_slots/128*20 + {vt}")
+    if layout.get("col_blocks", 0):
+        nb = layout["col_blocks"]
+        ng = (n + 255) // 256
+        multi = ng > 1024 * 16  # launch_spmv: one launch per column block past 16 groups per block
+        kname = "spmv_cb_kernel (one launch per column block)" if multi else "spmv_cbp_kernel"
+        extra = 2 * (nb - 1) * n * 8 if multi else 0
+        return (kname, nnz * (4 + 8) + nb * n * 2 + (nb * ng + 1) * 8 + v + extra,
+                f"nnz*(4+8) (column + value) + col_blocks*n*2 (row offsets) + (col_blocks*ng+1)*8 (segment "
+                f"pointers) + {vt}" + (" + 2*(col_blocks-1)*n*8 (running sums between launches)" if multi else ""))
+    if layout.get("pair"):
+        ps = layout["pair_slots"]
+        return ("spmv_pair_kernel", ps * (8 + 2) + ps / 128 * 4 + (n + 127) // 128 * 12 + v,
+                f"pair_slots*(8+2) + pair_slots/128*4 + slices*12 + {vt}")
+    slots, slices = layout["slots"], layout["slices"]
+    if layout["compact"]:
+        return ("spmv_sell_kernel (compact)", slots * (8 + 2) + slots / 64 * 4 + slices * 12 + v,
+                f"slots*(8+2) + slots/64*4 + slices*12 + {vt}")
+    return ("spmv_sell_kernel", slots * (8 + 4) + slices * 12 + v, f"slots*(8+4) + slices*12 + {vt}")
 
 
-def gmres_cycle_bytes(n, nnz, m=30, vb=8, ib=4):
-    """Per m-step cycle: (m + 1) S + (1950 + 37) n vb."""
-    return (m + 1) * spmv_S(n, nnz) + (1950 + 37) * n * vb
+def hbm_roofline(kernel, bytes_per_launch, seconds_per_launch, formula, launches, traffic=None, **extra):
+    """A roofline object: algorithmic bytes per launch over the measured
+    average launch time, against the 8 TB/s HBM3E spec."""
+    gbs = bytes_per_launch / seconds_per_launch / 1e9
+    out = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+           "traffic": traffic, "kernel": kernel, "ms_per_launch": 1e3 * seconds_per_launch,
+           "bytes_per_launch": bytes_per_launch, "bytes_formula": formula, "launches_timed": launches,
+           "timing": "HIP events on the solver stream around every launch of a pass after the timed region"}
+    out.update(extra)
+    return out
+
+
+def profiled(ctx, ids, fn):
+    """Run fn() with HIP-event timing of every launch of the kernel ids in
+    `ids` (ProfScope, krylov_amd/csrc); returns {id: (launches, ms)}."""
+    ctx.synchronize()
+    ctx.profile(True, kernels=list(ids), every=1)
+    try:
+        fn()
+        ctx.synchronize()
+        return {i: ctx.profile_read(i) for i in ids}
+    finally:
+        ctx.profile(False)
+
+
+def gather_ceiling(label):
+    """The measured random-gather ceiling for a column-blocked image
+    (profiles/<GATHER_CEILING>, tools/gather_ceiling.py), if present."""
+    try:
+        with open(os.path.join(REPO, "profiles", GATHER_CEILING)) as f:
+            return json.load(f).get(label)
+    except OSError:
+        return None
 
 
 def dist_setup():
@@ -119,7 +174,7 @@ def _iterate(st, k, ncols, chunk=32):
         done += s
 
 
-def run_cg_bench(A_host, B, steps, warmup, world, rank, local, pg, roofline_launches=64):
+def run_cg_bench(A_host, B, steps, warmup, world, rank, local, pg, roofline_launches=64, prof_ids=None):
     """CG on this rank's RHS block B (n or n x k) of A: warmup, then EXACTLY
     `steps` iterations between barrier + device sync on both sides (max over
     ranks), then a separate pass of max(steps, roofline_launches) iterations
@@ -143,17 +198,17 @@ def run_cg_bench(A_host, B, steps, warmup, world, rank, local, pg, roofline_laun
     t1 = time.perf_counter()
     barrier(pg)
     elapsed = allmax(pg, t1 - t0)
-    ctx.profile(True, kernels=[_lib.PROF_SPMV], every=1)
-    _iterate(st, max(steps, roofline_launches), ncols, chunk)
-    ctx.synchronize()
-    cnt, spmv_ms = ctx.profile_read(_lib.PROF_SPMV)
-    ctx.profile(False)
+    ids = [_lib.PROF_SPMV] + [i for i in (prof_ids or []) if i != _lib.PROF_SPMV]
+    prof = profiled(ctx, ids, lambda: _iterate(st, max(steps, roofline_launches), ncols, chunk))
+    cnt, spmv_ms = prof[_lib.PROF_SPMV]
+    defer = st.defer_info()
     del st
     if comm is not None:
         comm.close()
     layout = A.layout()
     return {"elapsed": elapsed, "spmv_count": cnt, "spmv_avg_s": spmv_ms / max(cnt, 1) / 1e3, "n": A.n,
-            "nnz": A.nnz, "layout": layout, "rhs": ncols // world, "persistent_loop": chunk == 256}
+            "nnz": A.nnz, "layout": layout, "rhs": ncols // world, "persistent_loop": chunk == 256, "prof": prof,
+            "prof_iters": max(steps, roofline_launches), "ydefer": defer}
 
 
 def spmv_kernel_desc(layout, n):
@@ -204,6 +259,7 @@ def roofline_of(res, n, nnz, traffic=None):
         "traffic_source": traffic.get("source"),
         "kernel": kname,
         "spmv_ms": 1e3 * t,
+        "ms_per_launch": 1e3 * t,
         "bytes_per_launch": image_bytes,
         "bytes_formula": formula,
         "launches_timed": res["spmv_count"],
@@ -214,6 +270,34 @@ def roofline_of(res, n, nnz, traffic=None):
         "csr_S_formula": "S = nnz*(8+4) + (n+1)*4 + 2*n*8 (SURVEY §8(d), the int32-CSR algorithmic bytes: an "
                          "effective rate, not HBM traffic, for an image that moves fewer bytes)",
     }
+
+
+def cfg4_rooflines(res, steps):
+    """Block CG (k columns, DIA image): the block SpMV's roofline and the
+    iteration's, on the bytes the kernels must move: SpMV (values, the
+    per-slot-column descriptors, p read, Ap written), the r pass (r, Ap in;
+    r out), the p pass (r, p_i in; p_{i+1} out) and, with yk deferred D steps,
+    once per D steps y in and out and the D older p vectors in (D = 0: the
+    fused y / p pass, r, y, p in and y, p out)."""
+    from krylov_amd import _lib
+
+    n, k = res["n"], res["rhs"]
+    lay = res["layout"]
+    vec = n * k * 8
+    ds = lay["dia_slots"]
+    sb = ds * 8 + ds / 128 * 20 + 2 * vec
+    cnt, ms = res["prof"][_lib.PROF_SPMV]
+    spmv = hbm_roofline("spmv_dia_blk_kernel<double,double,2,8,SrcPlain,EpiApDot> (block DIA SpMV, k = %d)" % k,
+                        sb, ms / max(cnt, 1) / 1e3,
+                        "dia_slots*8 + dia_slots/128*20 + 2*n*k*8 (values, descriptors, p read, Ap written)", cnt)
+    D = res["ydefer"][0]
+    pass_b = 3 * vec + 3 * vec + ((D + 2) / D * vec if D else 2 * vec)
+    it_b = sb + pass_b
+    t_it = res["elapsed"] / steps
+    return spmv, {"bound": "hbm", "achieved": it_b / t_it / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": it_b / t_it / 1e9 / HBM_PEAK_GBS, "bytes_per_iteration": it_b, "ydefer": D,
+                  "bytes_formula": "SpMV (above) + 3*n*k*8 (r pass) + 3*n*k*8 (p pass) + "
+                                   + ("(D+2)/D*n*k*8 (yk flush every D steps)" if D else "2*n*k*8 (y in the y/p pass)")}
 
 
 def run_cg_config(A_host, B, steps, warmup=5):
@@ -232,20 +316,17 @@ def run_cg_config(A_host, B, steps, warmup=5):
     ctx.synchronize()
     t = time.perf_counter() - t0
     k = 1 if B.ndim == 1 else B.shape[1]
-    # algorithmic_gbs: SURVEY §8(d)'s per-iteration bytes of the launch-per-pass
-    # CG over the measured time. The persistent small-n loop (cfg2) keeps y and
-    # Ap on chip and moves about half of them (profiles/r01_pmc_cfg2.json), so
-    # there this figure is an effective rate, not HBM traffic.
     return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "rhs": k, "n": A.n, "nnz": A.nnz,
-            "algorithmic_gbs": cg_iteration_bytes(A.n, A.nnz, k) * steps / t / 1e9,
             "persistent_loop": chunk == 256}
 
 
-def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"):
+def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle", ceiling_key=None):
     """GMRES(30) iterations/s, one 30-step cycle (tol = 0) incl. the final
-    x = x0 + V y; median of 3 after one warm-up cycle. Default matrix: cfg3."""
+    x = x0 + V y; median of 3 after one warm-up cycle. Default matrix: cfg3.
+    Then one more cycle with HIP events around every SpMV and MGS launch:
+    each kernel's roofline on the bytes it must move, and the cycle's."""
     import krylov_amd
-    from krylov_amd import _helpers, problems
+    from krylov_amd import _helpers, _lib, problems
     from krylov_amd.device import get_context
     from krylov_amd.gmres import _GmresState
 
@@ -255,8 +336,8 @@ def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"
     prob = _helpers.Problem(A, np.ones(R.shape[0]), None, None)
     ctx = get_context()
     st = _GmresState(prob, 30, 1)
-    times = []
-    for rep in range(4):
+
+    def cycle():
         st.start()
         st.set_criterion(np.zeros(1))
         ctx.synchronize()
@@ -264,20 +345,76 @@ def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle"
         hist, _ = st.run(30)
         st.solution()
         ctx.synchronize()
-        t1 = time.perf_counter()
         assert len(hist) == 30
-        if rep >= 1:
-            times.append(t1 - t0)
+        return time.perf_counter() - t0
+
+    times = [cycle() for _ in range(4)][1:]
     t = float(np.median(times))
-    return {"it_per_s": 30.0 / t, "cycle_ms": 1e3 * t, "gbs": gmres_cycle_bytes(R.shape[0], R.nnz) / t / 1e9,
-            "n": R.shape[0], "nnz": int(R.nnz), "config": label}
+    n, nnz = R.shape[0], int(R.nnz)
+    prof = profiled(ctx, [_lib.PROF_SPMV, _lib.PROF_MGS], cycle)
+    (ns, ms_s), (nm, ms_m) = prof[_lib.PROF_SPMV], prof[_lib.PROF_MGS]
+    layout = A.layout()
+    kname, sb, sform = image_bytes_k1(layout, n, nnz, vectors=3)
+    # MGS of Arnoldi step j: w in, V_0..V_j read once, V_{j+1} out (the first
+    # inner product <V_0, w> is the SpMV epilogue's): (j + 3) n 8 B
+    mgs_b = sum((j + 3) * n * 8 for j in range(30))
+    sol_b = 32 * n * 8  # x = x0 + V y: V_0..V_29 and x0 read, x written
+    cyc_b = 30 * sb + mgs_b + sol_b
+    spmv_roof = hbm_roofline(kname, sb, ms_s / max(ns, 1) / 1e3, sform + " (w = A V_k stored; V_0 read for <V_0, w>)",
+                             ns)
+    mgs_roof = hbm_roofline("gm_mgsl_kernel / gm_mgsp_kernel (all MGS passes of a step in one launch)",
+                            mgs_b / max(nm, 1), ms_m / max(nm, 1) / 1e3, "mean over steps j = 0..29 of (j + 3)*n*8 (w in, V_0..V_j read "
+                            "once, V_{j+1} out)", nm)
+    share_s, share_m = ms_s / 1e3 / t, ms_m / 1e3 / t
+    out = {"it_per_s": 30.0 / t, "cycle_ms": 1e3 * t, "n": n, "nnz": nnz, "config": label,
+           "roofline": spmv_roof if share_s >= share_m else mgs_roof,
+           "spmv": spmv_roof, "mgs": mgs_roof,
+           "time_share": {"spmv": share_s, "mgs": share_m, "rest": 1.0 - share_s - share_m},
+           "cycle_roofline": {"bound": "hbm", "achieved": cyc_b / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": cyc_b / t / 1e9 / HBM_PEAK_GBS, "bytes_per_cycle": cyc_b,
+                              "bytes_formula": "30 SpMVs (above) + sum_j (j+3)*n*8 (MGS) + 32*n*8 (x = x0 + V y)"}}
+    if kname.startswith("spmv_cb"):
+        cal = gather_ceiling(ceiling_key or "cfg3")
+        if cal:
+            sec = ms_s / max(ns, 1) / 1e3
+            out["spmv"]["gather"] = {"bound": "gather", "achieved": nnz / sec / 1e9, "unit": "G gathers/s",
+                                     "peak": cal["ceiling_g_per_s"], "frac": nnz / sec / 1e9 / cal["ceiling_g_per_s"],
+                                     "peak_source": f"profiles/{GATHER_CEILING}[{ceiling_key or 'cfg3'}]: "
+                                                    + cal["what"]}
+    return out
+
+
+def run_gmres_restarted(A_host, cycles=10):
+    """krylov_amd.gmres_restarted(A, b, restart=30) on the metric matrix for
+    `cycles` x0-chained cycles (tol small enough that none succeeds): the
+    whole call (b upload, the chain on the device, the final x download) over
+    its cycles, median of 3 after a warm-up."""
+    import krylov_amd
+
+    A = krylov_amd.CsrOperator(A_host)
+    b = np.ones(A.n)
+
+    def call():
+        t0 = time.perf_counter()
+        _, infos = krylov_amd.gmres_restarted(A, b, restart=30, tol=1e-300, atol=0.0, max_cycles=cycles)
+        t = time.perf_counter() - t0
+        assert len(infos) == cycles and all(i.numsteps == 30 for i in infos)
+        return t
+
+    call()
+    t = float(np.median([call() for _ in range(3)]))
+    return {"cycles": cycles, "call_ms": 1e3 * t, "cycle_ms": 1e3 * t / cycles, "it_per_s": 30 * cycles / t,
+            "config": f"metric 15-point, krylov_amd.gmres_restarted restart=30, {cycles} x0-chained cycles "
+                      "(b upload and x download included; the chain stays on the device)"}
 
 
 def run_bicgstab(R, iters=30):
     """krylov_amd.bicgstab on the cfg3 matrix (tol = 0, `iters` iterations,
-    3 SpMVs and 6 inner products each, the scalars chained on the device):
-    the call's rate at the host-array boundary, median of 3 after a warm-up."""
+    2 SpMVs and 6 inner products each, the scalars chained on the device):
+    the call's rate at the host-array boundary, median of 3 after a warm-up;
+    then one call with HIP events around every SpMV (the dominant kernel)."""
     import krylov_amd
+    from krylov_amd import _lib
 
     A = krylov_amd.CsrOperator(R)
     b = np.ones(R.shape[0])
@@ -289,7 +426,12 @@ def run_bicgstab(R, iters=30):
         ts.append(time.perf_counter() - t0)
         assert info.numsteps == iters
     t = float(np.median(ts))
-    return {"it_per_s": iters / t, "call_ms": 1e3 * t, "n": R.shape[0], "nnz": int(R.nnz),
+    n, nnz = R.shape[0], int(R.nnz)
+    prof = profiled(A.ctx, [_lib.PROF_SPMV], lambda: krylov_amd.bicgstab(A, b, tol=0.0, atol=0.0, maxiter=iters))
+    cnt, ms = prof[_lib.PROF_SPMV]
+    kname, sb, sform = image_bytes_k1(A.layout(), n, nnz)
+    roof = hbm_roofline(kname, sb, ms / max(cnt, 1) / 1e3, sform, cnt, spmv_share_of_call=ms / 1e3 / t)
+    return {"it_per_s": iters / t, "call_ms": 1e3 * t, "n": n, "nnz": nnz, "roofline": roof,
             "config": f"cfg3 random nonsym n=2e6, krylov_amd.bicgstab tol=0 maxiter={iters} (b upload and x download "
                       "included)"}
 
@@ -352,6 +494,7 @@ def run_minres_cfg5(steps=100):
 
 
 PMC_SUMMARY = "r03b_pmc_traffic.json"
+GATHER_CEILING = "r04_gather_ceiling.json"
 
 
 def pmc_traffic(n, nnz, kernel):
@@ -441,6 +584,29 @@ def run_spmv_general(A_host, steps):
     return roof
 
 
+def run_spmv_unstructured(A_host, steps):
+    """The metric matrix under a fixed random symmetric permutation
+    (problems.permuted_sym, seed 0: the same nonzeros and values, scattered
+    columns): CG's SpMV as general CSR takes it, with the kernel it lands on
+    and that kernel's roofline on its image bytes (and, for the column-blocked
+    kernels, its gather rate against the measured ceiling)."""
+    from krylov_amd import problems
+
+    B = problems.permuted_sym(A_host, 0)
+    n, nnz = B.shape[0], int(B.nnz)
+    res = run_cg_bench(B, np.ones(n), steps, 5, 1, 0, 0, None, roofline_launches=steps)
+    kname, sb, form = image_bytes_k1(res["layout"], n, nnz)
+    roof = hbm_roofline(kname, sb, res["spmv_avg_s"], form, res["spmv_count"],
+                        cg_it_per_s=steps / res["elapsed"], matrix="15-point 216^3 under P A P^T, P = "
+                        "default_rng(0).permutation(n)")
+    cal = gather_ceiling("metric_permuted")
+    if cal and kname.startswith("spmv_cb"):
+        roof["gather"] = {"bound": "gather", "achieved": nnz / res["spmv_avg_s"] / 1e9, "unit": "G gathers/s",
+                          "peak": cal["ceiling_g_per_s"], "frac": nnz / res["spmv_avg_s"] / 1e9 / cal["ceiling_g_per_s"],
+                          "peak_source": f"profiles/{GATHER_CEILING}[metric_permuted]: " + cal["what"]}
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -467,8 +633,10 @@ def main():
     cfg4 = None
     if args.workload == "cfg4" or not args.quick:
         P3 = problems.poisson2d(3163)
+        from krylov_amd import _lib
+
         cfg4 = run_cg_bench(P3, cfg4_rhs(P3.shape[0], rank), min(args.steps, 40), min(args.warmup, 5), world, rank,
-                            local, pg, roofline_launches=16)
+                            local, pg, roofline_launches=16, prof_ids=[_lib.PROF_UPDATE, _lib.PROF_OTHER])
     if args.workload == "cfg4":
         res, hn, hnnz = cfg4, P3.shape[0], int(P3.nnz)
         workload = (f"krylov.cg block CG, 2-D 5-point Poisson 3163^2, {cfg4['rhs']} RHS per GPU (BASELINE cfg4), "
@@ -481,8 +649,19 @@ def main():
         steps_timed = args.steps
     T = res["elapsed"]
     rhs = res["rhs"]
-    kname = spmv_kernel_desc(res["layout"], hn)[0]
-    roof = roofline_of(res, hn, hnnz, pmc_traffic(hn, hnnz, kname) if rhs == 1 else None)
+    if args.workload == "cfg4":
+        roof, it_roof = cfg4_rooflines(res, steps_timed)
+    else:
+        kname = spmv_kernel_desc(res["layout"], hn)[0]
+        roof = roofline_of(res, hn, hnnz, pmc_traffic(hn, hnnz, kname))
+        # the iteration: the SpMV's image bytes + the one-launch update
+        # (cg_upd_kernel: r, y, p read and written, Ap read = 7 n 8 B)
+        it_b = roof["bytes_per_launch"] + 7 * hn * 8
+        t_it = T / steps_timed
+        it_roof = {"bound": "hbm", "achieved": it_b / t_it / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": it_b / t_it / 1e9 / HBM_PEAK_GBS, "bytes_per_iteration": it_b,
+                   "bytes_formula": "SpMV image bytes (roofline.bytes_per_launch) + 7*n*8 (cg_upd_kernel: r, y, p "
+                                    "in and out, Ap in)"}
     out = {
         "metric": "CG iters/sec + SpMV GB/s (fp64, n=10M, nnz=150M); GMRES(30) iters/sec",
         "value": world * rhs * steps_timed / T,
@@ -506,9 +685,9 @@ def main():
             "parallelism": f"rhs-shard x{world}" + (" (one RCCL resnorm allreduce per iteration)" if world > 1 else ""),
         },
         "spmv_gbs": roof["achieved"],
-        "spmv_ms": roof["spmv_ms"],
-        "cg_iter_gbs_per_gpu": cg_iteration_bytes(hn, hnnz, rhs) * steps_timed / T / 1e9,
+        "spmv_ms": roof["ms_per_launch"],
         "roofline": roof,
+        "iteration_roofline": it_roof,
     }
     if cfg4 is not None and args.workload != "cfg4":
         c4 = P3.shape[0]
@@ -520,21 +699,26 @@ def main():
             "n": c4,
             "nnz": int(P3.nnz),
             "spmv_ms": 1e3 * cfg4["spmv_avg_s"],
-            "iteration_gbs_per_gpu": cg_iteration_bytes(c4, int(P3.nnz), cfg4["rhs"]) * min(args.steps, 40)
-                                     / cfg4["elapsed"] / 1e9,
             "config": "BASELINE cfg4: Poisson 3163^2 block CG, 8 RHS per GPU, one RCCL allreduce per iteration",
         }
+        c4_spmv, c4_it = cfg4_rooflines(cfg4, min(args.steps, 40))
+        out["cfg4_sharded"]["roofline"] = c4_spmv
+        out["cfg4_sharded"]["iteration_roofline"] = c4_it
     del P3
     if world == 1 and not args.quick and args.workload == "metric":
         out["spmv_general"] = run_spmv_general(A_host, args.steps)
+        out["spmv_unstructured"] = run_spmv_unstructured(A_host, min(args.steps, 64))
         R3 = problems.random_nonsym(2_000_000)
-        g = run_gmres(R3)
+        g = run_gmres(R3, ceiling_key="cfg3")
         out["gmres30_it_per_s"] = g["it_per_s"]
         out["gmres"] = g
         out["bicgstab_cfg3"] = run_bicgstab(R3)
         del R3
         # north_star: GMRES(30) on the same (metric) matrix
         out["gmres_metric"] = run_gmres(A_host, f"metric 15-point {args.m}^3, GMRES(30) mgs, one cycle")
+        out["gmres_metric_restarted"] = run_gmres_restarted(A_host)
+        out["gmres_metric_restarted"]["vs_single_cycle"] = (out["gmres_metric_restarted"]["cycle_ms"]
+                                                            / out["gmres_metric"]["cycle_ms"])
         out["end_to_end"] = run_end_to_end(A_host, args.steps)
     if world == 1 and args.configs:
         extra = {}

@@ -200,20 +200,26 @@ def _num_operations(k):
     }
 
 
-def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_dev=None, host_x=True):
+def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_in=None, x_out=None, host_x=True):
     """One ``gmres`` call's loop (gmres.py:150-251) on the device state ``st``.
 
     ``tol_of_r0`` (restarts) maps the device's initial residual norm
     ``||Ml (b - A x0)||`` to this call's ``tol``, so the norm is read once.
-    ``x_dev`` (restarts): x0 is this DeviceVector instead of the problem's
-    host x0, and the cycle leaves its xk in it (device to device); the host
-    copy of xk is made only if ``host_x`` (else the returned xk is None).
-    Returns ``(success, xk, numsteps, resnorms)``."""
-    rn0 = st.start(x_dev)
+    Restarts keep the iterate on the device: ``x_in`` (a DeviceVector) is x0
+    instead of the problem's own, ``x_out`` receives xk device to device (it
+    may be ``x_in``), and the host copy of xk is made only if ``host_x`` (else
+    the returned xk is None). Returns ``(success, xk, numsteps, resnorms)``."""
+    rn0 = st.start(x_in)
     resnorms = [prob.colvals(rn0)]
+
+    def host_x0():
+        if x_in is None:
+            return prob.x0_or_zeros()  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
+        return prob.unpad_vec(x_in.to_host(), prob.r0_dtype)
+
     if callback is not None:
         # the reference passes Ml_r0 = Ml (b - A x0) here (gmres.py:143-144)
-        x0h = prob.x0_or_zeros() if x_dev is None else prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
+        x0h = host_x0()
         callback(x0h, prob.apply_host("Ml", prob.b - prob.A @ x0h))
     if tol_of_r0 is not None:
         tol = tol_of_r0(resnorms[0])
@@ -230,11 +236,6 @@ def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_dev=None, h
         if not solved:
             st.solution()
             solved = True
-
-    def host_x0():
-        if x_dev is None:
-            return prob.x0_or_zeros()  # _get_xk(None) / k == 0 returns x0 itself (gmres.py:89-99)
-        return prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
 
     while True:
         if np.all(resnorms[-1] <= criterion):
@@ -256,12 +257,13 @@ def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_dev=None, h
             solve()
             callback(st.xk(), np.array(resnorms[-1]))
 
+    if x_out is not None:
+        solve()
+        st.xk_into(x_out)
     if steps_done == 0:
-        xk = host_x0() if host_x else None  # x0 itself; x_dev already holds it
+        xk = host_x0() if host_x else None
     else:
         solve()
-        if x_dev is not None:
-            st.xk_into(x_dev)
         xk = st.xk() if host_x else None
     return success, xk, k, resnorms
 
@@ -314,16 +316,17 @@ def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycle
         return tol * bnorm / np.maximum(r0, 1e-300)
 
     st = _GmresState(prob, restart, sweeps)
-    x_dev = DeviceVector(prob.ctx, prob.n, prob.kpad, prob.dtype)
-    x_dev.upload(prob.pad(np.zeros(b.shape, dtype=prob.dtype) if x0 is None else np.asarray(x0)))
+    x_buf = DeviceVector(prob.ctx, prob.n, prob.kpad, prob.dtype)
+    x_cur = prob.x0_dev  # None: x0 = 0 on the device, nothing uploaded
     infos = []
     x = None
     for c in range(max_cycles):
         last = c == max_cycles - 1
         success, xk, k, resnorms = _cycle(prob, st, restart, tol, atol, callback, tol_of_r0=tol_of_r0,
-                                          x_dev=x_dev, host_x=last)
+                                          x_in=x_cur, x_out=x_buf, host_x=last)
+        x_cur = x_buf
         if success and xk is None:
-            xk = prob.unpad_vec(x_dev.to_host(), prob.r0_dtype)
+            xk = prob.unpad_vec(x_buf.to_host(), prob.r0_dtype)
         infos.append(Info(success, xk, k, resnorms, num_operations=_num_operations(k)))
         x = xk
         if success:

@@ -1,0 +1,61 @@
+"""Gather ceilings of the column-blocked SpMV (tools/gather_ceiling.hip) on
+the matrices whose single-RHS SpMV takes it: cfg3 (random nonsymmetric,
+n = 2e6, 19 random columns per row) and the metric matrix under a random
+symmetric permutation (bench.py's spmv_unstructured). Writes
+profiles/r04_gather_ceiling.json, which bench.py reads for the gather view of
+those legs' rooflines.
+
+    python3 tools/gather_ceiling.py [out.json]
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from krylov_amd import problems  # noqa: E402
+
+
+def run(lib, A, reps=20):
+    ip = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    ix = np.ascontiguousarray(A.indices, dtype=np.int32)
+    dv = np.ascontiguousarray(A.data, dtype=np.float64)
+    res = np.zeros(8)
+    rc = lib.gc_run(ctypes.c_int64(A.shape[0]), ctypes.c_int64(A.nnz), ip.ctypes.data_as(ctypes.c_void_p),
+                    ix.ctypes.data_as(ctypes.c_void_p), dv.ctypes.data_as(ctypes.c_void_p), reps,
+                    res.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0, rc
+    nnz = int(A.nnz)
+    g = lambda ms: nnz / (ms * 1e-3) / 1e9  # noqa: E731
+    return {
+        "n": int(A.shape[0]), "nnz": nnz, "col_blocks": int(res[4]), "cols_per_block": int(res[5]),
+        "library_spmv_ms": res[0], "library_g_per_s": g(res[0]),
+        "gather_only_ms": res[1], "gather_only_g_per_s": g(res[1]),
+        "image_and_gather_ms": res[2], "image_and_gather_g_per_s": g(res[2]),
+        "window_2mb_g_per_s": res[3],
+        "ceiling_g_per_s": g(res[2]),
+        "what": "one 8-B gather of x per entry plus the 12-B column + value stream of the column-blocked image, "
+                "in storage order, 16-B loads, 4 entries per thread per round, grid-stride over 8192 x 256 threads "
+                "(no row bookkeeping, no LDS, no y write): tools/gather_ceiling.hip",
+        "library_frac_of_ceiling": res[2] / res[0],
+    }
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_gather_ceiling.json")
+    lib = ctypes.CDLL(os.path.join(REPO, "tools", "libgather_ceiling.so"))
+    result = {}
+    result["cfg3"] = run(lib, problems.random_nonsym(2_000_000))
+    print("cfg3", json.dumps(result["cfg3"]), flush=True)
+    result["metric_permuted"] = run(lib, problems.permuted_sym(problems.stencil15_3d(216), 0))
+    print("metric_permuted", json.dumps(result["metric_permuted"]), flush=True)
+    with open(out, "w") as f:
+        json.dump(result, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
