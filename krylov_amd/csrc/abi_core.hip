@@ -493,7 +493,6 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
       A->cb_roff = dev_alloc(cb.roff.size() * 2);
       A->cb_col = dev_alloc(cb.col.size() * 4);
       A->cb_val = dev_alloc(cb.val.size() * sizeof(MV));
-      A->cb_y = dev_alloc((size_t)n * 8 + 64);
       KRY_HIP(hipMemcpyAsync(A->cb_gptr, cb.gptr.data(), cb.gptr.size() * 8, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->cb_roff, cb.roff.data(), cb.roff.size() * 2, hipMemcpyHostToDevice, st));
       KRY_HIP(hipMemcpyAsync(A->cb_col, cb.col.data(), cb.col.size() * 4, hipMemcpyHostToDevice, st));
@@ -548,7 +547,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
 static void csr_free(kry_csr *A) {
   void *bufs[] = {A->sptr,   A->swidth,   A->sidx,     A->sval,     A->indptr,    A->indices,
                   A->data,   A->sdelta,   A->scbase,   A->cb_gptr,  A->cb_roff,   A->cb_col,
-                  A->cb_val, A->cb_y,     A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val,
+                  A->cb_val, A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val,
                   A->sp_sptr, A->sp_width, A->sp_cbase, A->sp_delta, A->sp_val};
   for (void *b : bufs) dev_free(b);
 }

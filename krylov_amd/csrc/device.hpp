@@ -1214,63 +1214,24 @@ __device__ __forceinline__ void cb_segment(int64_t s0, int len, int r0, int r1, 
 }
 
 // ------------------------------------------- column-blocked SpMV (k = 1)
-// Pass b of cb_nb: each block takes 256-row groups; the group's entries with
-// columns in block b (stored in row order) are multiplied against the
-// L2-resident x block with coalesced loads and staged in LDS, then thread r
-// adds its row's products to the running sum in stored order (the same
-// sequence of roundings as csr_matvec: sum from 0, product rounded, then
-// added). The running sums live in cb_y between passes; the last pass applies
-// the epilogue.
-template <bool VEC, typename V, typename MV, class Src, class Epi>
-__global__ __launch_bounds__(kBlock) void spmv_cb_kernel(int b, int nb, int64_t n, int64_t ng,
-                                                         const int64_t *__restrict__ gptr,
-                                                         const uint16_t *__restrict__ roff,
-                                                         const int *__restrict__ col, const MV *__restrict__ val,
-                                                         double *__restrict__ ysum, Src src, Epi epi,
-                                                         double *__restrict__ part, const Ctrl *ctrl, int step) {
-  if (halted(ctrl, step)) return;
-  __shared__ V prod[kCbCap];
-  __shared__ double red[kBlock];
-  const int tid = threadIdx.x;
-  const auto bs = src.template bind<1>(0);
-  const bool last = b + 1 == nb;
-  double dacc = 0.0;
-  for (int64_t g = blockIdx.x; g < ng; g += gridDim.x) {
-    const int64_t s0 = gptr[(int64_t)b * ng + g];
-    const int len = (int)(gptr[(int64_t)b * ng + g + 1] - s0);
-    const int64_t row = g * kCbRows + tid;
-    const bool has = row < n;
-    int r0 = 0, r1 = 0;
-    if (has) {
-      r0 = roff[(int64_t)b * n + row];
-      r1 = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
-    }
-    V acc = (b == 0 || !has) ? V(0) : (V)ysum[row];
-    cb_segment<VEC, V, MV>(s0, len, r0, r1, col, val, bs, prod, acc, tid);
-    if (has) {
-      if (!last) ysum[row] = (double)acc;
-      else dacc += epi(row, 0, acc, bs(row, 0));
-    }
-  }
-  if (last && part != nullptr) {
-    __syncthreads();
-    red[tid] = dacc;
-    block_tree_reduce(red, kBlock, 1);
-    if (tid == 0) part[blockIdx.x] = red[0];
-  }
-}
-
-// Single-launch form of the column-blocked SpMV: block `blk` owns groups
-// blk, blk + G, ... (at most kCbMaxOwn of them) and walks the column blocks
-// in order for all of them, keeping every row's running sum in a register, so
-// there is no cb_y traffic and one launch instead of cb_nb. Blocks never wait
-// for each other (no residency assumption); they stay roughly in step on the
-// column blocks because their work per block is similar, which is what keeps
-// the current x block L2-resident. Same per-row summation order => bitwise.
+// Block `blk` owns the 256-row groups g0 + blk, g0 + blk + G, ... below g1
+// (at most kCbMaxOwn of them) and walks the column blocks in order for all of
+// them: per (column block, group) segment the entries are multiplied against
+// the L2-resident x block with coalesced loads and staged in LDS, then thread
+// r adds its row's products to the row's running sum (a register), in stored
+// order (the same sequence of roundings as csr_matvec: sum from 0, product
+// rounded, then added; rows are sorted, so block order is stored order). The
+// last column block applies the epilogue. Blocks never wait for each other
+// (no residency assumption); they stay roughly in step on the column blocks
+// because their work per block is similar, which is what keeps the current x
+// block L2-resident. A matrix with more than kCbPersistGrid * kCbMaxOwn groups
+// takes one launch per range of that many groups (round 4; before, one launch
+// per column block with the running sums carried through HBM: 2.4 GB per
+// SpMV at n = 10 M).
 constexpr int kCbMaxOwn = 16;
 constexpr int kCbPersistGrid = 1024;  // 4 blocks per CU: all resident, so they start together
 template <bool VEC, typename V, typename MV, class Src, class Epi>
-__global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int64_t ng,
+__global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int64_t ng, int64_t g0, int64_t g1,
                                                           const int64_t *__restrict__ gptr,
                                                           const uint16_t *__restrict__ roff,
                                                           const int *__restrict__ col, const MV *__restrict__ val,
@@ -1287,8 +1248,8 @@ __global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int
   for (int b = 0; b < nb; ++b) {
 #pragma unroll
     for (int o = 0; o < kCbMaxOwn; ++o) {
-      const int64_t g = (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
-      if (g >= ng) break;
+      const int64_t g = g0 + (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
+      if (g >= g1) break;
       const int64_t s0 = gptr[(int64_t)b * ng + g];
       const int len = (int)(gptr[(int64_t)b * ng + g + 1] - s0);
       const int64_t row = g * kCbRows + tid;
@@ -1304,8 +1265,8 @@ __global__ __launch_bounds__(kBlock) void spmv_cbp_kernel(int nb, int64_t n, int
   double dacc = 0.0;
 #pragma unroll
   for (int o = 0; o < kCbMaxOwn; ++o) {
-    const int64_t g = (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
-    if (g >= ng) break;
+    const int64_t g = g0 + (int64_t)blockIdx.x + (int64_t)o * gridDim.x;
+    if (g >= g1) break;
     const int64_t row = g * kCbRows + tid;
     if (row < n) dacc += epi(row, 0, acc[o], bs(row, 0));
   }
@@ -1441,37 +1402,28 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
       if (grid_out) *grid_out = grid;
       return;
     }
-    if (k == 1 && A->cb_nb > 0 && A->cb_ng <= (int64_t)kCbPersistGrid * kCbMaxOwn) {
+    if (k == 1 && A->cb_nb > 0) {
+      // one launch per range of kCbPersistGrid * kCbMaxOwn groups (one for n
+      // up to 4.2 M); launch l writes its block partials (every block writes
+      // one, 0 without groups) at part + l * grid: at most 32 launches
+      // (cb_build refuses more), so they fit the kMaxGridBlk partial rows
+      const int64_t per = (int64_t)kCbPersistGrid * kCbMaxOwn;
       grid = (int)std::min<int64_t>(A->cb_ng, kCbPersistGrid);
-      auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n, A->cb_ng,
-                           static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
-                           static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val), src, epi, part,
-                           ctrl, step);
-      };
-      if (cb_vec()) go(spmv_cbp_kernel<true, V, MV, Src, Epi>);
-      else go(spmv_cbp_kernel<false, V, MV, Src, Epi>);
-      KRY_HIP(hipGetLastError());
-      if (grid_out) *grid_out = grid;
-      return;
-    }
-    if (k == 1 && A->cb_nb > 0) {  // larger matrices: one launch per column block
-      static const int cb_grid = [] {
-        const char *e = getenv("KRY_CB_GRID");  // tuning override
-        return e ? std::max(1, std::min(atoi(e), kMaxGrid)) : kMaxGrid;
-      }();
-      grid = (int)std::min<int64_t>(A->cb_ng, cb_grid);
-      auto go = [&](auto kern) {
-        for (int b = 0; b < (int)A->cb_nb; ++b)
-          hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, b, (int)A->cb_nb, A->n, A->cb_ng,
+      int nl = 0;
+      for (int64_t g0 = 0; g0 < A->cb_ng; g0 += per, ++nl) {
+        const int64_t g1 = std::min<int64_t>(A->cb_ng, g0 + per);
+        double *pl = part ? part + (int64_t)nl * grid : nullptr;
+        auto go = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, (int)A->cb_nb, A->n, A->cb_ng, g0, g1,
                              static_cast<const int64_t *>(A->cb_gptr), static_cast<const uint16_t *>(A->cb_roff),
-                             static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val),
-                             static_cast<double *>(A->cb_y), src, epi, part, ctrl, step);
-      };
-      if (cb_vec()) go(spmv_cb_kernel<true, V, MV, Src, Epi>);
-      else go(spmv_cb_kernel<false, V, MV, Src, Epi>);
+                             static_cast<const int *>(A->cb_col), static_cast<const MV *>(A->cb_val), src, epi, pl,
+                             ctrl, step);
+        };
+        if (cb_vec()) go(spmv_cbp_kernel<true, V, MV, Src, Epi>);
+        else go(spmv_cbp_kernel<false, V, MV, Src, Epi>);
+      }
       KRY_HIP(hipGetLastError());
-      if (grid_out) *grid_out = grid;
+      if (grid_out) *grid_out = grid * nl;
       return;
     }
   }

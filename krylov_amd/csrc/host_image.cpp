@@ -296,6 +296,9 @@ bool cb_build(int64_t n, const I *ip, const I *ix, const MV *dv, CbHost<MV> &cb)
   for (int64_t f : far) nfar += f;
   if (!sorted || nnz == 0 || nfar * 4 < nnz) return false;
   const int64_t ng = (n + kCbRows - 1) / kCbRows;
+  // the SpMV takes one launch per 16,384 groups (1024 blocks x 16 owned
+  // groups) with 1024 block partials each, at most kMaxGridBlk = 32768 rows
+  if (ng > 32 * 16384) return false;
   // per (block, row) counts -> per (block, group) segment lengths
   hvec<uint16_t> roff;
   par_fill(roff, nb * n + 256, (uint16_t)0);

@@ -47,17 +47,17 @@ struct kry_csr {
   void *sdelta = nullptr;   // uint16, nslots (+ pad)
   void *scbase = nullptr;   // int32, nslots / 64 (+ pad): base of slot column j of slice s at sptr[s] / 64 + j
   // column-blocked image (scattered sparsity, single-RHS SpMV): the columns
-  // are cut into cb_nb blocks of cb_cols (x block L2-resident); pass b visits
-  // every 256-row group's entries with columns in block b, in stored order,
-  // carrying each row's running sum in cb_y between passes (bitwise: rows are
-  // sorted, so block order is stored order). Built only for int32 indices,
-  // sorted rows and scattered columns; the SELL image is kept for k > 1.
+  // are cut into cb_nb blocks of cb_cols (x block L2-resident); segment (b,
+  // g) holds 256-row group g's entries with columns in block b, in stored
+  // order (bitwise: rows are sorted, so block order is stored order); the
+  // SpMV walks the blocks in order with each row's running sum in a register
+  // (spmv_cbp_kernel). Built only for int32 indices, sorted rows and scattered
+  // columns; the SELL image is kept for k > 1.
   int64_t cb_nb = 0, cb_cols = 0, cb_ng = 0;
   void *cb_gptr = nullptr;  // int64, cb_nb * cb_ng + 1: segment (block b, group g) at [gptr[b ng + g], ...)
   void *cb_roff = nullptr;  // uint16, cb_nb * n (+ pad): row's first entry inside its segment
   void *cb_col = nullptr;   // int32, nnz (+ pad)
   void *cb_val = nullptr;   // dtype, nnz (+ pad)
-  void *cb_y = nullptr;     // double, n: running row sums between passes
   // diagonal-offset image (SELL-128/DIA, structured matrices, k = 1): in
   // every slice of 128 rows the columns of each row are row + o_j for a short
   // sorted list of offsets o_j shared by the slice, so slot column j holds the

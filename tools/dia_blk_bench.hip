@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) void dia_shift(const int64_t *__restrict__ spt
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 constexpr int kNear = 4;
-constexpr int kWinB = (128 + 2 * kNear) * 64;
+constexpr int kWinB = ((128 + 2 * kNear) * 64 + 1023) / 1024 * 1024;  // whole 1 KB DMA pieces
 constexpr int kValMax = 8;
 template <int MODE>
 __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,

@@ -12,7 +12,12 @@
 //   image    the same plus the 8-B values (the whole image stream + gathers):
 //            the ceiling the SpMV is measured against
 //   window   random 8-B gathers from one L2-resident 2 MB window (no stream)
+//   stream   the 12-B column + value stream alone (no gathers)
 //
+// The grid-stride kernels are not a ceiling for the SpMV (the library's
+// blocks walk the column blocks in step and run faster); the ceiling model
+// is max(nnz / window rate, stream time) if gathers and stream overlapped
+// perfectly, and their sum if they share the load path serially.
 // Each reports ms per launch and G gathers/s (nnz / time). Called from
 // tools/gather_ceiling.py, which builds cfg3 and the permuted metric matrix
 // and writes profiles/r04_gather_ceiling.json.
@@ -34,7 +39,7 @@ using namespace kry;
 typedef int gi4 __attribute__((ext_vector_type(4)));
 typedef double gd2 __attribute__((ext_vector_type(2)));
 
-template <bool VAL>
+template <bool VAL, bool GATHER = true>
 __global__ __launch_bounds__(256) void gc_stream(const gi4 *__restrict__ col, const gd2 *__restrict__ val, int64_t nnz,
                                                  const double *__restrict__ x, double *__restrict__ out) {
   const int64_t nq = (nnz + 3) / 4;
@@ -47,11 +52,15 @@ __global__ __launch_bounds__(256) void gc_stream(const gi4 *__restrict__ col, co
       a0 = v0.x; a1 = v0.y; a2 = v1.x; a3 = v1.y;
     }
     const int64_t e = 4 * q;
-    const double x0 = x[c.x];
-    const double x1 = e + 1 < nnz ? x[c.y] : 0.0;
-    const double x2 = e + 2 < nnz ? x[c.z] : 0.0;
-    const double x3 = e + 3 < nnz ? x[c.w] : 0.0;
-    s += a0 * x0 + a1 * x1 + a2 * x2 + a3 * x3;
+    if (GATHER) {
+      const double x0 = x[c.x];
+      const double x1 = e + 1 < nnz ? x[c.y] : 0.0;
+      const double x2 = e + 2 < nnz ? x[c.z] : 0.0;
+      const double x3 = e + 3 < nnz ? x[c.w] : 0.0;
+      s += a0 * x0 + a1 * x1 + a2 * x2 + a3 * x3;
+    } else {
+      s += a0 * (double)c.x + a1 * (double)c.y + a2 * (double)c.z + a3 * (double)c.w;
+    }
   }
   if (s == 1234.5678) out[0] = s;  // keeps the loads; never true for these inputs
 }
@@ -74,7 +83,8 @@ __global__ __launch_bounds__(256) void gc_window(const double *__restrict__ x, i
 }
 
 extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, const double *dv, int reps,
-                      double *res /* [0] library ms, [1] gather ms, [2] image ms, [3] window G/s, [4] nb, [5] cols */) {
+                      double *res /* [0] library ms, [1] gather ms, [2] image ms, [3] window G/s, [4] nb, [5] cols,
+                                  [6] stream ms */) {
   kry_ctx *ctx;
   if (kry_ctx_create(0, &ctx) != KRY_OK) return -1;
   kry_csr *A;
@@ -115,6 +125,9 @@ extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, cons
   const gd2 *val = static_cast<const gd2 *>(A->cb_val);
   res[1] = timeit([&] { hipLaunchKernelGGL(gc_stream<false>, dim3(8192), dim3(256), 0, st, col, val, nnz, x, o); });
   res[2] = timeit([&] { hipLaunchKernelGGL(gc_stream<true>, dim3(8192), dim3(256), 0, st, col, val, nnz, x, o); });
+  res[6] = timeit([&] {
+    hipLaunchKernelGGL((gc_stream<true, false>), dim3(8192), dim3(256), 0, st, col, val, nnz, x, o);
+  });
   const int64_t span = std::min<int64_t>(n, 262144);
   const int rounds = 64;
   const double wms = timeit([&] { hipLaunchKernelGGL(gc_window, dim3(8192), dim3(256), 0, st, x, span, rounds, o); });

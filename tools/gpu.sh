@@ -31,7 +31,7 @@ for step in "$@"; do
   echo "== step $i: $step" | tee -a "$OUT/steps.log"
   case $kind in
     tests)
-      timeout -k 10 900 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu ${arg//,/ } > "$log" 2>&1
+      timeout -k 10 900 python -u -m pytest --maxfail=8 -v -s --timeout 300 --timeout-method thread -m gpu ${arg//,/ } > "$log" 2>&1
       rc=$?; grep -E "PASSED|FAILED|ERROR|passed|failed|headroom|max rel" "$log" | tail -60 ;;
     suite)
       timeout -k 10 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > "$log" 2>&1

@@ -842,8 +842,8 @@ static int cb_tune(int64_t n, int reps) {
       printf("cb epilogue %-40s %.4f ms\n", name, tot / reps);
     };
     auto cbp = [&](auto src, auto epi, double *part) {
-      hipLaunchKernelGGL((spmv_cbp_kernel<double, double, decltype(src), decltype(epi)>), dim3(grid), dim3(kBlock), 0,
-                         0, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr, (const uint16_t *)A->cb_roff,
+      hipLaunchKernelGGL((spmv_cbp_kernel<true, double, double, decltype(src), decltype(epi)>), dim3(grid), dim3(kBlock),
+                         0, 0, (int)A->cb_nb, A->n, A->cb_ng, (int64_t)0, A->cb_ng, (const int64_t *)A->cb_gptr, (const uint16_t *)A->cb_roff,
                          (const int *)A->cb_col, (const double *)A->cb_val, src, epi, part, (const Ctrl *)nullptr, 0);
     };
     timeit("store y", [&] { cbp(SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, nullptr); });
@@ -891,35 +891,12 @@ static int cb_tune(int64_t n, int reps) {
     setenv("KRY_CB_COLS", cols, 1);
     kry_csr *A;
     KC(kry_csr_create(ctx, n, nnz, ip.data(), ix.data(), dv.data(), KRY_F64, KRY_I32, &A));
-    for (int grid : {1024, 2048, 4096, 8192}) {
-      auto launch = [&] {
-        for (int bb = 0; bb < (int)A->cb_nb; ++bb)
-          hipLaunchKernelGGL((spmv_cb_kernel<double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
-                             dim3(kBlock), 0, 0, bb, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr,
-                             (const uint16_t *)A->cb_roff, (const int *)A->cb_col, (const double *)A->cb_val,
-                             (double *)A->cb_y, SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1},
-                             (double *)nullptr, (const Ctrl *)nullptr, 0);
-      };
-      launch();
-      CK(hipDeviceSynchronize());
-      float tot = 0;
-      for (int r = 0; r < reps; ++r) {
-        CK(hipEventRecord(a, 0));
-        launch();
-        CK(hipEventRecord(b, 0));
-        CK(hipEventSynchronize(b));
-        float ms;
-        CK(hipEventElapsedTime(&ms, a, b));
-        tot += ms;
-      }
-      printf("cb cols=%s (nb=%ld) grid=%d: %.4f ms  %.0f GB/s (S)\n", cols, A->cb_nb, grid, tot / reps,
-             S / (tot / reps) / 1e6);
-    }
     for (int grid : {1024, 1536, 2048}) {
       if (A->cb_ng > (int64_t)grid * kCbMaxOwn) continue;
       auto launch = [&] {
-        hipLaunchKernelGGL((spmv_cbp_kernel<double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
-                           dim3(kBlock), 0, 0, (int)A->cb_nb, A->n, A->cb_ng, (const int64_t *)A->cb_gptr,
+        hipLaunchKernelGGL((spmv_cbp_kernel<true, double, double, SrcPlain<double>, EpiStore<double>>), dim3(grid),
+                           dim3(kBlock), 0, 0, (int)A->cb_nb, A->n, A->cb_ng, (int64_t)0, A->cb_ng,
+                           (const int64_t *)A->cb_gptr,
                            (const uint16_t *)A->cb_roff, (const int *)A->cb_col, (const double *)A->cb_val,
                            SrcPlain<double>{d_x, 1}, EpiStore<double>{d_y, 1}, (double *)nullptr, (const Ctrl *)nullptr, 0);
       };
