@@ -67,12 +67,11 @@ def image_bytes_k1(layout, n, nnz, vectors=2):
     if layout.get("col_blocks", 0):
         nb = layout["col_blocks"]
         ng = (n + 255) // 256
-        multi = ng > 1024 * 16  # launch_spmv: one launch per column block past 16 groups per block
-        kname = "spmv_cb_kernel (one launch per column block)" if multi else "spmv_cbp_kernel"
-        extra = 2 * (nb - 1) * n * 8 if multi else 0
-        return (kname, nnz * (4 + 8) + nb * n * 2 + (nb * ng + 1) * 8 + v + extra,
+        nl = (ng + 16383) // 16384  # launch_spmv: one launch per 16,384 row groups
+        kname = "spmv_cbp_kernel" + (f" ({nl} launches over row-group ranges)" if nl > 1 else "")
+        return (kname, nnz * (4 + 8) + nb * n * 2 + (nb * ng + 1) * 8 + v,
                 f"nnz*(4+8) (column + value) + col_blocks*n*2 (row offsets) + (col_blocks*ng+1)*8 (segment "
-                f"pointers) + {vt}" + (" + 2*(col_blocks-1)*n*8 (running sums between launches)" if multi else ""))
+                f"pointers) + {vt}")
     if layout.get("pair"):
         ps = layout["pair_slots"]
         return ("spmv_pair_kernel", ps * (8 + 2) + ps / 128 * 4 + (n + 127) // 128 * 12 + v,

@@ -456,6 +456,7 @@ __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr,
                                                double *__restrict__ part) {
   constexpr int CPL = 2, LPR = K / CPL, RPG = 64 / LPR, NG = kDiaSlice / RPG;
   constexpr bool VL = (MODE & 1) != 0;
+  constexpr bool HOIST = (MODE & 4) != 0;  // the first / last slot column, when far, loaded before the wait
   constexpr int PERW = kWinB + (VL ? kValMax * 1024 : 0);
   __shared__ __attribute__((aligned(16))) char lds[4 * PERW];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -495,6 +496,25 @@ __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr,
       for (int j = 0; j < w; ++j)
         __builtin_amdgcn_global_load_lds((glb_void *)(val + base + (int64_t)j * kDiaSlice + 2 * lane),
                                          (lds_void *)(my + kWinB + j * 1024), 16, 0, 0);
+    // far edge columns (Poisson: offsets -m and +m) into registers now, so
+    // their loads travel with the DMAs (one round trip per slice)
+    double xl[HOIST ? NG : 1][CPL], xr[HOIST ? NG : 1][CPL];
+    bool hl = false, hr = false;
+    if (HOIST && w > 0) {
+      const int o0 = doff[cb], o1 = doff[cb + w - 1];
+      hl = !(win && o0 >= lo && o0 <= hi);
+      hr = w > 1 && !(win && o1 >= lo && o1 <= hi);
+      const uint64_t l0 = dmask[2 * cb], l1 = dmask[2 * cb + 1];
+      const uint64_t h0 = dmask[2 * (cb + w - 1)], h1 = dmask[2 * (cb + w - 1) + 1];
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        const bool onl = hl && (((rl & 1) ? l1 : l0) >> (rl >> 1) & 1u) != 0;
+        const bool onr = hr && (((rl & 1) ? h1 : h0) >> (rl >> 1) & 1u) != 0;
+        ldx<CPL>(x + (onl ? r0 + rl + o0 : 0) * K + c0, xl[HOIST ? r : 0]);
+        ldx<CPL>(x + (onr ? r0 + rl + o1 : 0) * K + c0, xr[HOIST ? r : 0]);
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     double acc[NG][CPL];
 #pragma unroll
@@ -517,6 +537,12 @@ __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr,
           const d2v v = *reinterpret_cast<const d2v *>(my + (rl + off - lo) * K * 8 + c0 * 8);
           xv[r][0] = v.x;
           xv[r][1] = v.y;
+        } else if (HOIST && j == 0 && hl) {
+          xv[r][0] = xl[HOIST ? r : 0][0];
+          xv[r][1] = xl[HOIST ? r : 0][1];
+        } else if (HOIST && j == w - 1 && hr) {
+          xv[r][0] = xr[HOIST ? r : 0][0];
+          xv[r][1] = xr[HOIST ? r : 0][1];
         } else {
           ldx<CPL>(x + (on[r] ? r0 + rl + off : 0) * K + c0, xv[r]);
         }
@@ -668,6 +694,8 @@ int main(int argc, char **argv) {
       SM(2, 0, "slot-major CPL 2, 1 slice/wave", true);
       LD(0, "LDS window (near x), values direct");
       LD(1, "LDS window (near x) + LDS values");
+      LD(4, "LDS window, values direct, far x hoisted");
+      LD(5, "LDS window + LDS values, far x hoisted");
     }
   } else
   if (getenv("DIA_BLK_SHIFT")) {  // shifted-window variants against the slot-major kernel
