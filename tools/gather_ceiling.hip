@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "../include/krylov_hip.h"
@@ -82,9 +83,92 @@ __global__ __launch_bounds__(256) void gc_window(const double *__restrict__ x, i
   if (s == 1234.5678) out[0] = s;
 }
 
+// Candidate (round 4): contiguous ownership. Block blk owns the row groups
+// [gb, gb + own) (own <= OWN), so for column block b their segments are ONE
+// contiguous entry range: it is walked in full 1024-entry chunks (quads of
+// entries, as the library kernel), the products staged in LDS, and every
+// thread adds to each of its OWN rows' running sums the chunk's entries of
+// that row (its range from the row offsets), in stored order: bitwise the
+// library kernel. The library walks every (column block, group) segment as
+// its own chunk, and a segment of 256 rows holds ~240 (permuted metric) to
+// ~640 (cfg3) entries: most of each 1024-entry chunk idles.
+template <int OWN, class Epi>
+__global__ __launch_bounds__(256) void spmv_cbc(int nb, int64_t n, int64_t ng, int64_t g0, int64_t g1, int own,
+                                                const int64_t *__restrict__ gptr, const uint16_t *__restrict__ roff,
+                                                const int *__restrict__ col, const double *__restrict__ val,
+                                                const double *__restrict__ x, Epi epi) {
+  __shared__ double prod[kCbCap];
+  const int tid = threadIdx.x;
+  const int64_t gb = g0 + (int64_t)blockIdx.x * own;
+  const int no = (int)std::min<int64_t>(own, g1 - gb);
+  if (no <= 0) return;
+  double acc[OWN];
+#pragma unroll
+  for (int o = 0; o < OWN; ++o) acc[o] = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    const int64_t eb = gptr[(int64_t)b * ng + gb], ee = gptr[(int64_t)b * ng + gb + no];
+    int r0[OWN], r1[OWN];  // this thread's row of each owned group: entries [r0, r1) of the block's range
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      r0[o] = r1[o] = 0;
+      if (o < no) {
+        const int64_t s0 = gptr[(int64_t)b * ng + gb + o];
+        const int len = (int)(gptr[(int64_t)b * ng + gb + o + 1] - s0);
+        const int64_t row = (gb + o) * kCbRows + tid;
+        if (row < n) {
+          const int a = roff[(int64_t)b * n + row];
+          const int z = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
+          r0[o] = (int)(s0 - eb) + a;
+          r1[o] = (int)(s0 - eb) + z;
+        }
+      }
+    }
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const int64_t q0 = eb >> 2, qend = (ee + 3) >> 2;
+    for (int64_t qc = q0; qc < qend; qc += 256) {
+      const int64_t base = qc * 4 - eb;  // block-range-relative entry held by prod[0]
+      __syncthreads();                   // the previous chunk has been consumed
+      const int64_t q = qc + tid;
+      if (q < qend) {
+        const i4 c = __builtin_nontemporal_load(reinterpret_cast<const i4 *>(col) + q);
+        const d2 v0 = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q);
+        const d2 v1 = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q + 1);
+        const int jj[4] = {c.x, c.y, c.z, c.w};
+        const double aa[4] = {v0.x, v0.y, v1.x, v1.y};
+        double xj[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t e = base + 4 * (int64_t)tid + i;
+          xj[i] = (e >= 0 && e < ee - eb) ? x[jj[i]] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t e = base + 4 * (int64_t)tid + i;
+          if (e >= 0 && e < ee - eb) prod[4 * tid + i] = aa[i] * xj[i];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int o = 0; o < OWN; ++o) {
+        if (o >= no) break;
+        const int64_t lo = r0[o] > base ? r0[o] : base, hi = r1[o] < base + kCbCap ? r1[o] : base + kCbCap;
+        for (int64_t e = lo; e < hi; ++e) acc[o] = acc[o] + prod[e - base];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < OWN; ++o) {
+    if (o >= no) break;
+    const int64_t row = (gb + o) * kCbRows + tid;
+    if (row < n) epi(row, 0, acc[o], 0.0);
+  }
+}
+
 extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, const double *dv, int reps,
                       double *res /* [0] library ms, [1] gather ms, [2] image ms, [3] window G/s, [4] nb, [5] cols,
-                                  [6] stream ms */) {
+                                  [6] stream ms, [7] contiguous-ownership candidate ms, [8] its
+                                  entries differing from the library's y */) {
   kry_ctx *ctx;
   if (kry_ctx_create(0, &ctx) != KRY_OK) return -1;
   kry_csr *A;
@@ -125,6 +209,30 @@ extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, cons
   const gd2 *val = static_cast<const gd2 *>(A->cb_val);
   res[1] = timeit([&] { hipLaunchKernelGGL(gc_stream<false>, dim3(8192), dim3(256), 0, st, col, val, nnz, x, o); });
   res[2] = timeit([&] { hipLaunchKernelGGL(gc_stream<true>, dim3(8192), dim3(256), 0, st, col, val, nnz, x, o); });
+  {
+    // the contiguous-ownership candidate: bitwise against the library's y
+    std::vector<double> yl(n), yc(n);
+    hipMemcpy(yl.data(), y, n * 8, hipMemcpyDeviceToHost);
+    double *yc_d;
+    hipMalloc(&yc_d, n * 8 + 512);
+    const int grid = 1024;
+    const int64_t per = (int64_t)grid * 16;
+    res[7] = timeit([&] {
+      for (int64_t g0 = 0; g0 < A->cb_ng; g0 += per) {
+        const int64_t g1 = std::min<int64_t>(A->cb_ng, g0 + per);
+        const int own = (int)((g1 - g0 + grid - 1) / grid);
+        hipLaunchKernelGGL((spmv_cbc<16, EpiStore<double>>), dim3(grid), dim3(256), 0, st, (int)A->cb_nb, n, A->cb_ng,
+                           g0, g1, own, (const int64_t *)A->cb_gptr, (const uint16_t *)A->cb_roff,
+                           (const int *)A->cb_col, (const double *)A->cb_val, (const double *)x,
+                           EpiStore<double>{yc_d, 1});
+      }
+    });
+    hipMemcpy(yc.data(), yc_d, n * 8, hipMemcpyDeviceToHost);
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += memcmp(&yl[i], &yc[i], 8) != 0;
+    res[8] = (double)bad;
+    hipFree(yc_d);
+  }
   res[6] = timeit([&] {
     hipLaunchKernelGGL((gc_stream<true, false>), dim3(8192), dim3(256), 0, st, col, val, nnz, x, o);
   });

@@ -24,7 +24,7 @@ def run(lib, A, reps=20):
     ip = np.ascontiguousarray(A.indptr, dtype=np.int32)
     ix = np.ascontiguousarray(A.indices, dtype=np.int32)
     dv = np.ascontiguousarray(A.data, dtype=np.float64)
-    res = np.zeros(8)
+    res = np.zeros(12)
     rc = lib.gc_run(ctypes.c_int64(A.shape[0]), ctypes.c_int64(A.nnz), ip.ctypes.data_as(ctypes.c_void_p),
                     ix.ctypes.data_as(ctypes.c_void_p), dv.ctypes.data_as(ctypes.c_void_p), reps,
                     res.ctypes.data_as(ctypes.c_void_p))
@@ -46,16 +46,29 @@ def run(lib, A, reps=20):
                 "beside it as ceiling_serial_ms",
         "library_frac_of_ceiling": overlap_ms / res[0],
         "library_frac_of_serial": serial_ms / res[0],
+        "candidate_contiguous_ms": res[7], "candidate_contiguous_mismatches": int(res[8]),
     }
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_gather_ceiling.json")
+    which = sys.argv[2].split(",") if len(sys.argv) > 2 else ["cfg3", "metric_permuted"]
     lib = ctypes.CDLL(os.path.join(REPO, "tools", "libgather_ceiling.so"))
     result = {}
-    result["cfg3"] = run(lib, problems.random_nonsym(2_000_000))
-    print("cfg3", json.dumps(result["cfg3"]), flush=True)
-    result["metric_permuted"] = run(lib, problems.permuted_sym(problems.stencil15_3d(216), 0))
-    print("metric_permuted", json.dumps(result["metric_permuted"]), flush=True)
+    if "cfg3" in which:
+        result["cfg3"] = run(lib, problems.random_nonsym(2_000_000))
+        print("cfg3", json.dumps(result["cfg3"]), flush=True)
+    if "metric_permuted" in which:
+        B = problems.permuted_sym(problems.stencil15_3d(216), 0)
+        result["metric_permuted"] = run(lib, B)
+        print("metric_permuted", json.dumps(result["metric_permuted"]), flush=True)
+        # column-block widths (KRY_CB_COLS, read when the image is built)
+        for cols in (os.environ.get("GC_COLS_SWEEP") or "").split(","):
+            if cols:
+                os.environ["KRY_CB_COLS"] = cols
+                r = run(lib, B)
+                result[f"metric_permuted_cols{cols}"] = r
+                print(f"metric_permuted cols={cols}", json.dumps(r), flush=True)
+        os.environ.pop("KRY_CB_COLS", None)
     with open(out, "w") as f:
         json.dump(result, f, indent=1)
 
