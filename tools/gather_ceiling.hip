@@ -165,10 +165,141 @@ __global__ __launch_bounds__(256) void spmv_cbc(int nb, int64_t n, int64_t ng, i
   }
 }
 
+// Candidates (round 4, second set): contiguous ownership as spmv_cbc, plus
+//   QPT  quads per thread and chunk (chunk = 1024 * QPT entries): more
+//        loads and gathers in flight per wave;
+//   PF   the next chunk's column / value quads are loaded into registers
+//        before this chunk's gathers, across column blocks too (the chunk
+//        after a block's last one is the next block's first), so the stream
+//        latency hides behind the gathers;
+//   the products are double-buffered in LDS: one barrier per chunk.
+// The grid and the groups a block owns are the launcher's (OWN at most).
+template <int OWN, int QPT, bool PF, class Epi>
+__global__ __launch_bounds__(256) void spmv_cbx(int nb, int64_t n, int64_t ng, int64_t g0, int64_t g1, int own,
+                                                const int64_t *__restrict__ gptr, const uint16_t *__restrict__ roff,
+                                                const int *__restrict__ col, const double *__restrict__ val,
+                                                const double *__restrict__ x, Epi epi) {
+  constexpr int CAP = 1024 * QPT;
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  __shared__ double prod[2][CAP];
+  const int tid = threadIdx.x;
+  const int64_t gb = g0 + (int64_t)blockIdx.x * own;
+  const int no = (int)std::min<int64_t>(own, g1 - gb);
+  if (no <= 0) return;
+  double acc[OWN];
+#pragma unroll
+  for (int o = 0; o < OWN; ++o) acc[o] = 0.0;
+  int r0[OWN], r1[OWN];
+  auto setup = [&](int b, int64_t eb) {
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      r0[o] = r1[o] = 0;
+      if (o < no) {
+        const int64_t s0 = gptr[(int64_t)b * ng + gb + o];
+        const int len = (int)(gptr[(int64_t)b * ng + gb + o + 1] - s0);
+        const int64_t row = (gb + o) * kCbRows + tid;
+        if (row < n) {
+          const int a = roff[(int64_t)b * n + row];
+          const int z = (tid == kCbRows - 1 || row + 1 >= n) ? len : (int)roff[(int64_t)b * n + row + 1];
+          r0[o] = (int)(s0 - eb) + a;
+          r1[o] = (int)(s0 - eb) + z;
+        }
+      }
+    }
+  };
+  // chunk cursor: column block b, entries [eb, ee), quad qc
+  int b = 0;
+  int64_t eb = gptr[gb], ee = gptr[gb + no];
+  int64_t qc = eb >> 2;
+  auto advance = [&](int &bb, int64_t &ebb, int64_t &eee, int64_t &q) {  // to the next chunk; false at the end
+    q += 256 * QPT;
+    while (q >= ((eee + 3) >> 2)) {
+      if (++bb >= nb) return false;
+      ebb = gptr[(int64_t)bb * ng + gb];
+      eee = gptr[(int64_t)bb * ng + gb + no];
+      q = ebb >> 2;
+    }
+    return true;
+  };
+  // the first chunk may be empty too
+  {
+    int64_t q = qc - 256 * QPT;
+    if (!advance(b, eb, ee, q)) b = nb;
+    qc = q;
+  }
+  if (b < nb) setup(b, eb);
+  i4 c[QPT];
+  d2 v[2 * QPT];
+  auto load = [&](int64_t q0, int64_t qe, i4 *cc, d2 *vv) {
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int64_t q = q0 + u * 256 + tid;
+      if (q < qe) {
+        cc[u] = __builtin_nontemporal_load(reinterpret_cast<const i4 *>(col) + q);
+        vv[2 * u] = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q);
+        vv[2 * u + 1] = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(val) + 2 * q + 1);
+      }
+    }
+  };
+  if (b < nb) load(qc, (ee + 3) >> 2, c, v);
+  int buf = 0;
+  while (b < nb) {
+    int nbk = b;
+    int64_t neb = eb, nee = ee, nq = qc;
+    const bool more = advance(nbk, neb, nee, nq);
+    i4 cn[QPT];
+    d2 vn[2 * QPT];
+    if (PF && more) load(nq, (nee + 3) >> 2, cn, vn);
+    const int64_t base = qc * 4 - eb;
+    const int64_t len = ee - eb;
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int jj[4] = {c[u].x, c[u].y, c[u].z, c[u].w};
+      const double aa[4] = {v[2 * u].x, v[2 * u].y, v[2 * u + 1].x, v[2 * u + 1].y};
+      double xj[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t e = base + 4 * (int64_t)(u * 256 + tid) + i;
+        xj[i] = (e >= 0 && e < len) ? x[jj[i]] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t e = base + 4 * (int64_t)(u * 256 + tid) + i;
+        if (e >= 0 && e < len) prod[buf][4 * (u * 256 + tid) + i] = aa[i] * xj[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      if (o >= no) break;
+      const int64_t lo = r0[o] > base ? r0[o] : base, hi = r1[o] < base + CAP ? r1[o] : base + CAP;
+      for (int64_t e = lo; e < hi; ++e) acc[o] = acc[o] + prod[buf][e - base];
+    }
+    buf ^= 1;
+    if (!more) break;
+    if (nbk != b) setup(nbk, neb);
+    b = nbk; eb = neb; ee = nee; qc = nq;
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < QPT; ++u) { c[u] = cn[u]; v[2 * u] = vn[2 * u]; v[2 * u + 1] = vn[2 * u + 1]; }
+    } else {
+      load(qc, (ee + 3) >> 2, c, v);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < OWN; ++o) {
+    if (o >= no) break;
+    const int64_t row = (gb + o) * kCbRows + tid;
+    if (row < n) epi(row, 0, acc[o], 0.0);
+  }
+}
+
 extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, const double *dv, int reps,
                       double *res /* [0] library ms, [1] gather ms, [2] image ms, [3] window G/s, [4] nb, [5] cols,
                                   [6] stream ms, [7] contiguous-ownership candidate ms, [8] its
-                                  entries differing from the library's y */) {
+                                  entries differing from the library's y, [9 + 2 i], [10 + 2 i]: the same for
+                                  spmv_cbx variant i (i < 8) */) {
   kry_ctx *ctx;
   if (kry_ctx_create(0, &ctx) != KRY_OK) return -1;
   kry_csr *A;
@@ -231,6 +362,32 @@ extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, cons
     int64_t bad = 0;
     for (int64_t i = 0; i < n; ++i) bad += memcmp(&yl[i], &yc[i], 8) != 0;
     res[8] = (double)bad;
+    auto variant = [&](int i, auto kern, int grid, int ownmax) {
+      hipMemset(yc_d, 0, n * 8);
+      const int64_t per = (int64_t)grid * ownmax;
+      res[9 + 2 * i] = timeit([&] {
+        for (int64_t g0 = 0; g0 < A->cb_ng; g0 += per) {
+          const int64_t g1 = std::min<int64_t>(A->cb_ng, g0 + per);
+          const int own = (int)((g1 - g0 + grid - 1) / grid);
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, (int)A->cb_nb, n, A->cb_ng, g0, g1, own,
+                             (const int64_t *)A->cb_gptr, (const uint16_t *)A->cb_roff, (const int *)A->cb_col,
+                             (const double *)A->cb_val, (const double *)x, EpiStore<double>{yc_d, 1});
+        }
+      });
+      hipMemcpy(yc.data(), yc_d, n * 8, hipMemcpyDeviceToHost);
+      int64_t bd = 0;
+      for (int64_t r = 0; r < n; ++r) bd += memcmp(&yl[r], &yc[r], 8) != 0;
+      res[10 + 2 * i] = (double)bd;
+    };
+    using E = EpiStore<double>;
+    variant(0, spmv_cbx<16, 1, false, E>, 1024, 16);
+    variant(1, spmv_cbx<16, 1, true, E>, 1024, 16);
+    variant(2, spmv_cbx<16, 2, false, E>, 768, 16);
+    variant(3, spmv_cbx<16, 2, true, E>, 512, 16);
+    variant(4, spmv_cbx<8, 1, true, E>, 1280, 8);
+    variant(5, spmv_cbx<8, 2, true, E>, 768, 8);
+    variant(6, spmv_cbx<4, 2, true, E>, 1024, 4);
+    variant(7, spmv_cbx<16, 1, true, E>, 768, 16);
     hipFree(yc_d);
   }
   res[6] = timeit([&] {
@@ -240,6 +397,13 @@ extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, cons
   const int rounds = 64;
   const double wms = timeit([&] { hipLaunchKernelGGL(gc_window, dim3(8192), dim3(256), 0, st, x, span, rounds, o); });
   res[3] = 8192.0 * 256 * rounds * 8 / (wms * 1e-3) / 1e9;
+  // random-gather rate against the window size: 2, 3, 4, 5, 8 MB and the whole x
+  const int64_t spans[6] = {262144, 393216, 524288, 655360, 1048576, n};
+  for (int i = 0; i < 6; ++i) {
+    const int64_t sp = std::min<int64_t>(n, spans[i]);
+    const double t = timeit([&] { hipLaunchKernelGGL(gc_window, dim3(8192), dim3(256), 0, st, x, sp, rounds, o); });
+    res[25 + i] = 8192.0 * 256 * rounds * 8 / (t * 1e-3) / 1e9;
+  }
   res[4] = (double)A->cb_nb;
   res[5] = (double)A->cb_cols;
   hipFree(x);

@@ -24,7 +24,7 @@ def run(lib, A, reps=20):
     ip = np.ascontiguousarray(A.indptr, dtype=np.int32)
     ix = np.ascontiguousarray(A.indices, dtype=np.int32)
     dv = np.ascontiguousarray(A.data, dtype=np.float64)
-    res = np.zeros(12)
+    res = np.zeros(32)
     rc = lib.gc_run(ctypes.c_int64(A.shape[0]), ctypes.c_int64(A.nnz), ip.ctypes.data_as(ctypes.c_void_p),
                     ix.ctypes.data_as(ctypes.c_void_p), dv.ctypes.data_as(ctypes.c_void_p), reps,
                     res.ctypes.data_as(ctypes.c_void_p))
@@ -47,7 +47,16 @@ def run(lib, A, reps=20):
         "library_frac_of_ceiling": overlap_ms / res[0],
         "library_frac_of_serial": serial_ms / res[0],
         "candidate_contiguous_ms": res[7], "candidate_contiguous_mismatches": int(res[8]),
+        "cbx_variants": {name: {"ms": res[9 + 2 * i], "mismatches": int(res[10 + 2 * i])}
+                         for i, name in enumerate(CBX)},
+        "window_g_per_s_by_mb": dict(zip(["2", "3", "4", "5", "8", "all_x"], [float(v) for v in res[25:31]])),
+        "roff_bytes": int(res[4]) * int(A.shape[0]) * 2,
     }
+
+
+# spmv_cbx<OWN, QPT, PF> at a grid (tools/gather_ceiling.hip, gc_run's variant table)
+CBX = ["own16_q1_grid1024", "own16_q1_pf_grid1024", "own16_q2_grid768", "own16_q2_pf_grid512",
+       "own8_q1_pf_grid1280", "own8_q2_pf_grid768", "own4_q2_pf_grid1024", "own16_q1_pf_grid768"]
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_gather_ceiling.json")
