@@ -250,7 +250,7 @@ def test_dia_block_cg_matches_lane_group_and_oracle(golden, monkeypatch):
 
 
 @pytest.mark.parametrize("D", [1, 3, 7])
-@pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general"])
+@pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general", "Ml"])
 def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
     """Block CG with yk += alpha p deferred and applied D steps at a time
     (cg_pdefer_kernel, p cycling through D + 1 buffers, OpCgYFlush at each
@@ -258,13 +258,15 @@ def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
     roundings in the same order, so the history, the iterate and the step
     count are bitwise equal, for chunks of 1, 7, 32, 1 and 19 steps (ends
     that fall before, on and after a flush), a solve stopping in the middle
-    of a chunk (tol), a weighted inner product and a general (non-DIA)
-    matrix."""
+    of a chunk (tol), a weighted inner product, a general (non-DIA)
+    matrix and a left preconditioner Ml (cg.py:180,207: r and p carry Ml; the
+    deferral only needs p_i, so it stays on)."""
     import krylov_amd
     from krylov_amd import _helpers, problems
     from krylov_amd.cg import _CGState
 
     inner = None
+    Ml = None
     k = 4
     if case == "poisson2d_300_f64":
         A = problems.poisson2d(300)
@@ -282,6 +284,9 @@ def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
         A = A.tocsr()
         A.sort_indices()
         k = 2
+    elif case == "Ml":
+        A = problems.poisson2d(200)
+        Ml = scipy.sparse.diags(1.0 / A.diagonal() * np.random.default_rng(6).uniform(0.5, 1.5, A.shape[0])).tocsr()
     else:
         A = problems.poisson2d(200)
         inner = krylov_amd.WeightedInner(np.random.default_rng(4).uniform(1.0, 2.0, A.shape[0]))
@@ -292,12 +297,13 @@ def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
 
     def solve(d):
         monkeypatch.setenv("KRY_CG_YDEFER", str(d))
-        st = _CGState(_helpers.Problem(op, B, None, inner))
+        st = _CGState(_helpers.Problem(op, B, None, inner, Ml=Ml))
         st.start()
         st.set_criterion(np.zeros(k))
         hs = [st.run(n) for n in (1, 7, 32, 1, 19)]
+        assert st.defer_info()[0] == d
         h, x = np.concatenate(hs), st.get(0)
-        _, info = krylov_amd.cg(op, B, inner=inner, tol=1e-6)
+        _, info = krylov_amd.cg(op, B, Ml=Ml, inner=inner, tol=1e-6)
         return h, x, info
 
     h1, x1, info1 = solve(D)
