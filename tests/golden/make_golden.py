@@ -233,8 +233,29 @@ def make_solvers(krylov):
     with quiet:
         sol, info = krylov.cg(W64, np.ones(W.shape[0]), inner=inner, tol=1e-8)
     _info_arrays("cg_w20_weighted", sol, info, out)
+    out.update(make_weighted_spd(krylov))
 
     np.savez_compressed(os.path.join(HERE, "solvers.npz"), **out)
+
+
+def make_weighted_spd(krylov):
+    """CG with the weighted inner product on a positive definite operator
+    (round 4): the 20^3 Laplacian with no shift (sigma = 0), row-scaled by
+    1/w, so that A is self-adjoint and positive definite in <x, y>_W. The
+    cg_w20_weighted case above runs CG on the shifted, indefinite operator,
+    whose 641-step history is chaotic in the summation order; this one
+    converges in 87 steps and its history moves by <= 1.3e-12 when only the
+    summation order changes, so the weighted path is pinned at 1e-10."""
+    out = {}
+    W, w = problems.shifted_lap3d_weighted(20, sigma=0.0)
+
+    def inner(x, y):
+        return np.dot(x.T, w * y)
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        sol, info = krylov.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=inner, tol=1e-8)
+    _info_arrays("cg_w20spd_weighted", sol, info, out)
+    return out
 
 
 def make_precond(krylov):
@@ -296,6 +317,12 @@ def make_problem_hashes():
 
 if __name__ == "__main__":
     krylov = _import_reference()
+    if "--only-weighted-spd" in sys.argv:  # append to the existing solvers.npz
+        path = os.path.join(HERE, "solvers.npz")
+        out = dict(np.load(path))
+        out.update(make_weighted_spd(krylov))
+        np.savez_compressed(path, **out)
+        sys.exit(0)
     if "--only-precond" in sys.argv:
         make_precond(krylov)
         make_arnoldi(krylov)

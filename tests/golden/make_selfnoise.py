@@ -47,7 +47,10 @@ CASES = {
     "metric_cg": ("stencil15_3d(216)", 1e-8, "default"),
     "cfg2_cg": ("poisson2d(1000)", 1e-8, "default"),
     "cg_w20_weighted": ("shifted_lap3d_weighted(20)", 1e-8, "weighted"),
+    # round 4: the positive definite weighted case (make_golden.make_weighted_spd)
+    "cg_w20spd_weighted": ("shifted_lap3d_weighted(20, sigma=0.0)", 1e-8, "weighted"),
 }
+SMALL_CASES = ("cg_w20_weighted", "cg_w20spd_weighted")
 VARIANTS = {
     "blas1": {"OPENBLAS_NUM_THREADS": "1"},
     "blas2": {"OPENBLAS_NUM_THREADS": "2"},
@@ -128,7 +131,7 @@ def main():
         for variant, env in VARIANTS.items():
             if f"{case}_{variant}" in out:  # recorded by an earlier run
                 continue
-            if variant in SMALL_ONLY and case != "cg_w20_weighted":
+            if variant in SMALL_ONLY and case not in SMALL_CASES:
                 continue
             e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", **env)
             subprocess.check_call([sys.executable, __file__, "--one", case, variant, tmp], env=e)

@@ -228,6 +228,24 @@ def test_cg_weighted_histories(golden):
                     final_atol=1e-8 * ref[0])
 
 
+def test_cg_weighted_spd_histories(golden):
+    """Weighted CG pinned at the 1e-10 contract (round 4): the unshifted 20^3
+    Laplacian row-scaled by 1/w is positive definite in <x, y>_W, and the
+    reference's history on it moves by <= 1.3e-12 when only the summation order
+    of its inner product changes (selfnoise.npz, make_golden.make_weighted_spd), unlike the
+    indefinite case above. 87 steps; same step count and success, every
+    entry within 1e-10 relative, the solution to 1e-8."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    d = golden["solvers"]
+    W, w = problems.shifted_lap3d_weighted(20, sigma=0.0)
+    info = krylov_amd.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=krylov_amd.WeightedInner(w), tol=1e-8)[1]
+    ref = d["cg_w20spd_weighted_resnorms"]
+    assert int(d["cg_w20spd_weighted_numsteps"]) == 87
+    H.assert_parity(info, d, "cg_w20spd_weighted", rtol=1e-10, xtol=1e-8, final_atol=1e-8 * ref[0])
+
+
 def _restart_dev(hist, ref):
     """Per-entry relative deviation of a chained restart history."""
     return np.abs(hist - ref) / np.abs(ref)

@@ -106,6 +106,13 @@ def test_oracle_minres_histories(golden):
 
     _check("minres_w20_f32", *K.minres(W, np.ones(W.shape[0], dtype=np.float32), inner=inner, tol=0.0, maxiter=50), d)
     _check("cg_w20_weighted", *K.cg(W.astype(np.float64), np.ones(W.shape[0]), inner=inner, tol=1e-8), d)
+    # the positive definite weighted case (sigma = 0, make_golden.make_weighted_spd)
+    Ws, ws = problems.shifted_lap3d_weighted(20, sigma=0.0)
+
+    def inner_s(x, y):
+        return np.dot(x.T, ws * y)
+
+    _check("cg_w20spd_weighted", *K.cg(Ws.astype(np.float64), np.ones(Ws.shape[0]), inner=inner_s, tol=1e-8), d)
 
 
 def test_oracle_givens(golden):
