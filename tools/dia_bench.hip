@@ -373,6 +373,93 @@ __global__ __launch_bounds__(256) void dia_reuse(const int64_t *__restrict__ spt
   if (tid == 0) part[g] = red[0];
 }
 
+// Persistent DIA SpMV (round 4 probe for a fused CG iteration at n = 10 M):
+// one block of 512 threads per CU, laid out as cg_upd_kernel's granules, so
+// granule u of wave wv of block b is slice b * 8 NV + 8 u + wv and the lane's
+// two rows are its 16-B granule. Every slice's two row sums stay in
+// registers (acc[NV][2], 160 VGPRs at NV = 40) until the end of the launch,
+// where the fused kernel would exchange <p, Ap> and update r in place. MODE
+// bits: 1 Ap not stored (what the fused kernel's SpMV phase would cost);
+// otherwise stored at the end (bitwise check against the library kernel).
+template <int NV, int UNR, int MODE>
+__global__ __launch_bounds__(512) void dia_persist(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                   const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                   const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                   const double *__restrict__ x, double *__restrict__ y,
+                                                   double *__restrict__ part) {
+  __shared__ double red[512];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t sb = (int64_t)blockIdx.x * NV * 8;
+  double acc[NV][2];
+  double dacc = 0.0;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    acc[u][0] = acc[u][1] = 0.0;
+    const int64_t s = sb + 8 * u + wv;
+    if (s >= nslices) continue;
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * kDiaSlice + 2 * lane;
+    const int64_t c0 = base / kDiaSlice;
+    const int *mo = doff + c0;
+    const uint64_t *mk = dmask + 2 * c0;
+    const double *cv = val + base + 2 * lane;
+    double a0 = 0.0, a1 = 0.0;
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      int off[UNR];
+      uint64_t me[UNR], md[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) {
+        off[q] = mo[j0 + q];
+        me[q] = mk[2 * (j0 + q)];
+        md[q] = mk[2 * (j0 + q) + 1];
+      }
+      d2v a[UNR], xv[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; ++q)
+        a[q] = j0 + q < w ? __builtin_nontemporal_load(reinterpret_cast<const d2v *>(cv + (int64_t)(j0 + q) * kDiaSlice))
+                          : d2v{0.0, 0.0};
+      bool on0[UNR], on1[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) {
+        on0[q] = j0 + q < w && ((me[q] >> lane) & 1u) != 0;
+        on1[q] = j0 + q < w && ((md[q] >> lane) & 1u) != 0;
+        xv[q] = *reinterpret_cast<const d2v *>(x + ((on0[q] || on1[q]) ? row + off[q] : 0));
+      }
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) {
+        const double p0 = a[q].x * xv[q].x, p1 = a[q].y * xv[q].y;
+        const double t0 = a0 + p0, t1 = a1 + p1;
+        a0 = on0[q] ? t0 : a0;
+        a1 = on1[q] ? t1 : a1;
+      }
+    }
+    acc[u][0] = a0;
+    acc[u][1] = a1;
+  }
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int64_t s = sb + 8 * u + wv;
+    if (s >= nslices) continue;
+    const int64_t row = s * kDiaSlice + 2 * lane;
+    const d2v p = *reinterpret_cast<const d2v *>(x + row);
+    dacc += p.x * acc[u][0];
+    if (row + 1 < n) dacc += p.y * acc[u][1];
+    if (!(MODE & 1)) {
+      if (row + 1 < n) __builtin_nontemporal_store(d2v{acc[u][0], acc[u][1]}, reinterpret_cast<d2v *>(y + row));
+      else if (row < n) y[row] = acc[u][0];
+    }
+  }
+  red[tid] = dacc;
+  __syncthreads();
+  for (int h = 256; h > 0; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  if (tid == 0) part[blockIdx.x] = red[0];
+}
+
 __global__ void dpp_direction(int *o) { o[threadIdx.x] = __builtin_amdgcn_update_dpp(-7, (int)threadIdx.x, 0x130, 0xf, 0xf, false); }
 
 int main(int argc, char **argv) {
@@ -484,6 +571,28 @@ int main(int argc, char **argv) {
   PROBE(8, 0, "probe: UNR 8", true);
   PROBE(16, 16, "probe: interleaved slices", true);
   PROBE(16, 32, "probe: plain (not nt) store", true);
+  if (getenv("DIA_PERSIST")) {
+    const int pg = (int)((A->dia_nslices + 319) / 320);
+#define PERSIST(U, MODE, NAME, CHECK)                                                                            \
+  timeit(NAME, [&] {                                                                                            \
+    hipLaunchKernelGGL((dia_persist<40, U, MODE>), dim3(pg), dim3(512), 0, st, (const int64_t *)A->dia_sptr,    \
+                       (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,       \
+                       (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);              \
+  });                                                                                                           \
+  if (CHECK) check(NAME);
+    PERSIST(4, 0, "persist NV40 UNR4: Ap stored", true);
+    PERSIST(4, 1, "persist NV40 UNR4: Ap kept", false);
+    PERSIST(8, 0, "persist NV40 UNR8: Ap stored", true);
+    PERSIST(8, 1, "persist NV40 UNR8: Ap kept", false);
+    PERSIST(5, 1, "persist NV40 UNR5: Ap kept", false);
+    PERSIST(16, 1, "persist NV40 UNR16: Ap kept", false);
+    timeit("library spmv_dia (EpiApDot), again", [&] {
+      int P;
+      launch_spmv<double, double, int>(A, 1, SrcPlain<double>{x, 1}, EpiApDot<double>{yref, nullptr, 1}, part, &P,
+                                       nullptr, 0, st);
+    });
+    return 0;
+  }
   const int full = (int)std::min<int64_t>(65536, (A->dia_nslices + 3) / 4);  // one slice per wave
   for (int gr : {grid, 4096, full}) {
     char nm[80];
