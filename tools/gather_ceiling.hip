@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void spmv_cbc(int nb, int64_t n, int64_t ng, i
 //        latency hides behind the gathers;
 //   the products are double-buffered in LDS: one barrier per chunk.
 // The grid and the groups a block owns are the launcher's (OWN at most).
-template <int OWN, int QPT, bool PF, class Epi>
+template <int OWN, int QPT, bool PF, class Epi, bool NOROFF = false>
 __global__ __launch_bounds__(256) void spmv_cbx(int nb, int64_t n, int64_t ng, int64_t g0, int64_t g1, int own,
                                                 const int64_t *__restrict__ gptr, const uint16_t *__restrict__ roff,
                                                 const int *__restrict__ col, const double *__restrict__ val,
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void spmv_cbx(int nb, int64_t n, int64_t ng, i
 #pragma unroll
     for (int o = 0; o < OWN; ++o) {
       r0[o] = r1[o] = 0;
-      if (o < no) {
+      if (!NOROFF && o < no) {
         const int64_t s0 = gptr[(int64_t)b * ng + gb + o];
         const int len = (int)(gptr[(int64_t)b * ng + gb + o + 1] - s0);
         const int64_t row = (gb + o) * kCbRows + tid;
@@ -383,10 +383,10 @@ extern "C" int gc_run(int64_t n, int64_t nnz, const int *ip, const int *ix, cons
     variant(0, spmv_cbx<16, 1, false, E>, 1024, 16);
     variant(1, spmv_cbx<16, 1, true, E>, 1024, 16);
     variant(2, spmv_cbx<16, 2, false, E>, 768, 16);
-    variant(3, spmv_cbx<16, 2, true, E>, 512, 16);
+    variant(3, spmv_cbx<16, 1, false, E, true>, 1024, 16);  // no row offsets (wrong y): their cost
     variant(4, spmv_cbx<8, 1, true, E>, 1280, 8);
     variant(5, spmv_cbx<8, 2, true, E>, 768, 8);
-    variant(6, spmv_cbx<4, 2, true, E>, 1024, 4);
+    variant(6, spmv_cbx<16, 1, true, E, true>, 1024, 16);  // no row offsets, prefetch
     variant(7, spmv_cbx<16, 1, true, E>, 768, 16);
     hipFree(yc_d);
   }

@@ -55,8 +55,8 @@ def run(lib, A, reps=20):
 
 
 # spmv_cbx<OWN, QPT, PF> at a grid (tools/gather_ceiling.hip, gc_run's variant table)
-CBX = ["own16_q1_grid1024", "own16_q1_pf_grid1024", "own16_q2_grid768", "own16_q2_pf_grid512",
-       "own8_q1_pf_grid1280", "own8_q2_pf_grid768", "own4_q2_pf_grid1024", "own16_q1_pf_grid768"]
+CBX = ["own16_q1_grid1024", "own16_q1_pf_grid1024", "own16_q2_grid768", "own16_q1_grid1024_no_row_offsets",
+       "own8_q1_pf_grid1280", "own8_q2_pf_grid768", "own16_q1_pf_grid1024_no_row_offsets", "own16_q1_pf_grid768"]
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_gather_ceiling.json")
