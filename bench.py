@@ -54,16 +54,17 @@ def spmv_S(n, nnz, k=1, vb=8, ib=4, mvb=None):
     return nnz * (mvb + ib) + (n + 1) * ib + 2 * n * k * vb
 
 
-def image_bytes_k1(layout, n, nnz, vectors=2):
+def image_bytes_k1(layout, n, nnz, vectors=2, vb=8):
     """Bytes a k = 1 SpMV must move on the image launch_spmv picks:
     (kernel, bytes, formula). `vectors` n-vectors of 8 B beside the matrix
-    (2: x read, y written; GMRES's epilogue also reads V_0: 3)."""
+    (2: x read, y written; GMRES's epilogue also reads V_0: 3); `vb` the
+    matrix value bytes (DIA image; 8 on the other images' callers)."""
     v = vectors * n * 8
     vt = f"{vectors}*n*8"
     if layout["dia"]:
         ds = layout["dia_slots"]
-        return ("spmv_dia_kernel", ds * 8 + ds / 128 * 20 + v,
-                f"dia_slots*8 + dia_slots/128*20 + {vt}")
+        return ("spmv_dia_kernel", ds * vb + ds / 128 * 20 + v,
+                f"dia_slots*{vb} + dia_slots/128*20 + {vt}")
     if layout.get("col_blocks", 0):
         nb = layout["col_blocks"]
         ng = (n + 255) // 256
@@ -316,7 +317,40 @@ def run_cg_config(A_host, B, steps, warmup=5):
     t = time.perf_counter() - t0
     k = 1 if B.ndim == 1 else B.shape[1]
     return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "rhs": k, "n": A.n, "nnz": A.nnz,
-            "persistent_loop": chunk == 256}
+            "persistent_loop": chunk == 256, "layout": A.layout()}
+
+
+def run_cfg2(steps=200, warmup=10):
+    """BASELINE cfg2: CG on Poisson 1000^2 (n = 1e6), b = ones, tol = 0. The
+    default path is the persistent loop (cg_persist_kernel: a whole chunk of
+    iterations in one launch, y, Ap and p's gathers on chip), so the roofline
+    is the iteration's: the bytes that loop must move per iteration over the
+    measured time per iteration. It is bound by its two grid-wide exchanges
+    per iteration (the reference's two dependent inner products), not by HBM:
+    frac says how far."""
+    from krylov_amd import problems
+
+    P = problems.poisson2d(1000)
+    r = run_cg_config(P, np.ones(P.shape[0]), steps, warmup)
+    lay, n = r.pop("layout"), r["n"]
+    t_it = r["us_per_it"] * 1e-6
+    if r["persistent_loop"]:
+        slots, slices = lay["slots"], lay["slices"]
+        b = slots * (8 + 2) + slots / 64 * 4 + slices * 12 + 3 * n * 8
+        form = ("slots*(8+2) + slots/64*4 + slices*12 (compact SELL-64 image) + 3*n*8 (p read once, r and p "
+                "written; y, Ap and the partials stay on chip)")
+        kern = "cg_persist_kernel (one launch per chunk of iterations)"
+    else:
+        kern, b, form = image_bytes_k1(lay, n, r["nnz"])
+        b += 7 * n * 8
+        form += " + 7*n*8 (update)"
+    r["config"] = "BASELINE cfg2: CG on Poisson 1000^2, b = ones, tol = 0"
+    r["roofline"] = {"bound": "hbm", "achieved": b / t_it / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": b / t_it / 1e9 / HBM_PEAK_GBS, "kernel": kern, "bytes_per_iteration": b,
+                     "bytes_formula": form, "ms_per_iteration": 1e3 * t_it,
+                     "note": "latency-bound: two grid-wide exchanges per iteration; PMC 74.8 MB per iteration "
+                             "(profiles/r01_pmc_cfg2.json)"}
+    return r
 
 
 def run_gmres(R=None, label="cfg3 random nonsym n=2e6, GMRES(30) mgs, one cycle", ceiling_key=None):
@@ -466,8 +500,12 @@ def run_end_to_end(A_host, steps):
 
 
 def run_minres_cfg5(steps=100):
+    """BASELINE cfg5: MINRES on the shifted, row-scaled 3-D Laplacian 200^3
+    (fp32 matrix, W-weighted inner with float64 w, so float64 vectors as in
+    the reference), 100 fixed iterations. Then one more pass of 64 with HIP
+    events around every SpMV and update launch: each kernel's roofline."""
     import krylov_amd
-    from krylov_amd import _helpers, problems
+    from krylov_amd import _helpers, _lib, problems
     from krylov_amd.device import get_context
     from krylov_amd.minres import _MinresState
 
@@ -480,16 +518,36 @@ def run_minres_cfg5(steps=100):
     st.set_criterion(np.zeros(1))
     st.run(5)
     ctx.synchronize()
+
+    def iterate(k):
+        done = 0
+        while done < k:
+            hist, inv = st.run(min(32, k - done))
+            assert len(hist) == min(32, k - done) and not inv, "MINRES stopped early"
+            done += len(hist)
+
     t0 = time.perf_counter()
-    done = 0
-    while done < steps:
-        hist, inv = st.run(min(32, steps - done))
-        assert len(hist) == min(32, steps - done) and not inv, "MINRES stopped early"
-        done += len(hist)
+    iterate(steps)
     ctx.synchronize()
     t = time.perf_counter() - t0
-    return {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "n": W.shape[0], "nnz": int(W.nnz),
-            "config": "cfg5 shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights (vectors f64 as in the reference)"}
+    prof = profiled(ctx, [_lib.PROF_SPMV, _lib.PROF_UPDATE], lambda: iterate(64))
+    (ns, ms_s), (nu, ms_u) = prof[_lib.PROF_SPMV], prof[_lib.PROF_UPDATE]
+    n, nnz = W.shape[0], int(W.nnz)
+    kname, sb, sform = image_bytes_k1(A.layout(), n, nnz, vectors=3, vb=4)
+    ub = 8 * n * 8 + n * 8
+    out = {"it_per_s": steps / t, "us_per_it": 1e6 * t / steps, "n": n, "nnz": nnz,
+           "config": "BASELINE cfg5: MINRES on the shifted 3-D Laplacian 200^3, fp32 matrix, f64 weights "
+                     "(vectors f64 as in the reference), 100 fixed iterations",
+           "spmv": hbm_roofline(kname + " (EpiLanczos)", sb, ms_s / max(ns, 1) / 1e3,
+                                sform + " (Av = A v - h0 p_old: v read, p_old read, Av written; fp32 values)", ns),
+           "update": hbm_roofline("mr_upd_kernel (the step tail in one launch)", ub, ms_u / max(nu, 1) / 1e3,
+                                  "8*n*8 (w, p, W0, W1, yk in; z, yk, p_new out) + n*8 (weights)", nu)}
+    it_b = sb + ub
+    out["roofline"] = out["spmv"] if ms_s >= ms_u else out["update"]
+    out["iteration_roofline"] = {"bound": "hbm", "achieved": it_b / (t / steps) / 1e9, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": it_b / (t / steps) / 1e9 / HBM_PEAK_GBS,
+                                 "bytes_per_iteration": it_b, "bytes_formula": "SpMV + update (above)"}
+    return out
 
 
 PMC_SUMMARY = "r03b_pmc_traffic.json"
@@ -615,7 +673,8 @@ def main():
     ap.add_argument("--workload", choices=["metric", "cfg4"], default="metric",
                     help="headline: metric CG (1 RHS per GPU) or cfg4 block CG (8 RHS per GPU, Poisson 3163^2)")
     ap.add_argument("--quick", action="store_true", help="headline only (no other legs, no CPU baseline)")
-    ap.add_argument("--configs", action="store_true", help="also time the secondary BASELINE configs (cfg2, cfg4, cfg5)")
+    ap.add_argument("--configs", action="store_true",
+                    help="also time cfg4 as a plain 8-RHS block CG (and cfg2 / cfg5 under --quick; the full run has them)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -719,14 +778,18 @@ def main():
         out["gmres_metric_restarted"]["vs_single_cycle"] = (out["gmres_metric_restarted"]["cycle_ms"]
                                                             / out["gmres_metric"]["cycle_ms"])
         out["end_to_end"] = run_end_to_end(A_host, args.steps)
+        out["cfg2"] = run_cfg2()
+        out["cfg5"] = run_minres_cfg5()
     if world == 1 and args.configs:
         extra = {}
-        extra["cfg2_cg_poisson1000"] = run_cg_config(problems.poisson2d(1000), np.ones(1_000_000), 200, 10)
         P3 = problems.poisson2d(3163)
         B = np.random.default_rng(0).standard_normal((P3.shape[0], 8))
         extra["cfg4_blockcg_8rhs_per_gpu"] = run_cg_config(P3, B, 20, 3)
+        extra["cfg4_blockcg_8rhs_per_gpu"].pop("layout")
         del P3, B
-        extra["cfg5_minres_fp32_weighted"] = run_minres_cfg5()
+        if args.quick:
+            extra["cfg2"] = run_cfg2()
+            extra["cfg5"] = run_minres_cfg5()
         out["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu and not args.quick and args.workload == "metric":
         out["cpu_baseline"] = cpu_baseline(A_host)
