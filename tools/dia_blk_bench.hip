@@ -587,6 +587,100 @@ __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr,
   if (tid < K) part[(int64_t)g * K + tid] = red[tid];
 }
 
+// Column-major block vectors (round 4 probe): the k columns of p and Ap
+// stored one after another (column c at c * ns, ns = n rounded up), so the
+// block SpMV is the single-RHS DIA kernel's access pattern k times over one
+// value load: lane l owns rows 2l, 2l + 1 of the wave's slice, and per slot
+// column makes ONE 16-B value load and k 16-B x loads (one per column), all
+// coalesced 1 KB runs, against k/CPL... = 8 value loads of 8 B replicated
+// over a row's lanes plus 8 x runs in the row-major kernel. Each (row,
+// column) sums its slot columns in ascending order from 0: the same
+// roundings, bitwise the library's Ap. UNR slot columns' loads in flight.
+template <int UNR>
+__global__ __launch_bounds__(256) void dia_cm(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                              const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                              const double *__restrict__ val, int64_t nslices, int64_t n, int64_t ns,
+                                              const double *__restrict__ x, double *__restrict__ y,
+                                              double *__restrict__ part) {
+  __shared__ double red[256 * K];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t s = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 4 + wid;
+  double dacc[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) dacc[c] = 0.0;
+  if (s < nslices) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * kDiaSlice + 2 * lane;
+    const int64_t c0 = base / kDiaSlice;
+    const int *mo = doff + c0;
+    const uint64_t *mk = dmask + 2 * c0;
+    const double *cv = val + base + 2 * lane;
+    double acc[K][2];
+#pragma unroll
+    for (int c = 0; c < K; ++c) acc[c][0] = acc[c][1] = 0.0;
+    for (int j0 = 0; j0 < w; j0 += UNR) {
+      int off[UNR];
+      uint64_t me[UNR], md[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        off[u] = mo[j0 + u];
+        me[u] = mk[2 * (j0 + u)];
+        md[u] = mk[2 * (j0 + u) + 1];
+      }
+      d2v a[UNR], xv[UNR][K];
+      bool on0[UNR], on1[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        a[u] = j0 + u < w ? __builtin_nontemporal_load(reinterpret_cast<const d2v *>(cv + (int64_t)(j0 + u) * kDiaSlice))
+                          : d2v{0.0, 0.0};
+        on0[u] = j0 + u < w && ((me[u] >> lane) & 1u) != 0;
+        on1[u] = j0 + u < w && ((md[u] >> lane) & 1u) != 0;
+        const int64_t xr = (on0[u] || on1[u]) ? row + off[u] : 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) xv[u][c] = *reinterpret_cast<const d2v *>(x + (int64_t)c * ns + xr);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+          const double p0 = a[u].x * xv[u][c].x, p1 = a[u].y * xv[u][c].y;
+          const double t0 = acc[c][0] + p0, t1 = acc[c][1] + p1;
+          acc[c][0] = on0[u] ? t0 : acc[c][0];
+          acc[c][1] = on1[u] ? t1 : acc[c][1];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if (row + 1 < n) {
+        const d2v p = *reinterpret_cast<const d2v *>(x + (int64_t)c * ns + row);
+        __builtin_nontemporal_store(d2v{acc[c][0], acc[c][1]}, reinterpret_cast<d2v *>(y + (int64_t)c * ns + row));
+        dacc[c] += dterm(p.x, acc[c][0]);
+        dacc[c] += dterm(p.y, acc[c][1]);
+      } else if (row < n) {
+        const double p = x[(int64_t)c * ns + row];
+        y[(int64_t)c * ns + row] = acc[c][0];
+        dacc[c] += dterm(p, acc[c][0]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < K; ++c) red[tid * K + c] = dacc[c];
+  block_tree_reduce(red, 256 * K, K);
+  if (tid < K) part[(int64_t)blockIdx.x * K + tid] = red[tid];
+}
+
+// row-major (n x K) <-> column-major (K x ns)
+__global__ void to_cm(const double *__restrict__ a, double *__restrict__ b, int64_t n, int64_t ns) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * K; i += (int64_t)gridDim.x * blockDim.x)
+    b[(i % K) * ns + i / K] = a[i];
+}
+__global__ void from_cm(const double *__restrict__ b, double *__restrict__ a, int64_t n, int64_t ns) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * K; i += (int64_t)gridDim.x * blockDim.x)
+    a[i] = b[(i % K) * ns + i / K];
+}
+
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 3163;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -676,6 +770,41 @@ int main(int argc, char **argv) {
                          (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);              \
     });                                                                                                           \
     if (CHECK) check(nm);                                                                                         \
+  }
+  if (getenv("DIA_BLK_CM")) {  // round 4: column-major block vectors
+    const int64_t ns = (n + 63) / 64 * 64;
+    double *xcm0, *ycm0;
+    CK(hipMalloc(&xcm0, (K * ns + 128) * 8));
+    CK(hipMalloc(&ycm0, (K * ns + 128) * 8));
+    CK(hipMemset(xcm0, 0, (K * ns + 128) * 8));
+    double *xcm = xcm0 + 64, *ycm = ycm0 + 64;  // 512 B of readable slack before column 0
+    hipLaunchKernelGGL(to_cm, dim3(4096), dim3(256), 0, st, (const double *)x, xcm, n, ns);
+    const int full = (int)((A->dia_nslices + 3) / 4);
+#define CM(U, NAME)                                                                                                 \
+  {                                                                                                                 \
+    timeit(NAME, [&] {                                                                                              \
+      hipLaunchKernelGGL((dia_cm<U>), dim3(full), dim3(256), 0, st, (const int64_t *)A->dia_sptr,                   \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,        \
+                         (const double *)A->dia_val, A->dia_nslices, n, ns, (const double *)xcm, ycm, part);       \
+    });                                                                                                             \
+    hipLaunchKernelGGL(from_cm, dim3(4096), dim3(256), 0, st, (const double *)ycm, y, n, ns);                      \
+    check(NAME);                                                                                                    \
+  }
+    for (int rep = 0; rep < 2; ++rep) {
+      timeit("library spmv_dia_blk (EpiApDot), again", [&] {
+        int P;
+        launch_spmv<double, double, int>(A, K, SrcPlain<double>{x, K}, EpiApDot<double>{yref, nullptr, K}, part,
+                                         &P, nullptr, 0, st);
+      });
+      CM(1, "column-major, UNR 1");
+      CM(2, "column-major, UNR 2");
+      CM(3, "column-major, UNR 3");
+      CM(5, "column-major, UNR 5");
+    }
+    timeit("floor: p read + Ap write (16 B/lane copy)", [&] {
+      hipLaunchKernelGGL(copy_floor, dim3(8192), dim3(256), 0, st, (const d2v *)x, (d2v *)y, n * K / 2);
+    });
+    return 0;
   }
   if (getenv("DIA_BLK_LDS")) {  // round 4: the near-diagonal x window (and values) through LDS
     const int full = (int)((A->dia_nslices + 3) / 4);
