@@ -594,8 +594,11 @@ __global__ __launch_bounds__(256) void dia_lds(const int64_t *__restrict__ sptr,
 // column makes ONE 16-B value load and k 16-B x loads (one per column), all
 // coalesced 1 KB runs, against k/CPL... = 8 value loads of 8 B replicated
 // over a row's lanes plus 8 x runs in the row-major kernel. Each (row,
-// column) sums its slot columns in ascending order from 0: the same
-// roundings, bitwise the library's Ap. UNR slot columns' loads in flight.
+// column) sums its slot columns in ascending order from 0, as the library
+// does; UNR slot columns' loads in flight. A timing probe only: its output,
+// transposed back, did not match the library's Ap in the one run made
+// (profiles/r04_dia_blk_colmajor_probe.txt), and that was not chased, the
+// timing having already ruled the layout out.
 template <int UNR>
 __global__ __launch_bounds__(256) void dia_cm(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
                                               const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
