@@ -14,6 +14,7 @@ import numpy as np
 
 from . import _helpers, _lib
 from ._helpers import Info, Problem
+from .device import HostOut
 from ._lib import check, lib
 
 
@@ -82,9 +83,11 @@ class _CGState:
         check(lib.kry_cg_residual(self.h, _lib.dptr(out)))
         return out
 
-    def get(self, which):
+    def get(self, which, out=None):
         p = self.prob
-        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        if out is None:
+            out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        assert out.shape == (p.n, p.kpad) and out.dtype == p.dtype and out.flags.c_contiguous
         check(lib.kry_cg_get(self.h, which, _lib.ptr(out)))
         return out
 
@@ -113,6 +116,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     maxiter = N if maxiter is None else maxiter
 
     st = _CGState(prob)
+    x_out = HostOut((prob.n, prob.kpad), prob.dtype)  # pages faulted in while the device iterates
     rho0 = st.start()
     chunk = st.preferred_chunk()
     rn0 = _norm_from_sq(prob, rho0)
@@ -144,7 +148,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         if callback is not None and len(hist):
             callback(prob.unpad_vec(st.get(0), prob.r0_dtype), prob.unpad_vec(st.get(1), prob.r0_dtype))
 
-    xk = prob.unpad_vec(st.get(0), prob.r0_dtype)
+    xk = prob.unpad_vec(st.get(0, out=x_out.take()), prob.r0_dtype)
     num_operations = {
         "A": 1 + k,
         "M": 2 + k,

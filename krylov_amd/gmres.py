@@ -13,6 +13,7 @@ import numpy as np
 
 from . import _helpers, _lib
 from ._helpers import Info, Problem
+from .device import HostOut
 from ._lib import check, lib
 
 
@@ -101,9 +102,11 @@ class _GmresState:
         """xk (after solution()) into a DeviceVector, device to device."""
         check(lib.kry_gmres_xk_device(self.h, vec.handle))
 
-    def xk(self):
+    def xk(self, out=None):
         p = self.prob
-        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        if out is None:
+            out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        assert out.shape == (p.n, p.kpad) and out.dtype == p.dtype and out.flags.c_contiguous
         check(lib.kry_gmres_get(self.h, 0, _lib.ptr(out)))
         return p.unpad_vec(out, p.r0_dtype)
 
@@ -169,7 +172,8 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
     st = _GmresState(prob, maxiter, sweeps)
-    success, xk, k, resnorms = _cycle(prob, st, maxiter, tol, atol, callback)
+    host_out = HostOut((prob.n, prob.kpad), prob.dtype)  # pages faulted in while the device iterates
+    success, xk, k, resnorms = _cycle(prob, st, maxiter, tol, atol, callback, host_out=host_out)
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=_num_operations(k))
 
 
@@ -200,7 +204,8 @@ def _num_operations(k):
     }
 
 
-def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_in=None, x_out=None, host_x=True):
+def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_in=None, x_out=None, host_x=True,
+           host_out=None):
     """One ``gmres`` call's loop (gmres.py:150-251) on the device state ``st``.
 
     ``tol_of_r0`` (restarts) maps the device's initial residual norm
@@ -208,7 +213,8 @@ def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_in=None, x_
     Restarts keep the iterate on the device: ``x_in`` (a DeviceVector) is x0
     instead of the problem's own, ``x_out`` receives xk device to device (it
     may be ``x_in``), and the host copy of xk is made only if ``host_x`` (else
-    the returned xk is None). Returns ``(success, xk, numsteps, resnorms)``."""
+    the returned xk is None), into ``host_out`` (a ``HostOut``) when given.
+    Returns ``(success, xk, numsteps, resnorms)``."""
     rn0 = st.start(x_in)
     resnorms = [prob.colvals(rn0)]
 
@@ -264,7 +270,7 @@ def _cycle(prob, st, maxiter, tol, atol, callback, tol_of_r0=None, x_in=None, x_
         xk = host_x0() if host_x else None
     else:
         solve()
-        xk = st.xk() if host_x else None
+        xk = st.xk(out=host_out.take() if host_out is not None else None) if host_x else None
     return success, xk, k, resnorms
 
 
@@ -323,16 +329,17 @@ def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycle
 
     st = _GmresState(prob, restart, sweeps)
     x_buf = DeviceVector(prob.ctx, prob.n, prob.kpad, prob.dtype)
+    host_out = HostOut((prob.n, prob.kpad), prob.dtype)  # the final x's pages, faulted in during the cycles
     x_cur = prob.x0_dev  # None: x0 = 0 on the device, nothing uploaded
     infos = []
     x = None
     for c in range(max_cycles):
         last = c == max_cycles - 1
         success, xk, k, resnorms = _cycle(prob, st, restart, tol, atol, callback, tol_of_r0=tol_of_r0,
-                                          x_in=x_cur, x_out=x_buf, host_x=last)
+                                          x_in=x_cur, x_out=x_buf, host_x=last, host_out=host_out)
         x_cur = x_buf
         if success and xk is None:
-            xk = prob.unpad_vec(x_buf.to_host(), prob.r0_dtype)
+            xk = prob.unpad_vec(x_buf.to_host(out=host_out.take()), prob.r0_dtype)
         infos.append(Info(success, xk, k, resnorms, num_operations=_num_operations(k)))
         x = xk
         if success:

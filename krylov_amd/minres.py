@@ -9,6 +9,7 @@ import numpy as np
 
 from . import _helpers, _lib
 from ._helpers import Info, Problem
+from .device import HostOut
 from ._lib import check, lib
 
 
@@ -53,9 +54,11 @@ class _MinresState:
         check(lib.kry_minres_residual(self.h, _lib.dptr(out)))
         return out
 
-    def xk(self):
+    def xk(self, out=None):
         p = self.prob
-        out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        if out is None:
+            out = np.empty((p.n, p.kpad), dtype=p.dtype)
+        assert out.shape == (p.n, p.kpad) and out.dtype == p.dtype and out.flags.c_contiguous
         check(lib.kry_minres_get(self.h, 0, _lib.ptr(out)))
         return p.unpad_vec(out, p.r0_dtype)
 
@@ -114,6 +117,7 @@ def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1
     maxiter = N if maxiter is None else maxiter
 
     st = _MinresState(prob)
+    host_out = HostOut((prob.n, prob.kpad), prob.dtype)  # pages faulted in while the device iterates
     rn0 = st.start()
     first = prob.colvals(rn0)
     if callback is not None:
@@ -141,7 +145,7 @@ def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1
         if callback is not None and len(hist):
             callback(st.xk(), np.array(resnorms[-1]))
 
-    xk = st.xk()
+    xk = st.xk(out=host_out.take())
     num_operations = {
         "A": 1 + k,
         "M": 2 + k,
