@@ -264,10 +264,10 @@ int kry_cg_update_path(kry_cg *s, int32_t *info);
  * bitwise the per-step updates): *D = the steps per flush this solver uses
  * (0 = one update per step; decided at the first kry_cg_run), *bytes = the
  * device memory its D ring buffers of p and the alpha ring hold until
- * kry_cg_destroy. Default: D = 7 when an n x k vector exceeds 128 MB and
- * the ring fits an eighth of the device's total memory (3 if only that
- * fits), else 0; KRY_CG_YDEFER = D overrides; an allocation failure falls
- * back to D = 0. */
+ * kry_cg_destroy. Default, when an n x k vector exceeds 128 MB: the
+ * deepest D of 31, 15, 7, 3 whose ring fits an eighth of the device's total
+ * memory, else 0; KRY_CG_YDEFER = D (1..31) overrides; an allocation failure
+ * falls back to D = 0. */
 int kry_cg_defer_info(kry_cg *s, int32_t *D, int64_t *bytes);
 int kry_cg_residual(kry_cg *s, double *resnorm);
 int kry_cg_get(kry_cg *s, int which, void *host);

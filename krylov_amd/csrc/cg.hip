@@ -77,7 +77,7 @@ struct kry_cg {
   // cg_yflush at the chunk's end), p_i in pring[i % (ydefer + 1)] within a
   // chunk (pring[0] is p). ydefer = -1 undecided, 0 not used.
   int ydefer = -1;
-  void *pring[8] = {};
+  void *pring[33] = {};  // [1 .. ydefer] allocated (kCgYDeferMax = 31 at most)
   double *alpha_ring = nullptr;  // ydefer x k: alpha of step j at row j % ydefer
   int64_t ydefer_bytes = 0;      // what the rings hold (kry_cg_defer_info)
 };
@@ -87,7 +87,8 @@ namespace {
 enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_RHO_OLD = 6, S_COUNT = 7 };
 
 constexpr int kCgUpdateGrid = 1024;  // update-pass blocks: the <r, r> partials every yp block re-reduces
-constexpr int kCgYDefer = 7;         // deferred yk updates per flush (KRY_CG_YDEFER; 3 when memory is short)
+constexpr int kCgYDefer = 7;         // deferred yk updates per flush: the policy tries 31, 15, 7, 3 (KRY_CG_YDEFER)
+constexpr int kCgYDeferMax = 31;     // the ring holds at most 32 p buffers
 
 template <typename V>
 struct OpCgUpdate {
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void cg_yp_kernel(int64_t N, int k, V *__re
 // against 5 per step.
 template <typename V>
 struct PRing {
-  V *s[8];
+  V *s[kCgYDeferMax + 1];
 };
 
 template <typename V, typename S>
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   __shared__ double red[kBlock];
-  __shared__ double sh_a[8][kMaxCols];  // alpha of the flushed steps, oldest first
+  __shared__ double sh_a[kCgYDeferMax][8];  // alpha of the flushed steps, oldest first (k <= 8 on this path)
   __shared__ double sh_om[kMaxCols], rn[kMaxCols];
   __shared__ int flag;
   const int tid = threadIdx.x;
@@ -1257,13 +1258,24 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     // smaller y / p stay cache-resident between the passes, and reading the
     // ring's older p vectors back costs more than the y pass it saves: metric
     // CG, 80 MB vectors, 3,016 -> 2,874 it/s with D = 7; cfg4, 640 MB, 690 ->
-    // 748 it/s), with the D ring buffers within an eighth of the device's
-    // TOTAL memory (a fixed policy: the path does not depend on what other
-    // allocations happen to leave free); an allocation failure falls back to
-    // one update per step
+    // 748 it/s at D = 7, 731 -> 757 it/s from D = 7 to D = 31 on one box:
+    // the flush reads D + 2 vectors every D steps), the deepest ring of 31,
+    // 15, 7 or 3 whose D buffers fit an eighth of the device's TOTAL memory
+    // (a fixed policy: the path does not depend on what other allocations
+    // happen to leave free; cfg4 at D = 31: 19.8 GB of 288); an allocation
+    // failure falls back to one update per step
     const bool big = vb > (size_t(128) << 20);
-    int D = e ? atoi(e) : !big ? 0 : (kCgYDefer * vb <= tot / 8 ? kCgYDefer : (3 * vb <= tot / 8 ? 3 : 0));
-    if (D >= 1 && D <= 7 && k <= 8 && !s->M) {
+    int D = 0;
+    if (e) {
+      D = atoi(e);
+    } else if (big) {
+      for (int d : {kCgYDeferMax, 15, kCgYDefer, 3})
+        if ((size_t)d * vb <= tot / 8) {
+          D = d;
+          break;
+        }
+    }
+    if (D >= 1 && D <= kCgYDeferMax && k <= 8 && !s->M) {
       try {
         for (int q = 1; q <= D; ++q) s->pring[q] = dev_alloc(vb);
         s->alpha_ring = static_cast<double *>(dev_alloc((size_t)D * k * 8));
@@ -1420,9 +1432,9 @@ static void cg_free(kry_cg *s) {
   void *bufs[] = {s->b,    s->x0,   s->y,     s->r,    s->p,    s->Ap,       s->z,
                   s->t,    s->xk,   s->rt,    s->w,    s->part, s->scal,     s->hist,
                   s->ctrl, s->gbuf, s->gcrit, s->rs,   s->pb,   s->pb2,      s->yb,
-                  s->cgp_scal, s->cgp_words, s->upd_words, s->alpha_ring,
-                  s->pring[1], s->pring[2], s->pring[3], s->pring[4], s->pring[5], s->pring[6], s->pring[7]};
+                  s->cgp_scal, s->cgp_words, s->upd_words, s->alpha_ring};
   for (void *b : bufs) dev_free(b);
+  for (int q = 1; q <= kCgYDeferMax; ++q) dev_free(s->pring[q]);
 }
 
 extern "C" {

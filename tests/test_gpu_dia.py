@@ -249,7 +249,7 @@ def test_dia_block_cg_matches_lane_group_and_oracle(golden, monkeypatch):
         np.testing.assert_allclose(np.asarray(got.resnorms)[:-1], ref[:-1], rtol=1e-10)
 
 
-@pytest.mark.parametrize("D", [1, 3, 7])
+@pytest.mark.parametrize("D", [1, 3, 7, 15, 31])
 @pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general", "Ml"])
 def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
     """Block CG with yk += alpha p deferred and applied D steps at a time
