@@ -357,3 +357,26 @@ def test_single_rhs_cg_deferred_y_bitwise(path, monkeypatch):
     assert info1.numsteps == info0.numsteps and info1.success == info0.success
     _bits_equal(np.asarray(info1.resnorms), np.asarray(info0.resnorms))
     _bits_equal(info1.xk, info0.xk)
+
+
+def test_block_cg_default_ring_depth(monkeypatch):
+    """The deferral policy without an override: an n x k block above 128 MB
+    (Poisson 1500^2 x 8 columns, 144 MB) defers yk 31 steps at a time, its
+    ring of 31 p buffers and 31 x k alphas reported by kry_cg_defer_info;
+    a block below 128 MB does not defer."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+
+    monkeypatch.delenv("KRY_CG_YDEFER", raising=False)
+    for m, want in ((1500, 31), (1000, 0)):
+        P = problems.poisson2d(m)
+        B = np.random.default_rng(m).standard_normal((P.shape[0], 8))
+        st = _CGState(_helpers.Problem(krylov_amd.CsrOperator(P), B, None, None))
+        st.start()
+        st.set_criterion(np.zeros(8))
+        assert len(st.run(2)) == 2
+        D, nbytes = st.defer_info()
+        assert D == want
+        vb = (P.shape[0] * 8 + 15) // 16 * 16 * 8
+        assert nbytes == (D * vb + D * 8 * 8 if D else 0)
