@@ -1849,6 +1849,7 @@ int kry_gmres_xk_device(kry_gmres *s, kry_vec *out) {
   KRY_REQUIRE(s, KRY_EINVAL, "null solver");
   KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
   check_vec(out, s->n, s->k, s->dtype, "out");
+  KRY_REQUIRE(out->ctx && out->ctx->device == s->ctx->device, KRY_EINVAL, "out: a vector on another device");
   KRY_HIP(hipSetDevice(s->ctx->device));
   KRY_HIP(hipMemcpyAsync(out->d, s->xk, out->bytes(), hipMemcpyDeviceToDevice, s->ctx->stream));
   KRY_API_END
