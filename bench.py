@@ -277,8 +277,8 @@ def cfg4_rooflines(res, steps):
     iteration's, on the bytes the kernels must move: SpMV (values, the
     per-slot-column descriptors, p read, Ap written), the r pass (r, Ap in;
     r out), the p pass (r, p_i in; p_{i+1} out) and, with yk deferred D steps,
-    once per D steps y in and out and the D older p vectors in (D = 0: the
-    fused y / p pass, r, y, p in and y, p out)."""
+    once per D steps y in and out and the D - 1 older p vectors in (p_i is
+    the pass's own; D = 0: the fused y / p pass, r, y, p in and y, p out)."""
     from krylov_amd import _lib
 
     n, k = res["n"], res["rhs"]
@@ -291,13 +291,14 @@ def cfg4_rooflines(res, steps):
                         sb, ms / max(cnt, 1) / 1e3,
                         "dia_slots*8 + dia_slots/128*20 + 2*n*k*8 (values, descriptors, p read, Ap written)", cnt)
     D = res["ydefer"][0]
-    pass_b = 3 * vec + 3 * vec + ((D + 2) / D * vec if D else 2 * vec)
+    pass_b = 3 * vec + 3 * vec + ((D + 1) / D * vec if D else 2 * vec)
     it_b = sb + pass_b
     t_it = res["elapsed"] / steps
     return spmv, {"bound": "hbm", "achieved": it_b / t_it / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": it_b / t_it / 1e9 / HBM_PEAK_GBS, "bytes_per_iteration": it_b, "ydefer": D,
                   "bytes_formula": "SpMV (above) + 3*n*k*8 (r pass) + 3*n*k*8 (p pass) + "
-                                   + ("(D+2)/D*n*k*8 (yk flush every D steps)" if D else "2*n*k*8 (y in the y/p pass)")}
+                                   + ("(D+1)/D*n*k*8 (yk flush every D steps: y in and out, the D-1 older p in)"
+                                      if D else "2*n*k*8 (y in the y/p pass)")}
 
 
 def run_cg_config(A_host, B, steps, warmup=5):
