@@ -76,10 +76,10 @@ class HostOut:
     iterates. A fresh numpy array of 80 MB (the metric's x) otherwise pays its
     pages' first-touch zeroing inside the download: 3.8 ms against the 1.45 ms
     of the copy itself (tools/xfer_bench.hip, profiles/r04_xfer_probe.txt).
-    Below MIN_BYTES the array is plain. ``take()`` joins the helper and
+    Below MIN_BYTES (8 MiB) the array is plain. ``take()`` joins the helper and
     returns the array; the download then overwrites every element."""
 
-    MIN_BYTES = 16 << 20
+    MIN_BYTES = 8 << 20
 
     def __init__(self, shape, dtype):
         self.a = np.empty(shape, dtype=dtype)

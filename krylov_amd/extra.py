@@ -23,7 +23,7 @@ import numpy as np
 from . import _helpers, _lib
 from ._helpers import Info, Problem
 from ._lib import check, lib
-from .device import DeviceVector
+from .device import DeviceVector, HostOut
 
 LC_AXPY, LC_NEST_ADD, LC_NEST_SUB, LC_DIV, LC_SUB, LC_ADD, LC_COPY, LC_SCALE = range(8)
 SOP_COPY, SOP_DIVG, SOP_MULDIVG, SOP_SQRT, SOP_GUARD, SOP_SET = range(6)
@@ -36,6 +36,7 @@ class _Dev:
         self.prob = prob
         self.ctx = prob.ctx
         self.w = prob.w_dev
+        self.out = HostOut((prob.n, prob.kpad), prob.dtype)  # the returned iterate's pages, faulted in meanwhile
 
     def zeros(self):
         v = DeviceVector(self.ctx, self.prob.n, self.prob.kpad, self.prob.dtype)
@@ -48,6 +49,10 @@ class _Dev:
 
     def host(self, v):
         return self.prob.unpad_vec(v.to_host(), self.prob.r0_dtype)
+
+    def host_final(self, v):
+        """The returned iterate, into the array allocated at the start."""
+        return self.prob.unpad_vec(v.to_host(out=self.out.take()), self.prob.r0_dtype)
 
     def matvec(self, op, x):
         """op @ x into a new vector; op None = the reference's Identity (x itself)."""
@@ -265,7 +270,7 @@ def bicgstab(A, b, Ml=None, Mr=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15
             resnorms[-1] = D.cols(mid)
             success = True
             break
-    xk = D.host(x)
+    xk = D.host_final(x)
     return xk if success else None, Info(success, xk, k, resnorms)
 
 
@@ -329,7 +334,7 @@ def cgs(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None,
                 callback(D.host(x), D.host(r))
             resnorms.append(D.cols(row))
             k += 1
-    xk = D.host(x)
+    xk = D.host_final(x)
     return xk if success else None, Info(success, xk, k, resnorms)
 
 
@@ -395,7 +400,7 @@ def cgr(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None,
                 callback(D.host(x), D.host(r))
             resnorms.append(D.cols(row))
             k += 1
-    xk = D.host(x)
+    xk = D.host_final(x)
     return xk if success else None, Info(success, xk, k, resnorms)
 
 
@@ -468,5 +473,5 @@ def gcr(A, b, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callbac
                 callback(D.host(x), D.host(r))
             resnorms.append(D.cols(row))
             k += 1
-    xk = D.host(x)
+    xk = D.host_final(x)
     return xk if success else None, Info(success, xk, k, resnorms)

@@ -7,7 +7,7 @@ import numpy as np
 def test_hostout_large_is_prefaulted_and_usable():
     from krylov_amd.device import HostOut
 
-    h = HostOut((3_000_000, 1), np.float64)  # 24 MB: above MIN_BYTES, so a helper thread runs
+    h = HostOut((3_000_000, 1), np.float64)  # 24 MB: above MIN_BYTES (8 MiB), so a helper thread runs
     assert h._t is not None
     a = h.take()
     assert h._t is None and a.shape == (3_000_000, 1) and a.dtype == np.float64 and a.flags.c_contiguous
