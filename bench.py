@@ -639,6 +639,7 @@ def run_spmv_general(A_host, steps):
     n, nnz = A_host.shape[0], int(A_host.nnz)
     roof = roofline_of(res, n, nnz, pmc_traffic(n, nnz, spmv_kernel_desc(res["layout"], n)[0]))
     roof["cg_it_per_s"] = steps / res["elapsed"]
+    roof["n"], roof["nnz"] = n, nnz
     return roof
 
 
@@ -656,13 +657,144 @@ def run_spmv_unstructured(A_host, steps):
     kname, sb, form = image_bytes_k1(res["layout"], n, nnz)
     roof = hbm_roofline(kname, sb, res["spmv_avg_s"], form, res["spmv_count"],
                         cg_it_per_s=steps / res["elapsed"], matrix="15-point 216^3 under P A P^T, P = "
-                        "default_rng(0).permutation(n)")
+                        "default_rng(0).permutation(n)", n=n, nnz=nnz)
     cal = gather_ceiling("metric_permuted")
     if cal and kname.startswith("spmv_cb"):
         roof["gather"] = {"bound": "gather", "achieved": nnz / res["spmv_avg_s"] / 1e9, "unit": "G gathers/s",
                           "peak": cal["ceiling_g_per_s"], "frac": nnz / res["spmv_avg_s"] / 1e9 / cal["ceiling_g_per_s"],
                           "peak_source": f"profiles/{GATHER_CEILING}[metric_permuted]: " + cal["what"]}
     return roof
+
+
+TRAFFIC_INDEX = "r05_traffic_index.json"
+FORMULAS = "profiles/bench_formulas.md"
+
+
+def traffic_index():
+    """Per-leg HBM traffic per launch from the committed PMC summaries
+    (profiles/<TRAFFIC_INDEX>, built by tools/traffic_index.py from the
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes named in it): {leg: {kernel
+    key: {"bytes": B, "src": file}}}. Each entry is kept only when it was
+    taken on the same matrix (n, nnz)."""
+    try:
+        with open(os.path.join(REPO, "profiles", TRAFFIC_INDEX)) as f:
+            return json.load(f)
+    except OSError:
+        return {}
+
+
+def leg_traffic(idx, leg, key, n, nnz):
+    e = idx.get(leg, {}).get(key)
+    if not e or e.get("n") != n or e.get("nnz") != nnz:
+        return None, None
+    return e["bytes"], e["src"]
+
+
+def _r(x, d=4):
+    """Round to d significant digits (compact line)."""
+    if isinstance(x, float):
+        return float(f"{x:.{d}g}")
+    return x
+
+
+def _short(kernel):
+    """The kernel's name without template arguments or descriptions."""
+    return kernel.split("<")[0].split(" (")[0].strip()
+
+
+def _kroof(r, traffic=None, src=None):
+    """Compact form of one kernel roofline object."""
+    out = {"kernel": _short(r["kernel"]), "ms": _r(r["ms_per_launch"]), "bytes": int(r["bytes_per_launch"]),
+           "frac": _r(r["frac"], 3), "traffic": int(traffic) if traffic else r.get("traffic")}
+    if out["traffic"] and (src or r.get("traffic_source")):
+        out["traffic_src"] = (src or r.get("traffic_source", "")).split(" ")[0]
+    return out
+
+
+def compact(full, idx=None):
+    """The driver keeps only the tail of bench.py's stdout (about 8 KB), so
+    the printed line is this compact form (<= 6 KB): the contract keys, the
+    headline roofline and cpu_baseline, and per leg only its rate, its
+    dominant kernel (short name), bytes per launch, frac and HBM traffic.
+    Kernel template names and byte formulas are in profiles/bench_formulas.md
+    (FORMULAS); --full-out PATH writes the verbose line as well."""
+    idx = traffic_index() if idx is None else idx
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+    out = {k: _r(full[k]) if k in ("value", "ms_per_step") else full[k] for k in keys}
+    ro = full["roofline"]
+    out["roofline"] = {"bound": ro["bound"], "achieved": _r(ro["achieved"]), "peak": ro["peak"], "unit": ro["unit"],
+                       "frac": _r(ro["frac"], 3), "traffic": int(ro["traffic"]) if ro.get("traffic") else None,
+                       "kernel": _short(ro["kernel"]),
+                       "ms_per_launch": _r(ro["ms_per_launch"]), "bytes_per_launch": int(ro["bytes_per_launch"]),
+                       "launches_timed": ro.get("launches_timed")}
+    if ro.get("traffic_source"):
+        out["roofline"]["traffic_src"] = ro["traffic_source"].split(" ")[0]
+    it = full.get("iteration_roofline")
+    if it:
+        out["iteration_roofline"] = {"frac": _r(it["frac"], 3), "bytes": int(it.get("bytes_per_iteration", 0))}
+    legs = {}
+    c4 = full.get("cfg4_sharded")
+    if c4:
+        n, nnz = c4["n"], c4["nnz"]
+        t, src = leg_traffic(idx, "cfg4", "spmv", n, nnz)
+        legs["cfg4_sharded"] = {"it_per_s": _r(c4["it_per_s"]), "rhs_it_per_s": _r(c4["rhs_it_per_s"]),
+                                **_kroof(c4["roofline"], t, src), "iter_frac": _r(c4["iteration_roofline"]["frac"], 3),
+                                "ydefer": c4["iteration_roofline"].get("ydefer")}
+    for leg in ("spmv_general", "spmv_unstructured"):
+        r = full.get(leg)
+        if r:
+            n, nnz = r.get("n", 0), r.get("nnz", 0)
+            t, src = leg_traffic(idx, leg, "spmv", n, nnz)
+            legs[leg] = {"cg_it_per_s": _r(r.get("cg_it_per_s")), **_kroof(r, t, src)}
+            if "gather" in r:
+                legs[leg]["gather_frac"] = _r(r["gather"]["frac"], 3)
+    for leg in ("gmres", "gmres_metric"):
+        g = full.get(leg)
+        if g:
+            n, nnz = g["n"], g["nnz"]
+            ts, ss = leg_traffic(idx, leg, "spmv", n, nnz)
+            tm, sm = leg_traffic(idx, leg, "mgs", n, nnz)
+            legs[leg] = {"it_per_s": _r(g["it_per_s"]), "cycle_ms": _r(g["cycle_ms"]),
+                         "spmv": _kroof(g["spmv"], ts, ss), "mgs": _kroof(g["mgs"], tm, sm),
+                         "cycle_frac": _r(g["cycle_roofline"]["frac"], 3),
+                         "share": {k: _r(v, 3) for k, v in g["time_share"].items()}}
+            if "gather" in g["spmv"]:
+                legs[leg]["spmv"]["gather_frac"] = _r(g["spmv"]["gather"]["frac"], 3)
+    gr = full.get("gmres_metric_restarted")
+    if gr:
+        legs["gmres_metric_restarted"] = {"it_per_s": _r(gr["it_per_s"]), "cycle_ms": _r(gr["cycle_ms"]),
+                                          "vs_single_cycle": _r(gr.get("vs_single_cycle"))}
+    b = full.get("bicgstab_cfg3")
+    if b:
+        t, src = leg_traffic(idx, "bicgstab_cfg3", "spmv", b["n"], b["nnz"])
+        legs["bicgstab_cfg3"] = {"it_per_s": _r(b["it_per_s"]), **_kroof(b["roofline"], t, src)}
+    e = full.get("end_to_end")
+    if e:
+        legs["end_to_end"] = {k: _r(v) for k, v in e.items() if k != "includes"}
+    c2 = full.get("cfg2")
+    if c2:
+        r = c2["roofline"]
+        t, src = leg_traffic(idx, "cfg2", "iteration", c2["n"], c2["nnz"])
+        legs["cfg2"] = {"it_per_s": _r(c2["it_per_s"]), "kernel": _short(r["kernel"]),
+                        "ms": _r(r["ms_per_iteration"]), "bytes": int(r["bytes_per_iteration"]),
+                        "frac": _r(r["frac"], 3), "traffic": int(t) if t else None}
+        if src:
+            legs["cfg2"]["traffic_src"] = src
+    c5 = full.get("cfg5")
+    if c5:
+        ts, ss = leg_traffic(idx, "cfg5", "spmv", c5["n"], c5["nnz"])
+        tu, su = leg_traffic(idx, "cfg5", "update", c5["n"], c5["nnz"])
+        legs["cfg5"] = {"it_per_s": _r(c5["it_per_s"]), "spmv": _kroof(c5["spmv"], ts, ss),
+                        "update": _kroof(c5["update"], tu, su), "iter_frac": _r(c5["iteration_roofline"]["frac"], 3)}
+    if legs:
+        out["legs"] = legs
+    cb = full.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: (_r(cb[k]) if k == "value" else cb[k]) for k in ("value", "unit", "cores", "kind",
+                                                                                 "sample")}
+    out["formulas"] = FORMULAS
+    return out
 
 
 def main():
@@ -677,6 +809,7 @@ def main():
     ap.add_argument("--configs", action="store_true",
                     help="also time cfg4 as a plain 8-RHS block CG (and cfg2 / cfg5 under --quick; the full run has them)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--full-out", default=None, help="also write the verbose JSON line (formulas, timings) here")
     args = ap.parse_args()
 
     world, rank, local, pg = dist_setup()
@@ -758,7 +891,9 @@ def main():
             "n": c4,
             "nnz": int(P3.nnz),
             "spmv_ms": 1e3 * cfg4["spmv_avg_s"],
-            "config": "BASELINE cfg4: Poisson 3163^2 block CG, 8 RHS per GPU, one RCCL allreduce per iteration",
+            "config": "BASELINE cfg4: Poisson 3163^2 block CG, 8 RHS per GPU"
+                      + (f", {world} ranks, one RCCL allreduce per iteration" if world > 1
+                         else ", one GPU (no communicator attached at N = 1)"),
         }
         c4_spmv, c4_it = cfg4_rooflines(cfg4, min(args.steps, 40))
         out["cfg4_sharded"]["roofline"] = c4_spmv
@@ -795,7 +930,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and not args.quick and args.workload == "metric":
         out["cpu_baseline"] = cpu_baseline(A_host)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        if args.full_out:
+            with open(args.full_out, "w") as f:
+                f.write(json.dumps(out) + "\n")
+        print(json.dumps(compact(out)), flush=True)
     if pg is not None:
         pg.destroy_process_group()
 

@@ -17,9 +17,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
 # KRYLOV_LIB: load another build of the C-ABI instead, e.g. the host-only
 # sanitizer builds of the image builders (make -C krylov_amd/csrc sanitize;
-# tests/test_host_sanitize.py): entry points it lacks are then left unbound.
-HOST_ONLY = bool(os.environ.get("KRYLOV_LIB"))
-if HOST_ONLY:
+# tests/test_host_sanitize.py). Whether the loaded build is host-only is
+# decided by probing it for the device entry points (HOST_ONLY below), not by
+# the variable: another full GPU build loaded this way binds every entry point
+# and keeps the ordered teardown.
+if os.environ.get("KRYLOV_LIB"):
     LIB_PATH = os.environ["KRYLOV_LIB"]
 
 KRY_F32, KRY_F64 = 1, 2
@@ -44,6 +46,8 @@ if not os.path.exists(LIB_PATH):
     )
 
 lib = ctypes.CDLL(LIB_PATH)
+# a build without the device entry points (the host-only sanitizer builds)
+HOST_ONLY = not hasattr(lib, "kry_ctx_create")
 
 _vp = ctypes.c_void_p
 _pvp = ctypes.POINTER(ctypes.c_void_p)

@@ -419,9 +419,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   hipStream_t st = A->ctx->stream;
   const int64_t n = A->n, nnz = A->nnz;
   UploadTrace tr;
-  KRY_REQUIRE(ip[0] == 0 && (int64_t)ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
-  for (int64_t r = 0; r < n; ++r)
-    KRY_REQUIRE(ip[r + 1] >= ip[r], KRY_EINVAL, "indptr must be non-decreasing");
+  check_csr(n, nnz, ip, ix);
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
   sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);

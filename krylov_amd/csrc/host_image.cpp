@@ -44,6 +44,39 @@ static void par_fill(hvec<T> &v, size_t n, T val) {
   for (auto &x : th) x.join();
 }
 
+template <typename I>
+void check_csr(int64_t n, int64_t nnz, const I *ip, const I *ix) {
+  KRY_REQUIRE(n >= 0 && nnz >= 0 && ip, KRY_EINVAL, "bad CSR arguments");
+  KRY_REQUIRE(ip[0] == 0 && (int64_t)ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
+  KRY_REQUIRE(nnz == 0 || ix, KRY_EINVAL, "null indices");
+  const unsigned nt = n + nnz < (int64_t(1) << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::atomic<int> bad{0};  // 1: indptr decreases, 2: a column out of range
+  auto work = [&](unsigned t) {
+    const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+    for (int64_t r = r0; r < r1; ++r)
+      if (ip[r + 1] < ip[r]) {
+        bad = 1;
+        return;
+      }
+    // the rows are monotone here; the entries of [r0, r1) are [ip[r0], ip[r1])
+    const int64_t e0 = (int64_t)ip[r0], e1 = (int64_t)ip[r1];
+    for (int64_t e = e0; e < e1; ++e)
+      if (ix[e] < 0 || (int64_t)ix[e] >= n) {
+        bad = 2;
+        return;
+      }
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto &x : th) x.join();
+  }
+  KRY_REQUIRE(bad != 1, KRY_EINVAL, "indptr must be non-decreasing");
+  KRY_REQUIRE(bad != 2, KRY_EINVAL, "column index out of range [0, n)");
+}
+
 // ---------------------------------------------------------- SELL-64 layout
 // Host-side plan: slice s = rows [64 s, 64 s + 64); width = longest row;
 // a slice is irregular (CSR walk) when 64 * width > 2 * nnz_slice + 1024.
@@ -242,6 +275,7 @@ bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_s
 template <typename I>
 static void dia_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
                           int32_t *offsets, uint64_t *masks) {
+  check_csr(n, nnz, ip, ix);
   int64_t ns = 0, sell_slots = 0, irr = 0;
   sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
   hvec<double> zeros;
@@ -421,6 +455,7 @@ bool pair_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_
 template <typename I>
 static void pair_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
                            int32_t *cbase, uint16_t *deltas) {
+  check_csr(n, nnz, ip, ix);
   int64_t ns = 0, sell_slots = 0, irr = 0;
   sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
   hvec<double> zeros;
@@ -444,6 +479,7 @@ static void pair_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int
 // image is not, without a device.
 template <typename I>
 static void cb_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int64_t *gptr) {
+  check_csr(n, nnz, ip, ix);
   hvec<double> vals;
   par_fill(vals, (size_t)std::max<int64_t>(nnz, 1), 1.0);
   CbHost<double> cb;
@@ -461,6 +497,7 @@ static void cb_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64
 
 // explicit instantiations: the combinations kry_csr_create dispatches
 #define KRY_HOST_I(I)                                                                                              \
+  template void check_csr<I>(int64_t, int64_t, const I *, const I *);                                            \
   template void sell_plan<I>(int64_t, const I *, std::vector<int64_t> *, std::vector<int32_t> *, int64_t *,     \
                              int64_t *, int64_t *);                                                              \
   template bool compact_fill<I>(const std::vector<int64_t> &, const std::vector<int32_t> &, const hvec<I> &,     \

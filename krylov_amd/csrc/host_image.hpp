@@ -45,6 +45,13 @@ using hvec = std::vector<T, NoInit<T>>;
 template <class T>
 void release_later(hvec<T> &v);
 
+// Structural check of a square CSR matrix before any image is built from
+// it: indptr[0] = 0, indptr non-decreasing, indptr[n] = nnz, and every column
+// index in [0, n). Throws Error{KRY_EINVAL} otherwise (the builders index
+// host and device arrays with these values; threaded above 2^20 entries).
+template <typename I>
+void check_csr(int64_t n, int64_t nnz, const I *ip, const I *ix);
+
 // SELL-64 plan: slice s = rows [64 s, 64 s + 64); width = longest row; a
 // slice is irregular (CSR walk) when 64 * width > 2 * nnz_slice + 1024.
 template <typename I>

@@ -96,29 +96,59 @@ __device__ inline unsigned decide_exchange(unsigned *bar, unsigned tag, unsigned
   return old & 3u;
 }
 
+// One poll of a granule pair {lo, hi} = 16 B at agent scope (sc1: past the
+// CU's L1), through a wave-uniform buffer descriptor over the whole region
+// and a per-lane byte offset (no per-lane descriptors, no waterfall loop).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const unsigned long long *gr, int G) {
+  const uint64_t a = reinterpret_cast<uint64_t>(gr);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(G * 16), 0x00020000);
+}
+typedef unsigned int granule_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ granule_u4 poll_granule(__amdgpu_buffer_rsrc_t r, int b) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, b * 16, 0, 16 /* sc1 */);
+}
+
 // Wave 0 only; returns the same value in every lane (false = timed out /
 // aborted). spin_limit: ticks of wall_clock64 (kSpinLimit). AGREE: the commit / abort decision is shared by all blocks
 // (decide_exchange); otherwise a timed-out block only raises bar[9] and a
 // caller that has stored nothing yet re-checks it.
+// Round 5: each block's granule pair is read with ONE 16-B load, and a lane
+// re-polls only the pairs whose tags have not matched yet (the round-4 form
+// re-read every pair with two 8-B loads per poll). tools/xchg_probe.hip at
+// 256 blocks: 3.74 -> 3.21 us per exchange round with nothing in flight,
+// 3.4-4.6 -> 2.7-2.8 us with the MGS kernel's prefetch loads in flight
+// (profiles/r05_xchg_probe.jsonl); two-level (per-XCD) trees and 8 or 32
+// reader blocks were slower (a second hop). The values and their summation
+// order are unchanged (lane l: blocks l, l + 64, ..., then the butterfly).
 template <bool AGREE = false>
 __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out,
                                       unsigned spin_limit = kSpinLimit) {
   const int lane = threadIdx.x;
-  unsigned long long g[4][2];
+  const __amdgpu_buffer_rsrc_t rs = granule_rsrc(gr, G);
+  granule_u4 g[4];
+  bool got[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    got[i] = lane + 64 * i >= G;
+    g[i] = granule_u4{0u, 0u, 0u, 0u};
+  }
   unsigned spins = 0;
   bool expired = false;
   const unsigned long long t0 = wall_clock64();
   bool committed = false;  // AGREE: another block has committed this exchange
   for (;;) {
+    asm volatile("" ::: "memory");  // a fresh poll every round: the loads are not hoisted
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (!got[i]) g[i] = poll_granule(rs, lane + 64 * i);
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int b = lane + 64 * i;
-      if (b < G) {
-        g[i][0] = __hip_atomic_load(gr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        g[i][1] = __hip_atomic_load(gr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = ok && (unsigned)(g[i][0] >> 32) == tag && (unsigned)(g[i][1] >> 32) == tag;
-      }
+      if (!got[i]) got[i] = g[i].y == tag && g[i].w == tag;
+      ok = ok && got[i];
     }
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(1);
@@ -160,7 +190,7 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int b = lane + 64 * i;
-    if (b < G) s += __longlong_as_double((long long)((g[i][1] << 32) | (g[i][0] & 0xffffffffull)));
+    if (b < G) s += __longlong_as_double((long long)(((unsigned long long)g[i].z << 32) | (unsigned long long)g[i].x));
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);

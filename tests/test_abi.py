@@ -440,3 +440,35 @@ def test_plans_of_large_matrices_match():
     slot = sptr[rows // 128] + 128 * j + rows % 128
     np.testing.assert_array_equal(p["cbase"][slot // 128].astype(np.int64) + p["deltas"][slot], B.indices)
     assert np.count_nonzero(p["deltas"] != 0xFFFF) == B.nnz
+
+
+@pytest.mark.parametrize("defect", ["nnz_short", "nnz_long", "indptr_start", "indptr_decreasing", "col_negative",
+                                    "col_too_large"])
+@pytest.mark.parametrize("plan", ["dia", "pair", "cb"])
+def test_plans_reject_malformed_csr(plan, defect):
+    """Every host plan entry point (kry_dia_plan / kry_pair_plan /
+    kry_cb_plan) checks the CSR arrays before building anything: indptr
+    starting at 0, non-decreasing, ending at nnz = len(indices), and every
+    column in [0, n). An inconsistent pair is KRY_EINVAL (ValueError), never
+    an out-of-bounds read or write (the sanitizer runs of tests/
+    test_host_sanitize.py execute these cases too). Sizes are past the
+    checker's threading threshold."""
+    from krylov_amd import _lib, problems
+
+    A = problems.random_nonsym(1_100_000, per_row=3, seed=9)
+    ip, ix = A.indptr.astype(np.int32).copy(), A.indices.astype(np.int32).copy()
+    if defect == "nnz_short":
+        ix = ix[:-7]
+    elif defect == "nnz_long":
+        ix = np.concatenate([ix, np.zeros(5, np.int32)])
+    elif defect == "indptr_start":
+        ip[0] = 1
+    elif defect == "indptr_decreasing":
+        ip[777_777] = ip[777_778] + 2
+    elif defect == "col_negative":
+        ix[123_456] = -3
+    else:
+        ix[1_000_001] = A.shape[0]
+    fn = {"dia": _lib.dia_plan, "pair": _lib.pair_plan, "cb": _lib.cb_plan}[plan]
+    with pytest.raises(ValueError):
+        fn(ip, ix)
