@@ -77,6 +77,11 @@ def image_bytes_k1(layout, n, nnz, vectors=2, vb=8):
         ps = layout["pair_slots"]
         return ("spmv_pair_kernel", ps * (8 + 2) + ps / 128 * 4 + (n + 127) // 128 * 12 + v,
                 f"pair_slots*(8+2) + pair_slots/128*4 + slices*12 + {vt}")
+    if layout.get("rs"):
+        rs = layout["rs_slots"]
+        kname = "spmv_rs_kernel" + (" (renumbered)" if layout.get("renumbered") else "")
+        return (kname, rs * (8 + 4) + (n + 127) // 128 * 12 + v,
+                f"rs_slots*(8+4) (values + column/rank words) + slices*12 + {vt}")
     slots, slices = layout["slots"], layout["slices"]
     if layout["compact"]:
         return ("spmv_sell_kernel (compact)", slots * (8 + 2) + slots / 64 * 4 + slices * 12 + v,

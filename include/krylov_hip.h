@@ -89,6 +89,53 @@ int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr,
                    const void *indices, const void *data, int dtype, int itype,
                    kry_csr **out);
 int kry_csr_destroy(kry_csr *A);
+/* kry_csr_create with another operator's bandwidth-reducing renumbering
+ * (kry_version() >= 104): the image holds P M P^T for `like`'s permutation P
+ * (rows' entries in their stored order), so M can precondition solves with
+ * `like` (kry_*_set_preconditioners refuses operators renumbered differently).
+ * Same as kry_csr_create when `like` is not renumbered. Replaces the
+ * preconditioner operands M / Ml / Mr of cg.py:70-110, gmres.py:105-139,
+ * minres.py:95-151 for a renumbered A. */
+int kry_csr_create_like(kry_ctx *ctx, const kry_csr *like, int64_t n, int64_t nnz, const void *indptr,
+                        const void *indices, const void *data, int dtype, int itype, kry_csr **out);
+/* Renumbering (kry_version() >= 104). kry_csr_create renumbers a matrix whose
+ * columns are scattered (the column-blocked test below) but whose graph has
+ * narrow BFS levels (a mesh or stencil stored in a bad order) by reverse
+ * Cuthill-McKee; its images then hold P A P^T with every row's entries in
+ * stored order, so the SpMV stays bitwise csr_matvec. Every vector still
+ * crosses the C-ABI in the caller's numbering: kry_*_start permutes b / x0 /
+ * weights in, kry_*_get, kry_gmres_xk_device and kry_spmv permute out. The
+ * reference multiplies the caller's matrix as given (_helpers.py:44-48): this
+ * is storage order only. kry_csr_permute moves the rows of an n x k block
+ * into the operator's numbering (to_operator = 1: dst[r] = src[perm[r]]) or
+ * back (0), for callers that keep their own device vectors in the operator's
+ * numbering (kry_prog_*). KRY_RENUMBER=0 disables renumbering. */
+int kry_csr_permute(kry_ctx *ctx, const kry_csr *A, const kry_vec *src, kry_vec *dst, int to_operator);
+/* kry_spmv with x and y already in the operator's numbering (kry_csr_permute);
+ * the same as kry_spmv for an operator that is not renumbered. */
+int kry_spmv_op(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y);
+/* Host-only (no device): the reverse Cuthill-McKee order kry_csr_create
+ * would use (int32 indices): info[0..1] = built (0 = a BFS level exceeded
+ * wlimit nodes: no narrow level structure), BFS levels of the numbering;
+ * when built and perm is non-null: perm[n], new row r = old row perm[r].
+ * wlimit <= 0 takes the library's default (max(2^16, n / 32)). */
+int kry_rcm_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t wlimit,
+                 int64_t *info, int32_t *perm);
+/* The same order computed on the device (what kry_csr_create runs; int32
+ * CSR from the host, uploaded inside): info[0] = 1 built, 0 refused, -1 gave
+ * up (more than 64 components: kry_csr_create then uses the host order),
+ * info[1] = levels; perm as kry_rcm_plan's, node for node. */
+int kry_rcm_device(kry_ctx *ctx, int64_t n, int64_t nnz, const int32_t *indptr, const int32_t *indices, int64_t wlimit,
+                   int64_t *info, int32_t *perm);
+/* Host-only: the rank-sorted SELL-128 plan (kry_version() >= 104; the image a
+ * matrix takes for single-RHS SpMVs when no DIA, column-blocked or paired
+ * image is built): info[0..3] = built, slices, slots, widest slice; when built
+ * and the arrays are non-null: widths[slices], colrank[slots] (slot of row r,
+ * slot column j of its slice at 128 * (sptr[s] / 128 + j) + r - 128 s: the
+ * column in bits 0..27, its position among the run of 16 stored entries it
+ * belongs to in bits 28..31, 0xFFFFFFFF = padding). */
+int kry_rs_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                int32_t *widths, uint32_t *colrank);
 /* Host-only (no GPU needed): the SELL-64 plan kry_csr_create will build —
  * slice count, stored slots (nonzeros + padding of regular slices) and the
  * number of irregular slices (64 * width > 2 * slice_nnz + 1024) that the
@@ -139,7 +186,11 @@ int kry_cb_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices,
  * columns, at most 1.25x the SELL-64 slots; KRY_SPMV_PAIR=0 disables) and
  * that image's slot count. Fields added later go at the end, so a caller
  * built against this header keeps working (kry_version() >= 101). */
-#define KRY_CSR_INFO_LEN 9
+/* then (kry_version() >= 104) rs (1 when the rank-sorted SELL-128 image
+ * serves single-RHS SpMVs), its slot count, renumbered (1 when the images hold
+ * the reverse Cuthill-McKee renumbering P A P^T) and the renumbering's BFS
+ * level count. */
+#define KRY_CSR_INFO_LEN 13
 int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len);
 /* The version-100 form: info[0..4] only (`info` holds 5 values). */
 int kry_csr_info(const kry_csr *A, int64_t *info);
@@ -365,6 +416,12 @@ int kry_minres_get(kry_minres *s, int which, void *host);
 int kry_comm_unique_id(void *id128);
 int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id128,
                     kry_comm **out);
+/* One communicator per context of one process (ncclCommInitAll over the
+ * contexts' devices; out[i] is rank i of n), kry_version() >= 104: the
+ * single-process multi-GPU path, krylov_amd.cg / gmres / minres(...,
+ * devices=[...]), one host thread per device. Replaces the per-process
+ * ranks of SURVEY §8(e) when the caller has one process for the node. */
+int kry_comm_create_all(kry_ctx **ctxs, int32_t n, kry_comm **out);
 int kry_comm_destroy(kry_comm *c);
 /* in-place sum over ranks of `count` host doubles (setup-time exchanges) */
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);

@@ -116,7 +116,7 @@ class Problem:
             if _is_identity(op):
                 self.ops[name] = None
                 continue
-            dop = as_device_operator(op, device=self.ctx.device)
+            dop = as_device_operator(op, device=self.ctx.device, like=self.A)
             if dop.shape != self.A.shape:
                 raise ValueError(f"preconditioner {name} has shape {dop.shape}, the operator {self.A.shape}")
             self.ops[name] = dop

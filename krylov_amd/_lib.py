@@ -66,6 +66,12 @@ _SIGNATURES = {
     "kry_ctx_synchronize": [_vp],
     "kry_csr_create": [_vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
     "kry_csr_destroy": [_vp],
+    "kry_csr_create_like": [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
+    "kry_csr_permute": [_vp, _vp, _vp, _vp, _int],
+    "kry_spmv_op": [_vp, _vp, _vp, _vp],
+    "kry_rcm_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, ctypes.c_int64, _ip64, _vp],
+    "kry_rs_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp],
+    "kry_rcm_device": [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, ctypes.c_int64, _ip64, _vp],
     "kry_csr_layout": [_i64, _vp, _int, _ip64, _ip64, _ip64],
     "kry_dia_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
     "kry_pair_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp, _vp],
@@ -119,6 +125,7 @@ _SIGNATURES = {
     "kry_comm_unique_id": [_vp],
     "kry_comm_create": [_vp, _i32, _i32, _vp, _pvp],
     "kry_comm_destroy": [_vp],
+    "kry_comm_create_all": [_vp, _i32, _vp],
     "kry_comm_allreduce": [_vp, _dp, _i32],
     "kry_cg_attach_comm": [_vp, _vp, _i32, _i32],
     "kry_gmres_attach_comm": [_vp, _vp, _i32, _i32],
@@ -275,6 +282,41 @@ def cb_plan(indptr, indices):
     gptr = np.zeros(nb * ng + 1, dtype=np.int64)
     check(lib.kry_cb_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, ptr(gptr)))
     return {"nb": nb, "cols": int(info[2]), "ng": ng, "gptr": gptr}
+
+
+def rcm_plan(indptr, indices, wlimit=0):
+    """Host-only reverse Cuthill-McKee order (kry_rcm_plan): None if refused
+    (a BFS level wider than wlimit), else (perm, levels) with new row r = old
+    row perm[r]."""
+    indptr = np.ascontiguousarray(indptr)
+    indices = np.ascontiguousarray(indices, dtype=indptr.dtype)
+    n, nnz = indptr.shape[0] - 1, indices.shape[0]
+    info = np.zeros(2, dtype=np.int64)
+    perm = np.zeros(max(n, 1), dtype=np.int32)
+    check(lib.kry_rcm_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), int(wlimit),
+                           info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ptr(perm)))
+    if not info[0]:
+        return None
+    return perm[:n], int(info[1])
+
+
+def rs_plan(indptr, indices):
+    """Host-only rank-sorted SELL-128 plan (kry_rs_plan): None if not built,
+    else {"slices", "slots", "max_width", "widths", "colrank"}."""
+    indptr = np.ascontiguousarray(indptr)
+    indices = np.ascontiguousarray(indices, dtype=indptr.dtype)
+    n, nnz = indptr.shape[0] - 1, indices.shape[0]
+    info = np.zeros(4, dtype=np.int64)
+    ip64 = info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    check(lib.kry_rs_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, None, None))
+    if not info[0]:
+        return None
+    widths = np.zeros(int(info[1]), dtype=np.int32)
+    colrank = np.zeros(int(info[2]), dtype=np.uint32)
+    check(lib.kry_rs_plan(n, nnz, ptr(indptr), ptr(indices), itype_code(indptr.dtype), ip64, ptr(widths),
+                          ptr(colrank)))
+    return {"slices": int(info[1]), "slots": int(info[2]), "max_width": int(info[3]), "widths": widths,
+            "colrank": colrank}
 
 
 def csr_layout(indptr):

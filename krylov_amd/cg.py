@@ -103,14 +103,24 @@ def _norm_from_sq(prob, sq):
 
 
 def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None,
-       return_arnoldi=False, callback=None):
+       return_arnoldi=False, callback=None, *, devices=None):
     """Preconditioned CG, reference signature (``cg.py:16-28``).
 
     ``A``: ``krylov_amd.CsrOperator``, scipy.sparse matrix or dense ndarray
     (uploaded once as CSR). ``inner``: ``None`` or ``WeightedInner``.
     ``M``/``Ml``: ``None``/``Identity`` or an operator of the same kinds as
     ``A`` (applied on the device as SpMVs, cg.py:70-90, 180, 207).
+    ``devices=[...]``: split the columns of a block ``b`` over these GPUs of
+    this process (``krylov_amd.multi``: one RCCL allreduce per iteration, the
+    global iterate gathered), the same steps and history as one device.
     """
+    if devices is not None:
+        if inner is not None or return_arnoldi:
+            raise NotImplementedError("devices=[...] takes the Euclidean inner product, no return_arnoldi")
+        from .multi import solve
+
+        return solve("cg", A, b, devices, x0=x0, tol=tol, atol=atol, maxiter=maxiter, callback=callback, M=M,
+                     Ml=Ml)
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter

@@ -223,6 +223,65 @@ double *ctx_scratch(kry_ctx *ctx, size_t bytes) {
   return ctx->scratch;
 }
 
+
+// ------------------------------------------------ renumbering: row moves
+template <int ES>
+__global__ __launch_bounds__(kBlock) void permute_rows_kernel(int64_t n, int kshift, const int32_t *__restrict__ idx,
+                                                              const char *__restrict__ src, char *__restrict__ dst) {
+  typedef typename std::conditional<ES == 8, unsigned long long, unsigned>::type T;
+  const int64_t N = n << kshift;
+  const int64_t k1 = ((int64_t)1 << kshift) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i >> kshift;
+    const int64_t from = ((int64_t)idx[r] << kshift) | (i & k1);
+    reinterpret_cast<T *>(dst)[i] = reinterpret_cast<const T *>(src)[from];
+  }
+}
+
+void permute_rows(const kry_csr *A, const void *src, void *dst, int k, size_t esize, bool to_op, hipStream_t st) {
+  const size_t bytes = (size_t)A->n * k * esize;
+  if (!A->renumbered) {
+    if (bytes) KRY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  KRY_REQUIRE(src != dst, KRY_EINVAL, "permute_rows: in place");
+  int ks = 0;
+  while ((1 << ks) < k) ++ks;
+  KRY_REQUIRE((1 << ks) == k, KRY_EINVAL, "permute_rows: k must be a power of two");
+  const int64_t N = A->n * (int64_t)k;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (N + kBlock - 1) / kBlock));
+  const int32_t *idx = static_cast<const int32_t *>(to_op ? A->perm : A->iperm);
+  if (esize == 8)
+    hipLaunchKernelGGL(permute_rows_kernel<8>, dim3(grid), dim3(kBlock), 0, st, A->n, ks, idx,
+                       static_cast<const char *>(src), static_cast<char *>(dst));
+  else
+    hipLaunchKernelGGL(permute_rows_kernel<4>, dim3(grid), dim3(kBlock), 0, st, A->n, ks, idx,
+                       static_cast<const char *>(src), static_cast<char *>(dst));
+  KRY_HIP(hipGetLastError());
+}
+
+void load_in(const kry_csr *A, const void *src, void *dst, int k, size_t esize, hipStream_t st) {
+  permute_rows(A, src, dst, k, esize, true, st);
+}
+
+void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st) {
+  const size_t bytes = (size_t)A->n * k * esize;
+  if (!A->renumbered) {
+    KRY_HIP(hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, st));
+    return;
+  }
+  void *tmp = dev_alloc(bytes + 16);
+  try {
+    permute_rows(A, src, tmp, k, esize, false, st);
+    KRY_HIP(hipMemcpyAsync(host, tmp, bytes, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  } catch (...) {
+    dev_free(tmp);
+    throw;
+  }
+  dev_free(tmp);
+}
+
 ProfScope::ProfScope(kry_ctx *c, int kernel_id) : ctx(c), id(kernel_id) {
   if (!((ctx->profile >> kernel_id) & 1u)) return;
   if (ctx->prof_calls[kernel_id]++ % ctx->prof_every != 0) return;
@@ -312,7 +371,7 @@ extern "C" {
 // 103: the per-step allreduces of the sharded solvers carry a fault count
 // (CG total_k + 1, GMRES / MINRES total_k + 2 values); kry_cg_defer_info,
 // kry_gmres_xk_device.
-int kry_version(void) { return 103; }
+int kry_version(void) { return 104; }
 
 int kry_device_count(int *count) {
   KRY_API_BEGIN
@@ -385,9 +444,10 @@ int kry_ctx_synchronize(kry_ctx *ctx) {
 int kry_csr_info_n(const kry_csr *A, int64_t *info, int32_t len) {
   KRY_API_BEGIN
   KRY_REQUIRE(A && (info || len == 0) && len >= 0, KRY_EINVAL, "bad argument");
-  const int64_t all[KRY_CSR_INFO_LEN] = {A->nslices, A->nslots, A->nirregular, A->compact ? 1 : 0,
-                                         A->cb_nb,     A->dia ? 1 : 0, A->dia_nslots, A->sp ? 1 : 0,
-                                         A->sp_nslots};
+  const int64_t all[KRY_CSR_INFO_LEN] = {A->nslices,   A->nslots,    A->nirregular,        A->compact ? 1 : 0,
+                                         A->cb_nb,      A->dia ? 1 : 0, A->dia_nslots,     A->sp ? 1 : 0,
+                                         A->sp_nslots,  A->rs ? 1 : 0, A->rs_nslots,     A->renumbered ? 1 : 0,
+                                         A->rcm_levels};
   for (int i = 0; i < len && i < KRY_CSR_INFO_LEN; ++i) info[i] = all[i];
   KRY_API_END
 }
@@ -414,12 +474,82 @@ struct UploadTrace {
   }
 };
 
+// FNV-1a over the permutation: preconditioners must carry their operator's
+uint64_t perm_fingerprint(const std::vector<int32_t> &p) {
+  uint64_t h = 1469598103934665603ull;
+  for (int32_t v : p) {
+    h ^= (uint32_t)v;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+bool env_off(const char *name) {
+  const char *e = getenv(name);
+  return e && atoi(e) == 0;
+}
+
+// like_perm: build P A P^T with another operator's renumbering (a
+// preconditioner of a renumbered operator); otherwise renumber when the
+// columns are scattered and the graph has narrow levels (KRY_RENUMBER=0
+// disables; KRY_RCM_WLIMIT sets the level-width limit, default max(2^16, n / 32)).
 template <typename I, typename MV>
-void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
+void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::vector<int32_t> *like_perm) {
   hipStream_t st = A->ctx->stream;
   const int64_t n = A->n, nnz = A->nnz;
   UploadTrace tr;
   check_csr(n, nnz, ip, ix);
+  std::vector<int32_t> own;
+  const std::vector<int32_t> *perm = like_perm;
+  if (perm) {
+    KRY_REQUIRE((int64_t)perm->size() == n, KRY_EINVAL, "renumbering of another size");
+  } else if (sizeof(I) == 4 && !env_off("KRY_RENUMBER") && scattered(n, ip, ix)) {
+    const char *we = getenv("KRY_RCM_WLIMIT");
+    const int64_t wlimit = we ? std::max<int64_t>(1, atoll(we)) : std::max<int64_t>(int64_t(1) << 16, n / 32);
+    // on the device (one H2D of indptr / indices; KRY_RCM_DEVICE=0: the host
+    // order, the same permutation)
+    int r = -1;
+    if constexpr (sizeof(I) == 4) {
+      if (!env_off("KRY_RCM_DEVICE")) {
+        void *dip = dev_alloc((size_t)(n + 1) * 4);
+        void *dix = dev_alloc((size_t)std::max<int64_t>(nnz, 1) * 4);
+        try {
+          KRY_HIP(hipMemcpyAsync(dip, ip, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
+          if (nnz) KRY_HIP(hipMemcpyAsync(dix, ix, (size_t)nnz * 4, hipMemcpyHostToDevice, st));
+          r = rcm_order_device(A->ctx, n, static_cast<const int32_t *>(dip), static_cast<const int32_t *>(dix), wlimit,
+                               own, &A->rcm_levels);
+        } catch (...) {
+          dev_free(dip);
+          dev_free(dix);
+          throw;
+        }
+        dev_free(dip);
+        dev_free(dix);
+      }
+    }
+    if (r < 0) r = rcm_order(n, ip, ix, wlimit, own, &A->rcm_levels) ? 1 : 0;
+    if (r == 1) perm = &own;
+    tr.mark("RCM order");
+  }
+  hvec<I> ip2, ix2;
+  hvec<MV> dv2;
+  if (perm) {
+    renumber_csr(n, ip, ix, dv, *perm, ip2, ix2, dv2);
+    ip = ip2.data();
+    ix = ix2.data();
+    dv = dv2.data();
+    A->renumbered = true;
+    A->perm_host = *perm;
+    A->perm_hash = perm_fingerprint(A->perm_host);
+    std::vector<int32_t> inv(n);
+    for (int64_t r = 0; r < n; ++r) inv[A->perm_host[r]] = (int32_t)r;
+    A->perm = dev_alloc((size_t)n * 4 + 4);
+    A->iperm = dev_alloc((size_t)n * 4 + 4);
+    KRY_HIP(hipMemcpyAsync(A->perm, A->perm_host.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    KRY_HIP(hipMemcpyAsync(A->iperm, inv.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    KRY_HIP(hipStreamSynchronize(st));
+    tr.mark("renumbered CSR + perm H2D");
+  }
   std::vector<int64_t> sptr;
   std::vector<int32_t> width;
   sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
@@ -481,7 +611,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   }
   // column-blocked image for scattered single-RHS SpMVs (KRY_SPMV_CB=0 disables)
   const char *cbenv = getenv("KRY_SPMV_CB");
-  if (!A->dia && !(cbenv && atoi(cbenv) == 0)) {
+  if (!A->dia && !A->renumbered && !(cbenv && atoi(cbenv) == 0)) {
     CbHost<MV> cb;
     if (cb_build(n, ip, ix, dv, cb)) {
       A->cb_nb = cb.nb;
@@ -504,7 +634,9 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
   }
   // paired-row SELL-128 image for general single-RHS SpMVs (KRY_SPMV_PAIR=0 disables)
   const char *penv = getenv("KRY_SPMV_PAIR");
-  if (!A->dia && A->cb_nb == 0 && !(penv && atoi(penv) == 0)) {
+  // (not for a renumbered matrix: its rows are unsorted in the new numbering,
+  // and the rank-sorted image's column-sorted runs gather coalesced)
+  if (!A->dia && A->cb_nb == 0 && !A->renumbered && !(penv && atoi(penv) == 0)) {
     PairHost<MV> ph;
     if (pair_build(n, ip, ix, dv, A->nslots, ph)) {
       A->sp = true;
@@ -527,6 +659,28 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
     }
     tr.mark("paired image + H2D");
   }
+  // rank-sorted SELL-128 image: unsorted rows or wide slot columns (KRY_SPMV_RS=0 disables)
+  if (!A->dia && A->cb_nb == 0 && !A->sp && !env_off("KRY_SPMV_RS")) {
+    RsHost<MV> rh;
+    if (rs_build(n, ip, ix, dv, A->nslots, rh)) {
+      A->rs = true;
+      A->rs_nslices = (int64_t)rh.width.size();
+      A->rs_nslots = rh.sptr.back();
+      A->rs_max_width = rh.max_width;
+      A->rs_sptr = dev_alloc(rh.sptr.size() * 8);
+      A->rs_width = dev_alloc(rh.width.size() * 4 + 4);
+      A->rs_colrank = dev_alloc(rh.colrank.size() * 4);
+      A->rs_val = dev_alloc(rh.val.size() * sizeof(MV));
+      KRY_HIP(hipMemcpyAsync(A->rs_sptr, rh.sptr.data(), rh.sptr.size() * 8, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->rs_width, rh.width.data(), rh.width.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->rs_colrank, rh.colrank.data(), rh.colrank.size() * 4, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->rs_val, rh.val.data(), rh.val.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+      KRY_HIP(hipStreamSynchronize(st));
+      release_later(rh.colrank);
+      release_later(rh.val);
+    }
+    tr.mark("rank-sorted image + H2D");
+  }
   if (A->nirregular > 0) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
     A->indices = dev_alloc((nnz + 1) * sizeof(I));
@@ -538,6 +692,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv) {
     }
   }
   KRY_HIP(hipStreamSynchronize(st));  // host staging vectors die at return
+  release_later(ix2);
+  release_later(dv2);
   tr.mark("CSR copy + final sync");
 }
 }  // namespace
@@ -546,21 +702,22 @@ static void csr_free(kry_csr *A) {
   void *bufs[] = {A->sptr,   A->swidth,   A->sidx,     A->sval,     A->indptr,    A->indices,
                   A->data,   A->sdelta,   A->scbase,   A->cb_gptr,  A->cb_roff,   A->cb_col,
                   A->cb_val, A->dia_sptr, A->dia_width, A->dia_off, A->dia_mask, A->dia_val,
-                  A->sp_sptr, A->sp_width, A->sp_cbase, A->sp_delta, A->sp_val};
+                  A->sp_sptr, A->sp_width, A->sp_cbase, A->sp_delta, A->sp_val,
+                  A->rs_sptr, A->rs_width, A->rs_colrank, A->rs_val, A->perm, A->iperm};
   for (void *b : bufs) dev_free(b);
 }
 
 extern "C" {
 
-int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
-                   const void *data, int dtype, int itype, kry_csr **out) {
-  KRY_API_BEGIN
-  KRY_REQUIRE(ctx && out && indptr && (nnz == 0 || (indices && data)), KRY_EINVAL, "null argument");
+static kry_csr *csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
+                           const void *data, int dtype, int itype, const kry_csr *like) {
+  KRY_REQUIRE(ctx && indptr && (nnz == 0 || (indices && data)), KRY_EINVAL, "null argument");
   KRY_REQUIRE(n >= 0 && nnz >= 0, KRY_EINVAL, "negative size");
   KRY_REQUIRE(dtype == KRY_F32 || dtype == KRY_F64, KRY_EINVAL, "dtype must be f32 or f64");
   KRY_REQUIRE(itype == KRY_I32 || itype == KRY_I64, KRY_EINVAL, "itype must be i32 or i64");
   if (itype == KRY_I32) KRY_REQUIRE(nnz < (int64_t(1) << 31) && n < (int64_t(1) << 31), KRY_EINVAL,
                                     "int32 indices cannot address this matrix");
+  KRY_REQUIRE(!like || like->n == n, KRY_EINVAL, "the operator to renumber like has another size");
   KRY_HIP(hipSetDevice(ctx->device));
   auto *A = new kry_csr();
   A->ctx = ctx;
@@ -571,23 +728,50 @@ int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, con
   static const int32_t zi32 = 0;
   static const int64_t zi64 = 0;
   static const double zd = 0;
+  const std::vector<int32_t> *lp = like && like->renumbered ? &like->perm_host : nullptr;
   try {
     const void *ix = nnz ? indices : (itype == KRY_I32 ? (const void *)&zi32 : (const void *)&zi64);
     const void *dv = nnz ? data : (const void *)&zd;
     if (itype == KRY_I32 && dtype == KRY_F64)
-      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const double *>(dv));
+      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const double *>(dv), lp);
     else if (itype == KRY_I32)
-      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const float *>(dv));
+      csr_upload(A, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(ix), static_cast<const float *>(dv), lp);
     else if (dtype == KRY_F64)
-      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const double *>(dv));
+      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const double *>(dv), lp);
     else
-      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const float *>(dv));
+      csr_upload(A, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(ix), static_cast<const float *>(dv), lp);
   } catch (...) {
     csr_free(A);
     delete A;
     throw;
   }
-  *out = A;
+  return A;
+}
+
+int kry_csr_create(kry_ctx *ctx, int64_t n, int64_t nnz, const void *indptr, const void *indices,
+                   const void *data, int dtype, int itype, kry_csr **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(out, KRY_EINVAL, "null argument");
+  *out = csr_create(ctx, n, nnz, indptr, indices, data, dtype, itype, nullptr);
+  KRY_API_END
+}
+
+int kry_csr_create_like(kry_ctx *ctx, const kry_csr *like, int64_t n, int64_t nnz, const void *indptr,
+                        const void *indices, const void *data, int dtype, int itype, kry_csr **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(out && like, KRY_EINVAL, "null argument");
+  *out = csr_create(ctx, n, nnz, indptr, indices, data, dtype, itype, like);
+  KRY_API_END
+}
+
+int kry_csr_permute(kry_ctx *ctx, const kry_csr *A, const kry_vec *src, kry_vec *dst, int to_operator) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && src && dst, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(src->n == A->n && dst->n == A->n && src->k == dst->k && src->dtype == dst->dtype, KRY_EINVAL,
+              "shape mismatch");
+  KRY_REQUIRE(src != dst, KRY_EINVAL, "src and dst must differ");
+  KRY_HIP(hipSetDevice(ctx->device));
+  permute_rows(A, src->d, dst->d, src->k, dsize(src->dtype), to_operator != 0, ctx->stream);
   KRY_API_END
 }
 
@@ -658,15 +842,52 @@ int kry_spmv(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y) {
   KRY_REQUIRE(is_pow2(x->k) && x->k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   KRY_HIP(hipSetDevice(ctx->device));
   const int k = x->k;
+  // a renumbered operator: x and y in the caller's numbering, moved through
+  // two temporaries (y = P^T (P A P^T) P x)
+  const size_t vb = (size_t)A->n * k * dsize(x->dtype) + 16;
+  void *xt = A->renumbered ? dev_alloc(vb) : nullptr;
+  void *yt = A->renumbered ? dev_alloc(vb) : nullptr;
+  try {
+    if (xt) permute_rows(A, x->d, xt, k, dsize(x->dtype), true, ctx->stream);
+    const void *xs = xt ? xt : x->d;
+    void *ys = yt ? yt : y->d;
+    dispatch_vmi(x->dtype, A->dtype, A->itype, [&](auto v0, auto m0, auto i0) {
+      using V = decltype(v0);
+      using MV = decltype(m0);
+      using I = decltype(i0);
+      ProfScope ps(ctx, PROF_SPMV);
+      launch_spmv<V, MV, I>(A, k, SrcPlain<V>{static_cast<const V *>(xs), k}, EpiStore<V>{static_cast<V *>(ys), k},
+                            nullptr, nullptr, nullptr, 0, ctx->stream);
+    });
+    if (yt) permute_rows(A, yt, y->d, k, dsize(x->dtype), false, ctx->stream);
+  } catch (...) {
+    dev_free(xt);
+    dev_free(yt);
+    throw;
+  }
+  dev_free(xt);  // the caching pool retires freed blocks only after a device sync
+  dev_free(yt);
+  KRY_HIP(hipGetLastError());  // stream-ordered: a download or reduction of y waits for it
+  KRY_API_END
+}
+
+int kry_spmv_op(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctx && A && x && y, KRY_EINVAL, "null argument");
+  KRY_REQUIRE(x->n == A->n && y->n == A->n && x->k == y->k, KRY_EINVAL, "shape mismatch");
+  KRY_REQUIRE(x->dtype == y->dtype, KRY_EINVAL, "dtype mismatch");
+  KRY_REQUIRE(is_pow2(x->k) && x->k <= kMaxCols, KRY_EUNSUPPORTED, "k must be a power of two <= 256");
+  KRY_HIP(hipSetDevice(ctx->device));
+  const int k = x->k;
   dispatch_vmi(x->dtype, A->dtype, A->itype, [&](auto v0, auto m0, auto i0) {
     using V = decltype(v0);
     using MV = decltype(m0);
     using I = decltype(i0);
     ProfScope ps(ctx, PROF_SPMV);
-    launch_spmv<V, MV, I>(A, k, SrcPlain<V>{static_cast<const V *>(x->d), k},
-                      EpiStore<V>{static_cast<V *>(y->d), k}, nullptr, nullptr, nullptr, 0, ctx->stream);
+    launch_spmv<V, MV, I>(A, k, SrcPlain<V>{static_cast<const V *>(x->d), k}, EpiStore<V>{static_cast<V *>(y->d), k},
+                          nullptr, nullptr, nullptr, 0, ctx->stream);
   });
-  KRY_HIP(hipGetLastError());  // stream-ordered: a download or reduction of y waits for it
+  KRY_HIP(hipGetLastError());
   KRY_API_END
 }
 

@@ -87,6 +87,7 @@ namespace {
 enum { S_RHO = 0, S_RHO_PREV = 1, S_ALPHA = 2, S_OMEGA = 3, S_CRIT = 4, S_TMP = 5, S_RHO_OLD = 6, S_COUNT = 7 };
 
 constexpr int kCgUpdateGrid = 1024;  // update-pass blocks: the <r, r> partials every yp block re-reduces
+constexpr size_t kCgYDeferBudget = size_t(10) << 30;  // default ring budget (bytes)
 constexpr int kCgYDefer = 7;         // deferred yk updates per flush: the policy tries 31, 15, 7, 3 (KRY_CG_YDEFER)
 constexpr int kCgYDeferMax = 31;     // the ring holds at most 32 p buffers
 
@@ -1258,19 +1259,22 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     // smaller y / p stay cache-resident between the passes, and reading the
     // ring's older p vectors back costs more than the y pass it saves: metric
     // CG, 80 MB vectors, 3,016 -> 2,874 it/s with D = 7; cfg4, 640 MB, 690 ->
-    // 748 it/s at D = 7, 731 -> 757 it/s from D = 7 to D = 31 on one box:
-    // the flush reads D + 2 vectors every D steps), the deepest ring of 31,
-    // 15, 7 or 3 whose D buffers fit an eighth of the device's TOTAL memory
-    // (a fixed policy: the path does not depend on what other allocations
-    // happen to leave free; cfg4 at D = 31: 19.8 GB of 288); an allocation
-    // failure falls back to one update per step
+    // 748 it/s at D = 7: the flush reads D + 2 vectors every D steps), the
+    // deepest ring of 15, 7 or 3 whose D buffers fit kCgYDeferBudget (10 GB)
+    // and a quarter of the memory free right now. Round 4 defaulted to 31
+    // steps within an eighth of the device (19.8 GB at cfg4) for +1.2 % over
+    // D = 15 (748 -> 757 it/s, profiles/r04_ydefer_depth.json): not worth 7 %
+    // of the device held per solver. cfg4 at D = 15: 9.6 GB. KRY_CG_YDEFER
+    // still selects any depth up to 31; an allocation failure falls back to
+    // one update per step
     const bool big = vb > (size_t(128) << 20);
+    const size_t budget = std::min(kCgYDeferBudget, fr / 4);
     int D = 0;
     if (e) {
       D = atoi(e);
     } else if (big) {
-      for (int d : {kCgYDeferMax, 15, kCgYDefer, 3})
-        if ((size_t)d * vb <= tot / 8) {
+      for (int d : {15, kCgYDefer, 3})
+        if ((size_t)d * vb <= budget) {
           D = d;
           break;
         }
@@ -1495,18 +1499,20 @@ int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   const size_t vb = b->bytes();
-  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  // b, x0 and the weights arrive in the caller's numbering (load_in: into a
+  // renumbered operator's, a plain copy otherwise)
+  load_in(s->A, b->d, s->b, s->k, dsize(s->dtype), st);
   dev_free(s->x0);
   s->x0 = nullptr;
   if (x0) {
     s->x0 = dev_alloc(((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype));
-    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, x0->d, s->x0, s->k, dsize(s->dtype), st);
   }
   dev_free(s->w);
   s->w = nullptr;
   if (w) {
     s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
-    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, w->d, s->w, 1, 8, st);
   }
   // the inner product's dtype: float32 for an unweighted fp32 solve (np.dot of
   // float32), float64 otherwise (weights are float64)
@@ -1656,7 +1662,6 @@ int kry_cg_get(kry_cg *s, int which, void *host) {
   KRY_REQUIRE(s && host && which >= 0 && which <= 2, KRY_EINVAL, "bad argument");
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  const size_t vb = (size_t)s->n * s->k * dsize(s->dtype);
   const int64_t N = s->n * (int64_t)s->k;
   if (which == 0) {
     if (s->dtype == KRY_F64)
@@ -1665,10 +1670,10 @@ int kry_cg_get(kry_cg *s, int which, void *host) {
     else
       launch_elementwise<float>(N, s->k, OpXk<float>{static_cast<const float *>(s->x0), static_cast<const float *>(s->y), static_cast<float *>(s->xk)},
                                 nullptr, nullptr, 0, st);
-    KRY_HIP(hipMemcpyAsync(host, s->xk, vb, hipMemcpyDeviceToHost, st));
+    store_out(s->A, s->xk, host, s->k, dsize(s->dtype), st);
   } else {
     // 1: Ml_rk; 2: M_Ml_rk (= Ml_rk without M)
-    KRY_HIP(hipMemcpyAsync(host, which == 2 && s->M ? s->z : s->r, vb, hipMemcpyDeviceToHost, st));
+    store_out(s->A, which == 2 && s->M ? s->z : s->r, host, s->k, dsize(s->dtype), st);
   }
   KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END
@@ -1694,6 +1699,8 @@ int kry_cg_set_preconditioners(kry_cg *s, kry_csr *M, kry_csr *Ml) {
     KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
     KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
                 "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+    KRY_REQUIRE(op->renumbered == s->A->renumbered && op->perm_hash == s->A->perm_hash, KRY_EINVAL,
+                "preconditioner renumbered differently from the operator (build it with kry_csr_create_like)");
   }
   KRY_HIP(hipSetDevice(s->ctx->device));
   const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype);

@@ -1,6 +1,8 @@
 // RCCL communicator for RHS-column sharding (one process per GPU over xGMI).
 #include <cstring>
 
+#include <vector>
+
 #include "solver_common.hpp"
 
 using namespace kry;
@@ -54,6 +56,32 @@ int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id12
     throw Error{KRY_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
   }
   *out = c;
+  KRY_API_END
+}
+
+// One communicator per context of ONE process (ncclCommInitAll over the
+// contexts' devices, rank i = ctxs[i]): the single-process multi-GPU path
+// (krylov_amd.cg(..., devices=[...])), one host thread per device.
+int kry_comm_create_all(kry_ctx **ctxs, int32_t n, kry_comm **out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(ctxs && out && n >= 1, KRY_EINVAL, "bad argument");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    KRY_REQUIRE(ctxs[i], KRY_EINVAL, "null context");
+    devs[i] = ctxs[i]->device;
+    for (int j = 0; j < i; ++j) KRY_REQUIRE(devs[j] != devs[i], KRY_EINVAL, "a device listed twice");
+  }
+  std::vector<ncclComm_t> comms(n, nullptr);
+  ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+  if (r != ncclSuccess) throw Error{KRY_ECOMM, std::string("ncclCommInitAll: ") + ncclGetErrorString(r)};
+  for (int i = 0; i < n; ++i) {
+    auto *c = new kry_comm();
+    c->ctx = ctxs[i];
+    c->comm = comms[i];
+    c->nranks = n;
+    c->rank = i;
+    out[i] = c;
+  }
   KRY_API_END
 }
 

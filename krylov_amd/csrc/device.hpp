@@ -771,6 +771,128 @@ __global__ __launch_bounds__(kBlock) void spmv_pair_kernel(const int64_t *__rest
   }
 }
 
+
+// ---------------------------------- rank-sorted SELL-128 SpMV (k = 1)
+// Round 5, kry_csr::rs_* (host_image.hpp rs_build): the paired-row slice
+// geometry (lane l owns rows 2l, 2l + 1; one 16-B value load and one 8-B
+// load of the two rows' column words per slot column) with int32 columns, for
+// matrices the DIA, column-blocked and paired images do not take: unsorted
+// rows, or slot columns wider than a uint16 delta (a renumbered matrix). In
+// every run of kRsChunk stored entries of a row the entries sit in column
+// order, so slot column j of neighbouring rows gathers neighbouring x entries
+// (the renumbered permuted metric: 0.155 cache lines per gather against 0.65
+// in stored order). The run's products are written to LDS at their stored
+// position (the word's top 4 bits) and summed back in that order, from 0,
+// one rounding per product and per add: bitwise csr_matvec. LDS: 2 x 16 x 64
+// products per wave, each lane reading back only what it wrote (no barrier).
+// The second row's x is the first row's 16-B pair load when its column is
+// the next one (neighbouring rows of a banded numbering), else an 8-B load
+// behind one wave-level branch, as in the paired kernel.
+constexpr int kRsRun = kRsChunk;
+template <typename V, typename MV, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_rs_kernel(const int64_t *__restrict__ sptr,
+                                                         const int *__restrict__ swidth,
+                                                         const uint32_t *__restrict__ colrank,
+                                                         const MV *__restrict__ val, int64_t nslices, int64_t n,
+                                                         Src src, Epi epi, double *__restrict__ part,
+                                                         const Ctrl *ctrl, int step) {
+  static_assert(kRsRun % UNR == 0, "a run is a whole number of unrolled rounds");
+  if (halted(ctrl, step)) return;
+  __shared__ double red[kBlock];
+  __shared__ V prod[kBlock / 64][2][kRsRun][64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const auto bs = src.template bind<1>(0);
+  V(*pw)[kRsRun][64] = prod[wid];
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  double dacc = 0.0;
+  for (int64_t s = (int64_t)g * 4 + wid; s < nslices; s += W) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * kPairSlice + 2 * lane;
+    const u2 *cr = reinterpret_cast<const u2 *>(colrank + base) + lane;
+    const MV *cv = val + base + 2 * lane;
+    V acc0 = V(0), acc1 = V(0);
+    for (int r0 = 0; r0 < w; r0 += kRsRun) {
+      const int re = w < r0 + kRsRun ? w : r0 + kRsRun;
+      int n0 = 0, n1 = 0;
+      for (int j0 = r0; j0 < re; j0 += UNR) {
+        uint32_t d0[UNR], d1[UNR];
+        MV a[UNR][2];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (j0 + u < re) {
+            const u2 t = __builtin_nontemporal_load(cr + (int64_t)(j0 + u) * (kPairSlice / 2));
+            d0[u] = t.x;
+            d1[u] = t.y;
+            pload_nt<MV>(cv + (int64_t)(j0 + u) * kPairSlice, a[u]);
+          } else {
+            d0[u] = 0xFFFFFFFFu;
+            d1[u] = 0xFFFFFFFFu;
+            a[u][0] = MV(0);
+            a[u][1] = MV(0);
+          }
+        }
+        V x0[UNR], x1[UNR];
+        bool v0[UNR], v1[UNR], need[UNR];
+        int64_t c1[UNR];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          v0[u] = d0[u] != 0xFFFFFFFFu;
+          v1[u] = d1[u] != 0xFFFFFFFFu;
+          const int64_t c0 = (int64_t)(d0[u] & 0x0FFFFFFFu);
+          c1[u] = (int64_t)(d1[u] & 0x0FFFFFFFu);
+          const bool pr = v0[u] && v1[u] && c1[u] == c0 + 1;
+          V xp[2];
+          bs.pair(v0[u] ? c0 : (v1[u] ? c1[u] : 0), xp);  // at worst x[n]: inside the allocation slack
+          x0[u] = xp[0];
+          x1[u] = pr ? xp[1] : xp[0];
+          need[u] = v0[u] && v1[u] && !pr;
+          any = any || need[u];
+        }
+        if (__any(any)) {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u)
+            if (need[u]) x1[u] = bs(c1[u], 0);
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const V p0 = (V)a[u][0] * x0[u];
+          const V p1 = (V)a[u][1] * x1[u];
+          if (v0[u]) pw[0][d0[u] >> 28][lane] = p0;
+          if (v1[u]) pw[1][d1[u] >> 28][lane] = p1;
+          n0 += v0[u] ? 1 : 0;
+          n1 += v1[u] ? 1 : 0;
+        }
+      }
+      // the run in stored order (entries of a row fill its first slots: the
+      // run's positions are 0 .. n - 1)
+      const int nm = n0 > n1 ? n0 : n1;
+      for (int k = 0; k < nm; ++k) {
+        if (k < n0) acc0 = acc0 + pw[0][k][lane];
+        if (k < n1) acc1 = acc1 + pw[1][k][lane];
+      }
+    }
+    if (row + 1 < n) {
+      V xi[2];
+      bs.pair(row, xi);
+      const V o[2] = {acc0, acc1};
+      dacc += epi.rows2(row, o, xi);
+    } else if (row < n) {
+      dacc += epi(row, 0, acc0, bs(row, 0));
+    }
+  }
+  if (part != nullptr) {
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[g] = red[0];
+  }
+}
+
 // ------------------------------ diagonal-offset SpMV, block RHS (k = 2..8)
 // The same SELL-128/DIA image for k right-hand sides stored row-major
 // (n x k): for a slot column of offset o the x rows of the slice's rows are
@@ -1352,6 +1474,16 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                        static_cast<const int64_t *>(A->sp_sptr), static_cast<const int *>(A->sp_width),
                        static_cast<const int *>(A->sp_cbase), static_cast<const uint32_t *>(A->sp_delta),
                        static_cast<const MV *>(A->sp_val), A->sp_nslices, A->n, src, epi, part, ctrl, step);
+    KRY_HIP(hipGetLastError());
+    if (grid_out) *grid_out = grid;
+    return;
+  }
+  if (k == 1 && A->rs) {
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGridBlk, (A->rs_nslices + 3) / 4));
+    hipLaunchKernelGGL((spmv_rs_kernel<V, MV, 8, Src, Epi>), dim3(grid), dim3(kBlock), 0, st,
+                       static_cast<const int64_t *>(A->rs_sptr), static_cast<const int *>(A->rs_width),
+                       static_cast<const uint32_t *>(A->rs_colrank), static_cast<const MV *>(A->rs_val),
+                       A->rs_nslices, A->n, src, epi, part, ctrl, step);
     KRY_HIP(hipGetLastError());
     if (grid_out) *grid_out = grid;
     return;

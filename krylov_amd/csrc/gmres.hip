@@ -1678,6 +1678,8 @@ int kry_gmres_set_preconditioners(kry_gmres *s, kry_csr *M, kry_csr *Ml, kry_csr
     KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
     KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
                 "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+    KRY_REQUIRE(op->renumbered == s->A->renumbered && op->perm_hash == s->A->perm_hash, KRY_EINVAL,
+                "preconditioner renumbered differently from the operator (build it with kry_csr_create_like)");
   }
   KRY_REQUIRE(!(M && s->householder), KRY_EINVAL, "Householder Arnoldi does not take M (gmres.py:160)");
   KRY_HIP(hipSetDevice(s->ctx->device));
@@ -1723,18 +1725,20 @@ int kry_gmres_start(kry_gmres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *r
   hipStream_t st = s->ctx->stream;
   const size_t vb = b->bytes();
   const int k = s->k;
-  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  // b, x0 and the weights arrive in the caller's numbering (load_in: into a
+  // renumbered operator's, a plain copy otherwise)
+  load_in(s->A, b->d, s->b, k, dsize(s->dtype), st);
   dev_free(s->x0);
   s->x0 = nullptr;
   if (x0) {
     s->x0 = dev_alloc(s->vstride * dsize(s->dtype));
-    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, x0->d, s->x0, k, dsize(s->dtype), st);
   }
   dev_free(s->w);
   s->w = nullptr;
   if (w) {
     s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
-    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, w->d, s->w, 1, 8, st);
   }
   const size_t m1 = (size_t)s->maxiter + 1;
   KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
@@ -1851,7 +1855,7 @@ int kry_gmres_xk_device(kry_gmres *s, kry_vec *out) {
   check_vec(out, s->n, s->k, s->dtype, "out");
   KRY_REQUIRE(out->ctx && out->ctx->device == s->ctx->device, KRY_EINVAL, "out: a vector on another device");
   KRY_HIP(hipSetDevice(s->ctx->device));
-  KRY_HIP(hipMemcpyAsync(out->d, s->xk, out->bytes(), hipMemcpyDeviceToDevice, s->ctx->stream));
+  permute_rows(s->A, s->xk, out->d, s->k, dsize(s->dtype), false, s->ctx->stream);  // the caller's numbering
   KRY_API_END
 }
 
@@ -1884,7 +1888,7 @@ int kry_gmres_get(kry_gmres *s, int which, void *host) {
   const size_t vb = (size_t)s->n * s->k * dsize(s->dtype);
   if (which == 0) {
     KRY_REQUIRE(s->have_solution, KRY_EINVAL, "call kry_gmres_solution first");
-    KRY_HIP(hipMemcpyAsync(host, s->xk, vb, hipMemcpyDeviceToHost, st));
+    store_out(s->A, s->xk, host, s->k, dsize(s->dtype), st);
   } else if (which == 3) {
     const int mi = s->maxiter > 0 ? s->maxiter : 1;
     KRY_HIP(hipMemcpyAsync(host, s->Hs, ((size_t)s->maxiter + 1) * mi * s->k * 8, hipMemcpyDeviceToHost, st));
@@ -1908,8 +1912,8 @@ int kry_gmres_get(kry_gmres *s, int which, void *host) {
     const void *base = (which == 2 && s->M) ? s->P : s->V;
     const size_t stride = s->vstride * dsize(s->dtype);
     for (int i = 0; i < nv; ++i)
-      KRY_HIP(hipMemcpyAsync(static_cast<char *>(host) + (size_t)i * vb, static_cast<const char *>(base) + i * stride,
-                             vb, hipMemcpyDeviceToHost, st));
+      store_out(s->A, static_cast<const char *>(base) + i * stride, static_cast<char *>(host) + (size_t)i * vb, s->k,
+                dsize(s->dtype), st);
   }
   KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END

@@ -20,6 +20,8 @@ constexpr int kDiaPad = 32;  // slot-column descriptors past the last one (uncon
 // paired-row SELL-128 image (kry_csr::sp_*): lane l owns rows 2l, 2l + 1
 constexpr int kPairSlice = 128;
 constexpr int kCbRows = 256;         // rows per column-blocked segment (one per thread)
+// rank-sorted SELL-128 image (kry_csr::rs_*): runs of stored entries sorted by column
+constexpr int kRsChunk = 16;
 
 // ---------------------------------------------------------------- errors
 void set_error(const std::string &msg);

@@ -9,6 +9,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 
 namespace kry {
@@ -270,6 +271,310 @@ bool dia_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_s
   return true;
 }
 
+
+// ------------------------------------------- bandwidth-reducing renumbering
+// A fork-join team for the level-synchronous passes: up to 16 threads that
+// live for one rcm_order call and meet at a spin barrier per level (a few
+// microseconds; a thread start per level would cost ~50 us each).
+namespace {
+struct Team {
+  unsigned nt;
+  std::vector<std::thread> th;
+  std::atomic<unsigned> gen{0}, left{0};
+  std::atomic<bool> quit{false};
+  std::function<void(unsigned)> job;
+  explicit Team(unsigned want) : nt(std::max(1u, want)) {
+    for (unsigned t = 1; t < nt; ++t)
+      th.emplace_back([this, t] {
+        unsigned seen = 0;
+        for (;;) {
+          unsigned g;
+          while ((g = gen.load(std::memory_order_acquire)) == seen) {
+            if (quit.load(std::memory_order_acquire)) return;
+            std::this_thread::yield();
+          }
+          seen = g;
+          job(t);
+          left.fetch_sub(1, std::memory_order_acq_rel);
+        }
+      });
+  }
+  void run(const std::function<void(unsigned)> &f) {
+    if (nt == 1) {
+      f(0);
+      return;
+    }
+    job = f;
+    left.store(nt - 1, std::memory_order_release);
+    gen.fetch_add(1, std::memory_order_acq_rel);
+    f(0);
+    while (left.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+  }
+  ~Team() {
+    quit.store(true, std::memory_order_release);
+    for (auto &x : th) x.join();
+  }
+};
+
+// One BFS level step: level[] of the frontier's unvisited neighbours set to
+// `next` (compare-and-swap: one owner each); returns them, in thread order.
+template <typename I>
+void bfs_expand(Team &tm, const I *ip, const I *ix, const int32_t *front, int64_t nf, int32_t next,
+                std::atomic<int32_t> *level, std::vector<std::vector<int32_t>> &loc, std::vector<int32_t> &out) {
+  tm.run([&](unsigned t) {
+    auto &v = loc[t];
+    v.clear();
+    const int64_t a = nf * t / tm.nt, b = nf * (t + 1) / tm.nt;
+    for (int64_t q = a; q < b; ++q) {
+      const int32_t u = front[q];
+      for (int64_t e = ip[u]; e < ip[u + 1]; ++e) {
+        const int32_t w = (int32_t)ix[e];
+        int32_t expect = -1;
+        if (level[w].load(std::memory_order_relaxed) == -1 &&
+            level[w].compare_exchange_strong(expect, next, std::memory_order_relaxed))
+          v.push_back(w);
+      }
+    }
+  });
+  out.clear();
+  for (auto &v : loc) out.insert(out.end(), v.begin(), v.end());
+}
+}  // namespace
+
+template <typename I>
+bool scattered(int64_t n, const I *ip, const I *ix) {
+  if (n * 8 < (int64_t(8) << 20)) return false;
+  const int64_t nnz = (int64_t)ip[n];
+  if (nnz == 0) return false;
+  const int64_t cols = std::max<int64_t>(int64_t(1) << 18, (n + 15) / 16);
+  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<int64_t> far(nt, 0);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+      int64_t f = 0;
+      for (int64_t r = r0; r < r1; ++r)
+        for (int64_t e = ip[r]; e < ip[r + 1]; ++e) {
+          const int64_t d = (int64_t)ix[e] - r;
+          f += (d > cols / 2 || d < -cols / 2);
+        }
+      far[t] = f;
+    });
+  for (auto &x : th) x.join();
+  int64_t nfar = 0;
+  for (int64_t f : far) nfar += f;
+  return nfar * 4 >= nnz;
+}
+
+template <typename I>
+bool rcm_order(int64_t n, const I *ip, const I *ix, int64_t wlimit, std::vector<int32_t> &perm, int64_t *levels) {
+  if (n <= 0 || n >= (int64_t(1) << 31) - 1) return false;
+  const unsigned nt = n < (int64_t(1) << 16) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  Team tm(nt);
+  std::vector<std::vector<int32_t>> loc(nt);
+  std::unique_ptr<std::atomic<int32_t>[]> level(new std::atomic<int32_t>[n]);
+  auto deg = [&](int64_t v) { return (int64_t)ip[v + 1] - (int64_t)ip[v]; };
+  auto clear_levels = [&] {
+    tm.run([&](unsigned t) {
+      for (int64_t v = n * t / tm.nt; v < n * (t + 1) / tm.nt; ++v) level[v].store(-1, std::memory_order_relaxed);
+    });
+  };
+  // levels-only BFS from `root`: the level count, and the last level's
+  // smallest-degree (lowest-index) node; -1 if a level exceeds wlimit
+  std::vector<int32_t> front, next;
+  auto sweep = [&](int32_t root, int32_t *far_node) -> int64_t {
+    clear_levels();
+    level[root].store(0, std::memory_order_relaxed);
+    front.assign(1, root);
+    int64_t nl = 1;
+    for (;;) {
+      bfs_expand(tm, ip, ix, front.data(), (int64_t)front.size(), (int32_t)nl, level.get(), loc, next);
+      if (next.empty()) break;
+      if ((int64_t)next.size() > wlimit) return -1;
+      front.swap(next);
+      ++nl;
+    }
+    int32_t best = front[0];
+    for (int32_t v : front)
+      if (deg(v) < deg(best) || (deg(v) == deg(best) && v < best)) best = v;
+    *far_node = best;
+    return nl;
+  };
+  int32_t root = 0;
+  for (int64_t v = 1; v < n; ++v)
+    if (deg(v) < deg(root)) root = (int32_t)v;
+  int32_t cand = root;
+  int64_t ecc = sweep(root, &cand);
+  if (ecc < 0) return false;
+  static const int max_sweeps = [] {  // tuning override: George-Liu sweeps after the first BFS
+    const char *e = getenv("KRY_RCM_SWEEPS");
+    return e ? std::max(0, atoi(e)) : 3;
+  }();
+  for (int it = 0; it < max_sweeps && cand != root; ++it) {
+    int32_t c2 = cand;
+    const int64_t e2 = sweep(cand, &c2);
+    if (e2 < 0) return false;
+    if (e2 <= ecc) break;
+    root = cand;
+    ecc = e2;
+    cand = c2;
+  }
+  // Cuthill-McKee numbering, level by level
+  clear_levels();
+  std::vector<int32_t> cm;
+  cm.reserve(n);
+  std::vector<int32_t> key(n, INT32_MAX);  // smallest parent number, written under the per-level owner rule below
+  std::unique_ptr<std::atomic<int32_t>[]> akey(new std::atomic<int32_t>[n]);
+  tm.run([&](unsigned t) {
+    for (int64_t v = n * t / tm.nt; v < n * (t + 1) / tm.nt; ++v) akey[v].store(INT32_MAX, std::memory_order_relaxed);
+  });
+  int64_t scan = 0;  // lowest index that may still be unnumbered (new components)
+  int64_t nlev = 0;
+  std::vector<int64_t> cnt;
+  while ((int64_t)cm.size() < n) {
+    if (cm.empty()) {
+      level[root].store(0, std::memory_order_relaxed);
+      cm.push_back(root);
+    } else {
+      while (level[scan].load(std::memory_order_relaxed) != -1) ++scan;
+      level[scan].store(0, std::memory_order_relaxed);
+      cm.push_back((int32_t)scan);
+    }
+    int64_t a = (int64_t)cm.size() - 1, b = (int64_t)cm.size();  // the current level: numbers [a, b)
+    ++nlev;
+    for (;;) {
+      // children of the level: claim (level = 1) and the smallest parent number
+      tm.run([&](unsigned t) {
+        auto &v = loc[t];
+        v.clear();
+        const int64_t qa = a + (b - a) * t / tm.nt, qb = a + (b - a) * (t + 1) / tm.nt;
+        for (int64_t q = qa; q < qb; ++q) {
+          const int32_t u = cm[q];
+          for (int64_t e = ip[u]; e < ip[u + 1]; ++e) {
+            const int32_t w = (int32_t)ix[e];
+            int32_t expect = -1;
+            if (level[w].load(std::memory_order_relaxed) == -1 &&
+                level[w].compare_exchange_strong(expect, 1, std::memory_order_relaxed))
+              v.push_back(w);
+            if (level[w].load(std::memory_order_relaxed) == 1) {
+              int32_t k = akey[w].load(std::memory_order_relaxed);
+              while ((int32_t)q < k && !akey[w].compare_exchange_weak(k, (int32_t)q, std::memory_order_relaxed)) {
+              }
+            }
+          }
+        }
+      });
+      next.clear();
+      for (auto &v : loc) next.insert(next.end(), v.begin(), v.end());
+      if (next.empty()) break;
+      if ((int64_t)next.size() > wlimit) return false;
+      // counting sort by parent number, then (degree, index) within a parent
+      const int64_t span = b - a;
+      cnt.assign(span + 1, 0);
+      for (int32_t w : next) cnt[akey[w].load(std::memory_order_relaxed) - a + 1]++;
+      for (int64_t i = 0; i < span; ++i) cnt[i + 1] += cnt[i];
+      front.resize(next.size());
+      for (int32_t w : next) front[cnt[akey[w].load(std::memory_order_relaxed) - a]++] = w;
+      int64_t i0 = 0;
+      while (i0 < (int64_t)front.size()) {
+        const int32_t k0 = akey[front[i0]].load(std::memory_order_relaxed);
+        int64_t i1 = i0 + 1;
+        while (i1 < (int64_t)front.size() && akey[front[i1]].load(std::memory_order_relaxed) == k0) ++i1;
+        std::sort(front.begin() + i0, front.begin() + i1, [&](int32_t x, int32_t y) {
+          return deg(x) != deg(y) ? deg(x) < deg(y) : x < y;
+        });
+        i0 = i1;
+      }
+      for (int32_t w : front) level[w].store(2, std::memory_order_relaxed);  // numbered
+      a = (int64_t)cm.size();
+      cm.insert(cm.end(), front.begin(), front.end());
+      b = (int64_t)cm.size();
+      ++nlev;
+    }
+  }
+  (void)key;
+  perm.resize(n);
+  for (int64_t r = 0; r < n; ++r) perm[r] = cm[n - 1 - r];
+  if (levels) *levels = nlev;
+  return true;
+}
+
+template <typename I, typename MV>
+void renumber_csr(int64_t n, const I *ip, const I *ix, const MV *dv, const std::vector<int32_t> &perm,
+                  hvec<I> &ip2, hvec<I> &ix2, hvec<MV> &dv2) {
+  std::vector<int32_t> iperm(n);
+  for (int64_t r = 0; r < n; ++r) iperm[perm[r]] = (int32_t)r;
+  ip2.resize(n + 1);
+  ip2[0] = 0;
+  for (int64_t r = 0; r < n; ++r) ip2[r + 1] = ip2[r] + (ip[perm[r] + 1] - ip[perm[r]]);
+  const int64_t nnz = (int64_t)ip[n];
+  ix2.resize(nnz + 1);
+  dv2.resize(nnz + 1);
+  const unsigned nt = n < (int64_t(1) << 16) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int64_t r = n * t / nt; r < n * (t + 1) / nt; ++r) {
+        const int64_t o = perm[r];
+        int64_t q = (int64_t)ip2[r];
+        for (int64_t e = ip[o]; e < ip[o + 1]; ++e, ++q) {
+          ix2[q] = (I)iperm[ix[e]];
+          dv2[q] = dv[e];
+        }
+      }
+    });
+  for (auto &x : th) x.join();
+}
+
+template <typename I, typename MV>
+bool rs_build(int64_t n, const I *ip, const I *ix, const MV *dv, int64_t sell_slots, RsHost<MV> &p) {
+  constexpr int H = kPairSlice;
+  if (n == 0 || n >= (int64_t(1) << 28) - 1) return false;
+  const int64_t ns = (n + H - 1) / H;
+  p.width.assign(ns, 0);
+  p.sptr.assign(ns + 1, 0);
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t r = s * H; r < std::min<int64_t>(n, (s + 1) * H); ++r) w = std::max<int64_t>(w, ip[r + 1] - ip[r]);
+    if (w > INT32_MAX / H) return false;
+    p.width[s] = (int32_t)w;
+    p.max_width = std::max(p.max_width, (int)w);
+    p.sptr[s + 1] = p.sptr[s] + H * w;
+  }
+  const int64_t slots = p.sptr[ns];
+  if (slots == 0 || slots * 4 > sell_slots * 5 + (int64_t)4 * H * p.max_width) return false;
+  par_fill(p.colrank, slots + 2 * H, 0xFFFFFFFFu);
+  par_fill(p.val, slots + 2 * H, MV(0));
+  auto fill = [&](int64_t sa, int64_t sb) {
+    std::vector<std::pair<int64_t, int>> run;  // (column, position in run)
+    for (int64_t s = sa; s < sb; ++s) {
+      const int64_t r0 = s * H, r1 = std::min<int64_t>(n, r0 + H), base = p.sptr[s];
+      for (int64_t r = r0; r < r1; ++r) {
+        const int64_t e0 = (int64_t)ip[r], len = (int64_t)ip[r + 1] - e0;
+        for (int64_t c0 = 0; c0 < len; c0 += kRsChunk) {
+          const int m = (int)std::min<int64_t>(kRsChunk, len - c0);
+          run.clear();
+          for (int k = 0; k < m; ++k) run.emplace_back((int64_t)ix[e0 + c0 + k], k);
+          std::stable_sort(run.begin(), run.end(),
+                           [](const std::pair<int64_t, int> &x, const std::pair<int64_t, int> &y) { return x.first < y.first; });
+          for (int j = 0; j < m; ++j) {
+            const int64_t q = base + (c0 + j) * H + (r - r0);
+            p.colrank[q] = (uint32_t)run[j].first | ((uint32_t)run[j].second << 28);
+            p.val[q] = dv[e0 + c0 + run[j].second];
+          }
+        }
+      }
+    }
+  };
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 2048) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(fill, ns * t / nt, ns * (t + 1) / nt);
+  for (auto &x : th) x.join();
+  return true;
+}
+
 // Host-only view of the diagonal-offset plan (kry_dia_plan): the image
 // kry_csr_create would build for these CSR arrays, without a device.
 template <typename I>
@@ -498,6 +803,8 @@ static void cb_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64
 // explicit instantiations: the combinations kry_csr_create dispatches
 #define KRY_HOST_I(I)                                                                                              \
   template void check_csr<I>(int64_t, int64_t, const I *, const I *);                                            \
+  template bool scattered<I>(int64_t, const I *, const I *);                                                     \
+  template bool rcm_order<I>(int64_t, const I *, const I *, int64_t, std::vector<int32_t> &, int64_t *);          \
   template void sell_plan<I>(int64_t, const I *, std::vector<int64_t> *, std::vector<int32_t> *, int64_t *,     \
                              int64_t *, int64_t *);                                                              \
   template bool compact_fill<I>(const std::vector<int64_t> &, const std::vector<int32_t> &, const hvec<I> &,     \
@@ -507,7 +814,10 @@ static void cb_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64
                                  const std::vector<int32_t> &, hvec<I> &, hvec<MV> &);                          \
   template bool dia_build<I, MV>(int64_t, const I *, const I *, const MV *, int64_t, DiaHost<MV> &);            \
   template bool cb_build<I, MV>(int64_t, const I *, const I *, const MV *, CbHost<MV> &);                       \
-  template bool pair_build<I, MV>(int64_t, const I *, const I *, const MV *, int64_t, PairHost<MV> &);
+  template bool pair_build<I, MV>(int64_t, const I *, const I *, const MV *, int64_t, PairHost<MV> &);          \
+  template void renumber_csr<I, MV>(int64_t, const I *, const I *, const MV *, const std::vector<int32_t> &,    \
+                                    hvec<I> &, hvec<I> &, hvec<MV> &);                                          \
+  template bool rs_build<I, MV>(int64_t, const I *, const I *, const MV *, int64_t, RsHost<MV> &);
 KRY_HOST_I(int32_t)
 KRY_HOST_I(int64_t)
 KRY_HOST_IM(int32_t, float)
@@ -520,6 +830,7 @@ template void release_later<float>(hvec<float> &);
 template void release_later<double>(hvec<double> &);
 template void release_later<uint16_t>(hvec<uint16_t> &);
 template void release_later<uint64_t>(hvec<uint64_t> &);
+template void release_later<uint32_t>(hvec<uint32_t> &);
 
 }  // namespace kry
 
@@ -537,6 +848,25 @@ using namespace kry;
     kry::set_error(e.what());        \
     return KRY_EDEVICE;              \
   }
+
+template <typename I>
+static void rs_plan_host(int64_t n, int64_t nnz, const I *ip, const I *ix, int64_t *info, int32_t *widths,
+                         uint32_t *colrank) {
+  check_csr(n, nnz, ip, ix);
+  int64_t ns = 0, sell_slots = 0, irr = 0;
+  sell_plan(n, ip, nullptr, nullptr, &ns, &sell_slots, &irr);
+  hvec<double> zeros;
+  par_fill(zeros, (size_t)std::max<int64_t>(nnz, 1), 0.0);
+  RsHost<double> r;
+  const bool built = rs_build(n, ip, ix, zeros.data(), sell_slots, r);
+  info[0] = built ? 1 : 0;
+  info[1] = built ? (int64_t)r.width.size() : 0;
+  info[2] = built ? r.sptr.back() : 0;
+  info[3] = built ? r.max_width : 0;
+  if (!built) return;
+  if (widths) std::copy(r.width.begin(), r.width.end(), widths);
+  if (colrank) std::copy(r.colrank.begin(), r.colrank.begin() + r.sptr.back(), colrank);
+}
 
 extern "C" {
 
@@ -593,6 +923,44 @@ int kry_cb_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices,
     cb_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, gptr);
   else if (itype == KRY_I64)
     cb_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, gptr);
+  else
+    throw Error{KRY_EINVAL, "bad itype"};
+  KRY_API_END
+}
+
+int kry_rcm_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t wlimit,
+                 int64_t *info, int32_t *perm) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
+  const int64_t wl = wlimit > 0 ? wlimit : std::max<int64_t>(int64_t(1) << 16, n / 32);
+  std::vector<int32_t> p;
+  int64_t levels = 0;
+  bool built = false;
+  if (itype == KRY_I32) {
+    check_csr(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices));
+    built = rcm_order(n, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), wl, p, &levels);
+  } else if (itype == KRY_I64) {
+    check_csr(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices));
+    built = rcm_order(n, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), wl, p, &levels);
+  } else {
+    throw Error{KRY_EINVAL, "bad itype"};
+  }
+  info[0] = built ? 1 : 0;
+  info[1] = built ? levels : 0;
+  if (built && perm) std::copy(p.begin(), p.end(), perm);
+  KRY_API_END
+}
+
+int kry_rs_plan(int64_t n, int64_t nnz, const void *indptr, const void *indices, int itype, int64_t *info,
+                int32_t *widths, uint32_t *colrank) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(indptr && info && n >= 0 && nnz >= 0 && (nnz == 0 || indices), KRY_EINVAL, "bad plan arguments");
+  if (itype == KRY_I32)
+    rs_plan_host(n, nnz, static_cast<const int32_t *>(indptr), static_cast<const int32_t *>(indices), info, widths,
+                 colrank);
+  else if (itype == KRY_I64)
+    rs_plan_host(n, nnz, static_cast<const int64_t *>(indptr), static_cast<const int64_t *>(indices), info, widths,
+                 colrank);
   else
     throw Error{KRY_EINVAL, "bad itype"};
   KRY_API_END

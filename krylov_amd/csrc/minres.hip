@@ -800,6 +800,8 @@ int kry_minres_set_preconditioners(kry_minres *s, kry_csr *M, kry_csr *Ml, kry_c
     KRY_REQUIRE(op->n == s->n, KRY_EINVAL, "preconditioner shape does not match the operator");
     KRY_REQUIRE(op->dtype == s->dtype || (s->dtype == KRY_F64 && op->dtype == KRY_F32), KRY_EINVAL,
                 "preconditioner dtype must match the vectors (or be float32 under float64 vectors)");
+    KRY_REQUIRE(op->renumbered == s->A->renumbered && op->perm_hash == s->A->perm_hash, KRY_EINVAL,
+                "preconditioner renumbered differently from the operator (build it with kry_csr_create_like)");
   }
   KRY_HIP(hipSetDevice(s->ctx->device));
   const size_t vb = ((size_t)s->n * s->k + 15) / 16 * 16 * dsize(s->dtype);
@@ -844,18 +846,18 @@ int kry_minres_start(kry_minres *s, kry_vec *b, kry_vec *x0, kry_vec *w, double 
   hipStream_t st = s->ctx->stream;
   const size_t elems = ((size_t)s->n * s->k + 15) / 16 * 16;
   const size_t vb = b->bytes();
-  KRY_HIP(hipMemcpyAsync(s->b, b->d, vb, hipMemcpyDeviceToDevice, st));
+  load_in(s->A, b->d, s->b, s->k, dsize(s->dtype), st);  // the caller's numbering in
   dev_free(s->x0);
   s->x0 = nullptr;
   if (x0) {
     s->x0 = dev_alloc(elems * dsize(s->dtype));
-    KRY_HIP(hipMemcpyAsync(s->x0, x0->d, vb, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, x0->d, s->x0, s->k, dsize(s->dtype), st);
   }
   dev_free(s->w);
   s->w = nullptr;
   if (w) {
     s->w = static_cast<double *>(dev_alloc(((size_t)s->n + 1) * 8));
-    KRY_HIP(hipMemcpyAsync(s->w, w->d, (size_t)s->n * 8, hipMemcpyDeviceToDevice, st));
+    load_in(s->A, w->d, s->w, 1, 8, st);
   }
   s->inner_f32 = (s->dtype == KRY_F32 && !w);
   KRY_HIP(hipMemsetAsync(s->yk, 0, vb, st));
@@ -967,7 +969,6 @@ int kry_minres_get(kry_minres *s, int which, void *host) {
   KRY_REQUIRE(s && host && which >= 0 && which <= 3, KRY_EINVAL, "bad argument");
   KRY_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  const int64_t N = s->n * (int64_t)s->k;
   if (which != 0) {
     KRY_REQUIRE(s->started, KRY_EINVAL, "kry_minres_start has not been called");
     if (which == 3) {
@@ -975,7 +976,7 @@ int kry_minres_get(kry_minres *s, int which, void *host) {
     } else {
       const void *src = s->P[s->it % 3];
       if (which == 2 && s->M) src = s->Vr[s->it % 2];
-      KRY_HIP(hipMemcpyAsync(host, src, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
+      store_out(s->A, src, host, s->k, dsize(s->dtype), st);
     }
     KRY_HIP(hipStreamSynchronize(st));
     return KRY_OK;
@@ -984,7 +985,7 @@ int kry_minres_get(kry_minres *s, int which, void *host) {
     mr_compute_xk<double>(s);
   else
     mr_compute_xk<float>(s);
-  KRY_HIP(hipMemcpyAsync(host, s->xk, (size_t)N * dsize(s->dtype), hipMemcpyDeviceToHost, st));
+  store_out(s->A, s->xk, host, s->k, dsize(s->dtype), st);
   KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END
 }

@@ -94,6 +94,30 @@ struct kry_csr {
   void *sp_cbase = nullptr;  // int32, sp_nslots / kPairSlice (+ kDiaPad)
   void *sp_delta = nullptr;  // uint16, sp_nslots (+ pad)
   void *sp_val = nullptr;    // dtype, sp_nslots (+ pad)
+  // rank-sorted SELL-128 image (round 5; spmv_rs_kernel, host_image.hpp
+  // rs_build): the paired-row geometry with int32 columns, each run of
+  // kRsChunk stored entries of a row sorted by column, the entry's position
+  // in its run in the word's top 4 bits (the kernel sums the run back in
+  // stored order). Built for k = 1 when no DIA, column-blocked or paired image
+  // is (unsorted rows, wide slot columns: a renumbered matrix).
+  bool rs = false;
+  int64_t rs_nslices = 0, rs_nslots = 0;
+  int rs_max_width = 0;
+  void *rs_sptr = nullptr;     // int64, rs_nslices + 1
+  void *rs_width = nullptr;    // int32, rs_nslices
+  void *rs_colrank = nullptr;  // uint32, rs_nslots (+ pad): column | run position << 28, 0xFFFFFFFF = padding
+  void *rs_val = nullptr;      // dtype, rs_nslots (+ pad)
+  // bandwidth-reducing renumbering (round 5): every image holds P A P^T
+  // (row r of the images is the caller's row perm[r], rows' entries in their
+  // stored order), and the solvers work in that numbering; vectors cross the
+  // C-ABI in the caller's numbering (kry_*_start permutes b / x0 / weights in,
+  // kry_*_get / kry_gmres_xk_device / kry_spmv permute results out).
+  bool renumbered = false;
+  std::vector<int32_t> perm_host;  // new -> old (preconditioners built "like" this operator reuse it)
+  uint64_t perm_hash = 0;          // preconditioners must carry the same renumbering
+  int64_t rcm_levels = 0;
+  void *perm = nullptr;            // int32, n: new -> old
+  void *iperm = nullptr;           // int32, n: old -> new
   // CSR arrays, kept on the device only when irregular slices exist
   void *indptr = nullptr;
   void *indices = nullptr;
@@ -119,6 +143,21 @@ void dev_free(void *p);  // to the caching pool (abi_core.hip)
 void mem_stats(int64_t *out);
 void mem_release();
 double *ctx_scratch(kry_ctx *ctx, size_t bytes);  // grown on demand, owned by the context
+// Renumbered operators (kry_csr::renumbered): rows of an n x k block moved
+// between the caller's numbering and the operator's. to_op: dst[r] = src[perm[r]]
+// (into the operator's numbering); otherwise dst[o] = src[iperm[o]]. Both are
+// gathers (no scatter races). Plain copies when A is not renumbered.
+void permute_rows(const kry_csr *A, const void *src, void *dst, int k, size_t esize, bool to_op, hipStream_t st);
+// The solver-start form: a caller-numbered block into solver storage.
+void load_in(const kry_csr *A, const void *src, void *dst, int k, size_t esize, hipStream_t st);
+// The get form: solver storage (operator numbering) to a host buffer in the
+// caller's numbering (through a temporary device block when renumbered).
+void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st);
+// Reverse Cuthill-McKee on the device over device CSR arrays (renumber.hip):
+// 1 built, 0 refused (a level wider than wlimit), -1 gave up (too many
+// components: use the host order, host_image.hpp rcm_order, the same order).
+int rcm_order_device(kry_ctx *ctx, int64_t n, const int32_t *d_ip, const int32_t *d_ix, int64_t wlimit,
+                     std::vector<int32_t> &perm, int64_t *levels);
 
 // Event-timed launch bracket used by the solvers around their SpMV launches.
 struct ProfScope {

@@ -81,6 +81,25 @@ class ShardComm:
         return c
 
     @classmethod
+    def all_devices(cls, devices):
+        """One communicator per device of THIS process (kry_comm_create_all,
+        ncclCommInitAll): the single-process multi-GPU path, rank i on
+        devices[i], each driven by its own host thread."""
+        devices = [int(d) for d in devices]
+        ctxs = [get_context(d) for d in devices]
+        arr = (ctypes.c_void_p * len(devices))(*[c.handle.value for c in ctxs])
+        outs = (ctypes.c_void_p * len(devices))()
+        check(lib.kry_comm_create_all(arr, len(devices), outs))
+        comms = []
+        for i, c in enumerate(ctxs):
+            obj = cls.__new__(cls)
+            obj.ctx, obj.rank, obj.world = c, i, len(devices)
+            obj.handle = ctypes.c_void_p(outs[i])
+            obj._fin = _lib.own(obj, lib.kry_comm_destroy, obj.handle)
+            comms.append(obj)
+        return comms
+
+    @classmethod
     def from_file(cls, path, rank, world, device=None, timeout=120.0):
         """Create the communicator without PyTorch: rank 0 writes the unique id
         to ``path`` (a fresh file name on a file system every rank sees, e.g.
@@ -131,7 +150,7 @@ def _run_global(lib_run, h, steps, total):
     return out[: done.value], bool(inv.value)
 
 
-def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None):
+def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None, kcs=None):
     """Block CG on this rank's RHS columns ``B`` (n, k_local), k_local equal
     on every rank, with the reference's global stop rule.
 
@@ -142,7 +161,7 @@ def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None)
     if callback is not None:
         raise NotImplementedError("callbacks are not supported on the sharded path")
     prob = Problem(A, _block(B), x0, None, device=comm.ctx.device)
-    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world, kcs)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
     st = _CGState(prob)
     check(lib.kry_cg_attach_comm(st.h, comm.handle, lay.off, lay.total))
@@ -154,7 +173,7 @@ def cg(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None)
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)
 
 
-def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"):
+def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs", kcs=None):
     """GMRES (MGS) on this rank's RHS columns ``B`` (n, k_local), k_local
     equal on every rank. Every Arnoldi step performs one RCCL allreduce of the
     residual norms and a non-invariant count, so all ranks apply the
@@ -168,7 +187,7 @@ def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"
     sweeps = 1 if len(ortho) == 3 else int(ortho[3:])
     prob = Problem(A, _block(B), x0, None, device=comm.ctx.device)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world, kcs)
     st = _GmresState(prob, maxiter, sweeps)
     check(lib.kry_gmres_attach_comm(st.h, comm.handle, lay.off, lay.total))
 
@@ -189,7 +208,7 @@ def gmres(A, B, comm, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None, ortho="mgs"
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=ops)
 
 
-def minres(A, B, comm, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None):
+def minres(A, B, comm, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, kcs=None):
     """MINRES on this rank's RHS columns ``B`` (n, k_local), k_local equal on
     every rank; one RCCL allreduce per iteration for the global stop rule
     (minres.py:162) and the Lanczos invariance test over all columns.
@@ -198,7 +217,7 @@ def minres(A, B, comm, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None
 
     prob = Problem(A, _block(B), x0, inner, device=comm.ctx.device)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
-    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world)
+    lay = ShardLayout(prob.kc, prob.kpad, comm.rank, comm.world, kcs)
     st = _MinresState(prob)
     check(lib.kry_minres_attach_comm(st.h, comm.handle, lay.off, lay.total))
     eng = _Engine(st, lambda steps: _run_global(lib.kry_minres_run, st.h, steps, lay.total), lay.total, st.start,

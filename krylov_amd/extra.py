@@ -35,8 +35,26 @@ class _Dev:
             raise NotImplementedError("at most 64 right-hand-side columns on bicgstab / cgs / cgr / gcr")
         self.prob = prob
         self.ctx = prob.ctx
-        self.w = prob.w_dev
+        # the chain's vectors live in the operator's numbering (a renumbered
+        # A: b and the weights moved in once; uploads and downloads move rows)
+        self.renumbered = prob.A.renumbered
+        self.b = self._to_op(prob.b_dev)
+        self.w = None if prob.w_dev is None else self._to_op(prob.w_dev)
         self.out = HostOut((prob.n, prob.kpad), prob.dtype)  # the returned iterate's pages, faulted in meanwhile
+
+    def _to_op(self, v):
+        if not self.renumbered:
+            return v
+        t = DeviceVector(self.ctx, v.n, v.k, v.dtype)
+        self.prob.A.permute(v, t, True)
+        return t
+
+    def _from_op(self, v):
+        if not self.renumbered:
+            return v
+        t = DeviceVector(self.ctx, v.n, v.k, v.dtype)
+        self.prob.A.permute(v, t, False)
+        return t
 
     def zeros(self):
         v = DeviceVector(self.ctx, self.prob.n, self.prob.kpad, self.prob.dtype)
@@ -45,21 +63,21 @@ class _Dev:
     def upload(self, a):
         v = self.zeros()
         v.upload(self.prob.pad(np.asarray(a).astype(self.prob.dtype, copy=False)))
-        return v
+        return self._to_op(v)
 
     def host(self, v):
-        return self.prob.unpad_vec(v.to_host(), self.prob.r0_dtype)
+        return self.prob.unpad_vec(self._from_op(v).to_host(), self.prob.r0_dtype)
 
     def host_final(self, v):
         """The returned iterate, into the array allocated at the start."""
-        return self.prob.unpad_vec(v.to_host(out=self.out.take()), self.prob.r0_dtype)
+        return self.prob.unpad_vec(self._from_op(v).to_host(out=self.out.take()), self.prob.r0_dtype)
 
     def matvec(self, op, x):
         """op @ x into a new vector; op None = the reference's Identity (x itself)."""
         if op is None:
             return x
         y = self.zeros()
-        op.matvec_device(x, y)
+        op.matvec_op(x, y)
         return y
 
     def A(self, x):
@@ -89,7 +107,7 @@ class _Dev:
 
     def residual(self, x):
         """b - A @ x."""
-        return self.lc(LC_SUB, self.prob.b_dev, self.A(x))
+        return self.lc(LC_SUB, self.b, self.A(x))
 
     def cols(self, v):
         """kpad per-column values -> the reference's scalar / (k,) array."""
@@ -186,7 +204,7 @@ def _start(D, x0):
     prob = D.prob
     if x0 is None:
         x = D.zeros()
-        r0 = D.copy(prob.b_dev)
+        r0 = D.copy(D.b)
     else:
         x = D.upload(x0)
         r0 = D.residual(x)
@@ -231,7 +249,7 @@ def bicgstab(A, b, Ml=None, Mr=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15
         C.lc(LC_AXPY, h, x, st, y=y, a="alpha")  # h = x + alpha y
         # resnorm_h = _norm(Ml (b - A x)) of the previous iterate x (bicgstab.py:123)
         C.spmv(prob.A, x, rx, st)
-        C.lc(LC_SUB, rx, prob.b_dev, st, y=rx)
+        C.lc(LC_SUB, rx, D.b, st, y=rx)
         C.norm(C.apply("Ml", rx, t3, st), t4, "nh", st, M="Ml" if ml else None)
         C.check("nh", st, mode=1)
         ml_s = C.apply("Ml", s_, t3, st)
@@ -344,7 +362,7 @@ def cgr(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None,
     D = _Dev(prob)
     if x0 is None:
         x = D.zeros()
-        r = D.copy(prob.b_dev)
+        r = D.copy(D.b)
     else:
         x = D.upload(x0)
         r = D.residual(x)
@@ -416,7 +434,7 @@ def gcr(A, b, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callbac
     D = _Dev(prob)
     if x0 is None:
         x = D.zeros()
-        r = D.copy(prob.b_dev)
+        r = D.copy(D.b)
     else:
         x = D.upload(x0)
         r = D.residual(x)
@@ -443,7 +461,7 @@ def gcr(A, b, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callbac
         C.sc(SOP_GUARD, "gb", st, a="beta")
         C.lc(LC_DIV, v[-1], v[-1], st, a="gb")
         C.lc(LC_DIV, s[-1], s[-1], st, a="gb")
-        C.dot(prob.b_dev, v[-1], "gamma", st)
+        C.dot(D.b, v[-1], "gamma", st)
         C.lc(LC_AXPY, x, x, st, y=s[-1], a="gamma")
         C.lc(LC_AXPY, r, r, st, y=v[-1], a="gamma", sa=-1.0)
         C.norm(r, None, "nr", st)

@@ -163,11 +163,18 @@ def arnoldi(A, v, maxiter, ortho="mgs", M=None, inner=None):
 
 
 def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=1e-5, atol=1.0e-15,
-          maxiter=None, callback=None):
+          maxiter=None, callback=None, *, devices=None):
     """Preconditioned GMRES, reference signature (``gmres.py:41-54``).
 
     ``ortho``: "mgs", "mgsK" (K MGS sweeps) or "householder" (Householder
     Arnoldi, arnoldi.py:33-104, one right-hand side, default inner, no M)."""
+    if devices is not None:  # several GPUs of this process (krylov_amd.multi)
+        if inner is not None:
+            raise NotImplementedError("devices=[...] takes the Euclidean inner product")
+        from .multi import solve
+
+        return solve("gmres", A, b, devices, x0=x0, tol=tol, atol=atol, maxiter=maxiter, ortho=ortho,
+                     callback=callback, M=M, Ml=Ml, Mr=Mr)
     sweeps = _sweeps(ortho, inner, M, b)
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
@@ -312,6 +319,9 @@ def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycle
     Aop = as_device_operator(A)
     b = np.asarray(b)
     prob = Problem(Aop, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
+    if max_cycles <= 0:  # no cycle: the iterate is x0 (zeros_like(b) without one), as the reference's start
+        return (np.array(x0, dtype=prob.r0_dtype, copy=True) if x0 is not None
+                else np.zeros(b.shape, dtype=prob.r0_dtype)), []
     # ||b|| (with Ml: ||Ml b||) in the solve's inner product, on the device:
     # the same two-stage reduction as the cycles' ||Ml (b - A x_c)|| (a host
     # norm of an 80 MB b took ~5 ms per call at the metric size)

@@ -110,8 +110,15 @@ def lanczos(A, v, maxiter, M=None, inner=None):
 
 
 def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxiter=None,
-           callback=None):
-    """Preconditioned MINRES, reference signature (``minres.py:28-40``)."""
+           callback=None, *, devices=None):
+    """Preconditioned MINRES, reference signature (``minres.py:28-40``).
+    ``devices=[...]``: the columns of a block ``b`` over several GPUs of this
+    process (``krylov_amd.multi``)."""
+    if devices is not None:
+        from .multi import solve
+
+        return solve("minres", A, b, devices, x0=x0, inner=inner, tol=tol, atol=atol, maxiter=maxiter,
+                     callback=callback, M=M, Ml=Ml, Mr=Mr)
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter

@@ -28,15 +28,24 @@ import numpy as np
 class ShardLayout:
     """Where this rank's columns sit in the global per-column vectors."""
 
-    def __init__(self, kc, kpad, rank, world):
+    def __init__(self, kc, kpad, rank, world, kcs=None):
+        """``kc`` device columns per rank (padded to ``kpad``); ``kcs``: the
+        real columns of each rank when they differ (an uneven split of K
+        columns: every rank holds kc device columns, rank r's first kcs[r]
+        real and the rest zero columns that never enter the history or the
+        stop rule); default kc on every rank."""
         if not (0 <= rank < world) or kc < 1 or kpad < kc:
             raise ValueError(f"bad shard layout kc={kc} kpad={kpad} rank={rank} world={world}")
+        kcs = [int(kc)] * int(world) if kcs is None else [int(c) for c in kcs]
+        if len(kcs) != world or any(c < 1 or c > kc for c in kcs):
+            raise ValueError(f"bad per-rank column counts {kcs} for kc={kc}, world={world}")
         self.kc, self.kpad, self.rank, self.world = int(kc), int(kpad), int(rank), int(world)
+        self.kcs = kcs
         self.total = self.kpad * self.world
         self.off = self.kpad * self.rank
         # global slot of every real column, in rank order (the reference's
         # column order of the unsharded block)
-        self.real = np.concatenate([np.arange(r * self.kpad, r * self.kpad + self.kc) for r in range(self.world)])
+        self.real = np.concatenate([np.arange(r * self.kpad, r * self.kpad + kcs[r]) for r in range(self.world)])
 
     def glob(self, local_vals, allreduce):
         """This rank's kpad values -> the global vector (zero-padded sum over

@@ -25,7 +25,14 @@ def _next_pow2(k):
 
 
 class CsrOperator:
-    def __init__(self, A, device=None):
+    """A device-resident CSR matrix. ``like``: build it with another
+    operator's bandwidth-reducing renumbering (a preconditioner of a
+    renumbered operator, kry_csr_create_like); the device picks the
+    renumbering on its own otherwise (reverse Cuthill-McKee for scattered
+    matrices with a narrow level structure). Vectors always cross in the
+    caller's numbering."""
+
+    def __init__(self, A, device=None, like=None):
         if isinstance(A, CsrOperator):
             raise TypeError("already a CsrOperator")
         if scipy.sparse.issparse(A):
@@ -57,14 +64,25 @@ class CsrOperator:
         data = np.ascontiguousarray(csr.data, dtype=dt)
         self.index_dtype = np.dtype(itype)
         h = ctypes.c_void_p()
-        check(
-            lib.kry_csr_create(
-                self.ctx.handle, self.n, self.nnz, _lib.ptr(indptr), _lib.ptr(indices),
-                _lib.ptr(data), _lib.dtype_code(dt), _lib.itype_code(itype), ctypes.byref(h),
+        if like is not None and like.renumbered:
+            if like.ctx is not self.ctx or like.n != self.n:
+                raise ValueError("like: an operator of the same size on the same device")
+            check(
+                lib.kry_csr_create_like(
+                    self.ctx.handle, like.handle, self.n, self.nnz, _lib.ptr(indptr), _lib.ptr(indices),
+                    _lib.ptr(data), _lib.dtype_code(dt), _lib.itype_code(itype), ctypes.byref(h),
+                )
             )
-        )
+        else:
+            check(
+                lib.kry_csr_create(
+                    self.ctx.handle, self.n, self.nnz, _lib.ptr(indptr), _lib.ptr(indices),
+                    _lib.ptr(data), _lib.dtype_code(dt), _lib.itype_code(itype), ctypes.byref(h),
+                )
+            )
         self.handle = h
         self._fin = _lib.own(self, lib.kry_csr_destroy, h)
+        self.renumbered = self.layout()["renumbered"]
 
     @property
     def device(self):
@@ -72,16 +90,28 @@ class CsrOperator:
 
     def layout(self):
         """The device image: {"slices", "slots", "irregular", "compact",
-        "col_blocks", "dia", "dia_slots", "pair", "pair_slots"} (kry_csr_info_n)."""
-        info = np.zeros(9, dtype=np.int64)
-        check(lib.kry_csr_info_n(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 9))
+        "col_blocks", "dia", "dia_slots", "pair", "pair_slots", "rs",
+        "rs_slots", "renumbered", "rcm_levels"} (kry_csr_info_n)."""
+        info = np.zeros(13, dtype=np.int64)
+        check(lib.kry_csr_info_n(self.handle, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 13))
         return {"slices": int(info[0]), "slots": int(info[1]), "irregular": int(info[2]), "compact": bool(info[3]),
                 "col_blocks": int(info[4]), "dia": bool(info[5]), "dia_slots": int(info[6]), "pair": bool(info[7]),
-                "pair_slots": int(info[8])}
+                "pair_slots": int(info[8]), "rs": bool(info[9]), "rs_slots": int(info[10]),
+                "renumbered": bool(info[11]), "rcm_levels": int(info[12])}
 
     def matvec_device(self, x, y):
-        """y = A x for DeviceVectors (no host traffic)."""
+        """y = A x for DeviceVectors in the caller's numbering (no host traffic)."""
         check(lib.kry_spmv(self.ctx.handle, self.handle, x.handle, y.handle))
+
+    def matvec_op(self, x, y):
+        """y = A x for DeviceVectors already in the operator's numbering
+        (kry_spmv_op; the same as matvec_device when not renumbered)."""
+        check(lib.kry_spmv_op(self.ctx.handle, self.handle, x.handle, y.handle))
+
+    def permute(self, src, dst, to_operator):
+        """dst = src with its rows moved into (to_operator) or out of the
+        operator's numbering (kry_csr_permute; a copy when not renumbered)."""
+        check(lib.kry_csr_permute(self.ctx.handle, self.handle, src.handle, dst.handle, 1 if to_operator else 0))
 
     def __matmul__(self, x):
         x = np.asarray(x)
@@ -146,23 +176,27 @@ def clear_operator_cache():
     _lib.empty_cache()
 
 
-def as_device_operator(A, device=None):
-    """Return ``A`` as a CsrOperator (uploading scipy/dense inputs once)."""
+def as_device_operator(A, device=None, like=None):
+    """Return ``A`` as a CsrOperator (uploading scipy/dense inputs once).
+    ``like``: the operator a preconditioner serves; when it is renumbered the
+    preconditioner is built with its renumbering (a CsrOperator given as a
+    preconditioner must already carry it)."""
     import os
 
+    lk = like if (like is not None and like.renumbered) else None
     if isinstance(A, CsrOperator):
         return A
     if os.environ.get("KRYLOV_CSR_CACHE", "1") == "0":
-        return CsrOperator(A, device=device)
+        return CsrOperator(A, device=device, like=lk)
     dev = get_context(device).device
     fp = _fingerprint(A)
     if fp is None:
-        return CsrOperator(A, device=device)
-    key = (dev, id(A))
+        return CsrOperator(A, device=device, like=lk)
+    key = (dev, id(A), None if lk is None else id(lk))
     hit = _cache.get(key)
     if hit is not None and hit[0]() is A and hit[1] == fp:
         return hit[2]
-    op = CsrOperator(A, device=dev)
+    op = CsrOperator(A, device=dev, like=lk)
     try:
         ref = weakref.ref(A, lambda _r, key=key: _cache.pop(key, None))
     except TypeError:

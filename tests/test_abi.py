@@ -472,3 +472,190 @@ def test_plans_reject_malformed_csr(plan, defect):
     fn = {"dia": _lib.dia_plan, "pair": _lib.pair_plan, "cb": _lib.cb_plan}[plan]
     with pytest.raises(ValueError):
         fn(ip, ix)
+
+
+def _rcm_py(indptr, indices, wlimit):
+    """Restatement of kry_rcm_plan (host_image.hpp rcm_order): George-Liu
+    root from the lowest-index node of smallest degree (at most 4 BFS
+    sweeps, the last level's smallest (degree, index) node next while the
+    level count grows), Cuthill-McKee levels ordered by (smallest parent
+    number, degree, index), new components from the lowest unnumbered index,
+    reversed. None when a BFS level exceeds wlimit."""
+    ip = indptr.astype(np.int64)
+    ix = indices.astype(np.int64)
+    n = ip.shape[0] - 1
+    deg = np.diff(ip)
+
+    def nbrs(v):
+        return ix[ip[v]:ip[v + 1]]
+
+    def sweep(root):
+        level = np.full(n, -1)
+        level[root] = 0
+        front, nl = [root], 1
+        while True:
+            nxt = []
+            for u in front:
+                for w in nbrs(u):
+                    if level[w] == -1:
+                        level[w] = nl
+                        nxt.append(int(w))
+            if not nxt:
+                break
+            if len(nxt) > wlimit:
+                return None
+            front, nl = nxt, nl + 1
+        return nl, min(front, key=lambda v: (deg[v], v))
+
+    root = int(np.lexsort((np.arange(n), deg))[0])
+    r = sweep(root)
+    if r is None:
+        return None
+    ecc, cand = r
+    for _ in range(3):
+        if cand == root:
+            break
+        r2 = sweep(cand)
+        if r2 is None:
+            return None
+        if r2[0] <= ecc:
+            break
+        root, ecc, cand = cand, r2[0], r2[1]
+    num = np.full(n, -1)
+    cm, scan, levels = [], 0, 0
+    while len(cm) < n:
+        if not cm:
+            start = root
+        else:
+            while num[scan] != -1:
+                scan += 1
+            start = scan
+        num[start] = len(cm)
+        cm.append(start)
+        a, b = len(cm) - 1, len(cm)
+        levels += 1
+        while True:
+            key = {}
+            for q in range(a, b):
+                for w in nbrs(cm[q]):
+                    w = int(w)
+                    if num[w] == -1:
+                        key[w] = min(key.get(w, q), q)
+            if not key:
+                break
+            if len(key) > wlimit:
+                return None
+            nxt = sorted(key, key=lambda w: (key[w], deg[w], w))
+            for w in nxt:
+                num[w] = len(cm)
+                cm.append(w)
+            a, b = b, len(cm)
+            levels += 1
+    return np.array(cm[::-1], dtype=np.int32), levels
+
+
+def _sym_perm(A, seed):
+    p = np.random.default_rng(seed).permutation(A.shape[0])
+    return A[p][:, p].tocsr()
+
+
+@pytest.mark.parametrize("case", ["grid", "threaded", "components", "unsymmetric", "refused"])
+def test_rcm_plan_matches_restatement(case):
+    """The host renumbering (kry_rcm_plan: reverse Cuthill-McKee with a
+    George-Liu root) against a pure-Python restatement of the same
+    definition, node for node: a randomly numbered 2-D grid, one large enough
+    for the threaded level passes (n > 2^16), disconnected components with
+    isolated nodes, an unsymmetric pattern, and the refusal of a random graph
+    whose BFS levels exceed the width limit. The renumbering brings the
+    grid's bandwidth back to O(sqrt n)."""
+    import scipy.sparse as sp
+    from krylov_amd import _lib, problems
+
+    wlimit = 1 << 16
+    if case == "grid":
+        A = _sym_perm(problems.poisson2d(30), 1)
+    elif case == "threaded":
+        A = _sym_perm(problems.poisson2d(265), 2)
+    elif case == "components":
+        A = _sym_perm(sp.block_diag([problems.poisson2d(12), sp.identity(7), problems.poisson2d(9)]).tocsr(), 3)
+    elif case == "unsymmetric":
+        rng = np.random.default_rng(4)
+        L = sp.random(600, 600, density=0.004, random_state=5, format="csr") + sp.identity(600)
+        A = _sym_perm(sp.tril(L).tocsr() + sp.diags(rng.uniform(1, 2, 600), 1, shape=(600, 600)), 6)
+    else:
+        A = problems.random_nonsym(20_000, per_row=6, seed=7)
+        wlimit = 500
+    A = A.tocsr()
+    A.sort_indices()
+    ip, ix = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+    got = _lib.rcm_plan(ip, ix, wlimit)
+    want = _rcm_py(ip, ix, wlimit)
+    if case == "refused":
+        assert got is None and want is None
+        return
+    assert got is not None and want is not None
+    np.testing.assert_array_equal(got[0], want[0])
+    assert got[1] == want[1]
+    assert np.array_equal(np.sort(got[0]), np.arange(A.shape[0]))
+    if case in ("grid", "threaded"):
+        p = got[0]
+        B = A[p][:, p].tocoo()
+        m = int(round(np.sqrt(A.shape[0])))
+        assert np.abs(B.row - B.col).max() <= 2 * m + 2
+
+
+def _rs_plan_py(indptr, indices):
+    """Restatement of kry_rs_plan: slices of 128 rows, width = the longest
+    row, slot (j, r) of a slice at 128 * (sptr[s] / 128 + j) + r - 128 s holds
+    the j-th entry of row r with every run of 16 stored entries sorted by
+    column (ties in stored order), as column | position-in-run << 28;
+    padding 0xFFFFFFFF; refused above 1.25x the SELL-64 slots."""
+    ip = indptr.astype(np.int64)
+    n = ip.shape[0] - 1
+    lens = np.diff(ip)
+    ns = (n + 127) // 128
+    widths = np.array([lens[128 * s:128 * s + 128].max() for s in range(ns)], dtype=np.int64)
+    sptr = np.concatenate([[0], 128 * np.cumsum(widths)])
+    sell = sum(64 * lens[64 * s:64 * s + 64].max() for s in range((n + 63) // 64))
+    if sptr[-1] == 0 or sptr[-1] * 4 > sell * 5 + 4 * 128 * widths.max():
+        return None
+    cr = np.full(sptr[-1], 0xFFFFFFFF, dtype=np.uint32)
+    for r in range(n):
+        s = r // 128
+        cols = indices[ip[r]:ip[r + 1]].astype(np.int64)
+        for c0 in range(0, len(cols), 16):
+            run = cols[c0:c0 + 16]
+            order = np.argsort(run, kind="stable")
+            for j, k in enumerate(order):
+                cr[sptr[s] + 128 * (c0 + j) + r - 128 * s] = run[k] | (k << 28)
+    return {"slices": ns, "slots": int(sptr[-1]), "widths": widths.astype(np.int32), "colrank": cr}
+
+
+@pytest.mark.parametrize("case", ["unsorted", "long_rows", "duplicates"])
+def test_rs_plan_matches_restatement(case):
+    """The rank-sorted SELL-128 image's host side (kry_rs_plan) against a
+    NumPy restatement: unsorted rows, rows longer than one 16-entry run, and
+    duplicate columns (stable order)."""
+    import scipy.sparse as sp
+    from krylov_amd import _lib, problems
+
+    if case == "unsorted":
+        A = _sym_perm(problems.stencil15_3d(12), 8)  # the permuted columns of each row are unsorted in storage
+        ip, ix = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+        ix = ix.copy()
+        rng = np.random.default_rng(9)
+        for r in range(0, A.shape[0], 3):
+            seg = ix[ip[r]:ip[r + 1]]
+            rng.shuffle(seg)
+    elif case == "long_rows":
+        A = sp.random(700, 700, density=0.06, random_state=10, format="csr") + sp.identity(700, format="csr")
+        ip, ix = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+    else:
+        ip = np.array([0, 3, 5, 9], dtype=np.int32)
+        ix = np.array([2, 0, 2, 1, 1, 0, 2, 0, 1], dtype=np.int32)
+    got = _lib.rs_plan(ip, ix)
+    want = _rs_plan_py(ip, ix)
+    assert got is not None and want is not None
+    assert got["slices"] == want["slices"] and got["slots"] == want["slots"]
+    np.testing.assert_array_equal(got["widths"], want["widths"])
+    np.testing.assert_array_equal(got["colrank"], want["colrank"])

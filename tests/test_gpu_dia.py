@@ -361,15 +361,15 @@ def test_single_rhs_cg_deferred_y_bitwise(path, monkeypatch):
 
 def test_block_cg_default_ring_depth(monkeypatch):
     """The deferral policy without an override: an n x k block above 128 MB
-    (Poisson 1500^2 x 8 columns, 144 MB) defers yk 31 steps at a time, its
-    ring of 31 p buffers and 31 x k alphas reported by kry_cg_defer_info;
+    (Poisson 1500^2 x 8 columns, 144 MB) defers yk 15 steps at a time, its
+    ring of 15 p buffers and 15 x k alphas reported by kry_cg_defer_info;
     a block below 128 MB does not defer."""
     import krylov_amd
     from krylov_amd import _helpers, problems
     from krylov_amd.cg import _CGState
 
     monkeypatch.delenv("KRY_CG_YDEFER", raising=False)
-    for m, want in ((1500, 31), (1000, 0)):
+    for m, want in ((1500, 15), (1000, 0)):
         P = problems.poisson2d(m)
         B = np.random.default_rng(m).standard_normal((P.shape[0], 8))
         st = _CGState(_helpers.Problem(krylov_amd.CsrOperator(P), B, None, None))
@@ -380,3 +380,54 @@ def test_block_cg_default_ring_depth(monkeypatch):
         assert D == want
         vb = (P.shape[0] * 8 + 15) // 16 * 16 * 8
         assert nbytes == (D * vb + D * 8 * 8 if D else 0)
+
+
+def _hip_free_bytes():
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    return free.value
+
+
+def test_block_cg_ring_depth_follows_free_memory(monkeypatch):
+    """The default ring is sized by what is free when the solver first runs
+    (a quarter of it, and at most 10 GB): with a balloon allocated next to
+    the solver so that about 2.5 GB stay free, the 144 MB block gets D = 3
+    (3 x 144 MB fit 625 MB, 7 x 144 MB do not) and still iterates bitwise as
+    one update per step."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+    from krylov_amd.device import DeviceVector
+
+    monkeypatch.delenv("KRY_CG_YDEFER", raising=False)
+    P = problems.poisson2d(1500)
+    B = np.random.default_rng(7).standard_normal((P.shape[0], 8))
+    A = krylov_amd.CsrOperator(P)
+
+    def solve():
+        st = _CGState(_helpers.Problem(A, B, None, None))
+        st.start()
+        st.set_criterion(np.zeros(8))
+        return st
+
+    st = solve()
+    krylov_amd.empty_cache()
+    keep = int(2.5 * 2**30)
+    free = _hip_free_bytes()
+    assert free > keep + 2**30
+    balloon = DeviceVector(A.ctx, (free - keep) // 8, 1, np.float64)
+    try:
+        h = st.run(12)
+        D, _ = st.defer_info()
+        assert D == 3
+    finally:
+        del balloon
+        krylov_amd.empty_cache()
+    monkeypatch.setenv("KRY_CG_YDEFER", "0")
+    st0 = solve()
+    h0 = st0.run(12)
+    assert st0.defer_info()[0] == 0
+    _bits_equal(np.asarray(h), np.asarray(h0))

@@ -6,9 +6,11 @@ Two general-CSR paths take the same nonzeros at the same scale:
 - with the DIA image off (KRY_SPMV_DIA=0) the paired-row SELL-128 image
   (spmv_pair_kernel): slot columns whose rows have adjacent columns;
 - under a random symmetric permutation P A P^T (problems.permuted_sym, the
-  bench's spmv_unstructured leg) the columns are scattered over all 10 M, and
-  the column-blocked image takes it: 39,366 row groups, more than one launch
-  of spmv_cbp_kernel holds, so the SpMV runs as 3 launches over group ranges.
+  bench's spmv_unstructured leg) the columns are scattered over all 10 M.
+  Since round 5 the upload renumbers it (reverse Cuthill-McKee) and the
+  rank-sorted SELL-128 image takes it; with KRY_RENUMBER=0 the
+  column-blocked image does: 39,366 row groups, more than one launch of
+  spmv_cbp_kernel holds, so the SpMV runs as 3 launches over group ranges.
 
 Each SpMV must equal SciPy's csr_matvec (the reference's `A @ x`,
 _helpers.py:44-48) bit for bit, and a CG on the permuted matrix must follow
@@ -53,9 +55,10 @@ def test_pair_image_metric_bitwise(metric, monkeypatch):
     _bitwise(op @ x, metric @ x)
 
 
-def test_permuted_metric_column_blocked_bitwise(permuted):
+def test_permuted_metric_column_blocked_bitwise(permuted, monkeypatch):
     import krylov_amd
 
+    monkeypatch.setenv("KRY_RENUMBER", "0")
     op = krylov_amd.CsrOperator(permuted)
     lay = op.layout()
     assert not lay["dia"] and lay["col_blocks"] > 0
@@ -78,3 +81,54 @@ def test_permuted_metric_cg_matches_oracle(permuted):
     assert info.numsteps == ref.numsteps == 12
     got, want = np.asarray(info.resnorms), np.asarray(ref.resnorms)
     np.testing.assert_allclose(got[:-1], want[:-1], rtol=1e-10)
+
+
+@pytest.fixture(scope="module")
+def permuted_op(permuted):
+    import krylov_amd
+
+    return krylov_amd.CsrOperator(permuted)
+
+
+def test_permuted_metric_renumbered_bitwise(permuted, permuted_op):
+    """The default upload renumbers the permuted metric (reverse
+    Cuthill-McKee) onto the rank-sorted image; y = A x in the caller's
+    numbering is SciPy's bit for bit."""
+    lay = permuted_op.layout()
+    assert lay["renumbered"] and lay["rs"] and lay["col_blocks"] == 0
+    for seed in (5, 7):
+        x = _x(permuted.shape[0], seed)
+        _bitwise(permuted_op @ x, permuted @ x)
+
+
+def test_permuted_metric_cg_to_convergence(permuted, permuted_op):
+    """CG to tol 1e-8 on the renumbered permuted metric against the reference's
+    own CG on the same (permuted) matrix (tests/golden/permuted.npz,
+    tests/golden/make_permuted.py): the same step count and success, the
+    history within 1e-10 rel or 2x the reference's own summation-order noise
+    of the metric CG (tests/golden/selfnoise.npz: the same iteration in another
+    basis), the final explicit residual within 64 eps (||b|| + ||A||_1 ||x||),
+    and x's size-independent summaries equal to the metric solution's."""
+    import os
+
+    import krylov_amd
+    from tests import gpu_helpers as H
+
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    F = np.load(os.path.join(gold, "permuted.npz"))
+    M = np.load(os.path.join(gold, "fullsize.npz"))
+    b = np.ones(permuted.shape[0])
+    x, info = krylov_amd.cg(permuted_op, b, tol=1e-8)
+    ref = F["perm_cg_resnorms"]
+    got = np.asarray(info.resnorms)
+    assert info.success and info.numsteps == int(F["perm_cg_numsteps"]) == int(M["metric_cg_numsteps"])
+    tol = np.maximum(1e-10, H.NOISE_FACTOR * H.selfnoise_envelope("metric_cg", M["metric_cg_resnorms"]))
+    dev = np.abs(got[:-1] - ref[:-1]) / np.abs(ref[:-1])
+    print(f"\npermuted metric CG (renumbered): {info.numsteps} steps, history max rel {dev.max():.2e} "
+          f"({(dev / tol).max():.2f} of the tolerance)")
+    assert np.all(dev <= tol)
+    eps = np.finfo(np.float64).eps
+    bound = 64 * eps * (np.linalg.norm(b) + float(abs(permuted).sum(axis=0).max()) * F["perm_cg_xstats"][1])
+    assert abs(got[-1] - ref[-1]) <= bound
+    xa = np.abs(x)
+    np.testing.assert_allclose([xa.sum(), np.linalg.norm(x), xa.max()], F["perm_cg_xstats"], rtol=1e-8)

@@ -1,0 +1,320 @@
+"""Bandwidth-reducing renumbering and the rank-sorted SELL-128 image (round 5).
+
+A matrix whose columns are scattered but whose graph has narrow BFS levels
+(a stencil or mesh stored in a random order: problems.permuted_sym) is
+renumbered at upload by reverse Cuthill-McKee (host_image.hpp rcm_order);
+the device images hold P A P^T with each row's entries in their stored
+order, and the solvers run in that numbering. The reference multiplies the
+caller's matrix as given (_helpers.py:44-48 -> SciPy csr_matvec), so:
+
+* every SpMV through the C-ABI (kry_spmv, the caller's numbering in and
+  out) is bitwise SciPy's;
+* the solvers' histories follow the oracle on the caller's matrix to the
+  parity tolerance (their inner products are summed in another order), and
+  every vector that comes back (xk, callbacks' iterates and residuals, the
+  Arnoldi basis) is in the caller's numbering;
+* preconditioners are built with the operator's renumbering, and an
+  operator renumbered differently is refused.
+
+The rank-sorted image (spmv_rs_kernel) serves any k = 1 matrix that the
+DIA, column-blocked and paired images do not take (unsorted rows, slot
+columns wider than a uint16 delta); it sorts each run of 16 stored entries by
+column for coalesced gathers and sums the run back in stored order.
+"""
+import numpy as np
+import pytest
+import scipy.sparse
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.dtype == b.dtype and a.shape == b.shape
+    np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def _adversarial(dtype, seed=0, n=5003, long_rows=True):
+    """Unsorted rows, duplicates, explicit zeros, empty rows, rows longer than
+    one 16-entry run (whole slices of them: the image refuses more than 1.25x
+    the SELL-64 slots), values and x over a wide exponent range."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 12, n)
+    if long_rows:
+        lens[1024:1280] = rng.integers(17, 70, 256)
+        lens[2048:2176] = rng.integers(30, 34, 128)
+    lens[100:130] = 0
+    indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    cols = rng.integers(0, n, indptr[-1]).astype(np.int32)  # unsorted, wide spans
+    dup = rng.integers(0, indptr[-1], indptr[-1] // 20)
+    cols[dup[1:]] = cols[dup[:-1]]
+    e = 30 if dtype == np.float64 else 8
+    vals = (rng.standard_normal(indptr[-1]) * 10.0 ** rng.integers(-e, e, indptr[-1])).astype(dtype)
+    vals[::13] = 0.0
+    A = scipy.sparse.csr_matrix((vals, cols, indptr), shape=(n, n))
+    x = (rng.standard_normal(n) * 10.0 ** rng.integers(-e, e, n)).astype(dtype)
+    return A, x
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_rs_image_bitwise_adversarial(dtype):
+    """Wide slot columns keep the paired image out: the rank-sorted image takes
+    the matrix, and its SpMV is SciPy's csr_matvec bit for bit (stored-order
+    sums through runs of 16, duplicates, explicit zeros, empty rows, rows of
+    up to 70 entries = 5 runs); block RHS stay on SELL-64, bitwise too."""
+    import krylov_amd
+
+    A, x = _adversarial(dtype)
+    assert not A.has_sorted_indices
+    op = krylov_amd.CsrOperator(A)
+    lay = op.layout()
+    assert lay["rs"] and not lay["pair"] and not lay["dia"] and lay["col_blocks"] == 0 and not lay["renumbered"]
+    _bits(op @ x, A @ x)
+    X = np.stack([x, x[::-1].copy()], axis=1)
+    _bits(op @ X, A @ X)
+
+
+def test_rs_image_int64_mixed_and_nan():
+    """int64 indices, a float32 matrix under float64 vectors (exact upcast),
+    and NaN in x entries no row references (never added)."""
+    import krylov_amd
+
+    A, _ = _adversarial(np.float32, seed=3)
+    A64 = scipy.sparse.csr_matrix((A.data, A.indices.astype(np.int64), A.indptr.astype(np.int64)), shape=A.shape)
+    op = krylov_amd.CsrOperator(A64)
+    assert op.layout()["rs"]
+    x = np.random.default_rng(4).standard_normal(A.shape[0])
+    used = np.zeros(A.shape[0], dtype=bool)
+    used[A.indices] = True
+    x[~used] = np.nan
+    assert (~used).any()
+    ref = A.astype(np.float64) @ x
+    assert np.isfinite(ref).all()
+    _bits(op @ x, ref)
+
+
+def test_rs_image_selection(monkeypatch):
+    """The paired image keeps the matrices whose slot columns fit a uint16
+    delta; KRY_SPMV_PAIR=0 sends them to the rank-sorted image (same bits);
+    KRY_SPMV_RS=0 leaves SELL-64."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    S = problems.stencil15_3d(20)
+    x = np.random.default_rng(1).standard_normal(S.shape[0])
+    monkeypatch.setenv("KRY_SPMV_DIA", "0")
+    assert krylov_amd.CsrOperator(S).layout()["pair"]
+    monkeypatch.setenv("KRY_SPMV_PAIR", "0")
+    op = krylov_amd.CsrOperator(S)
+    assert op.layout()["rs"]
+    _bits(op @ x, S @ x)
+    A, xa = _adversarial(np.float64, seed=5, n=3001)
+    monkeypatch.setenv("KRY_SPMV_RS", "0")
+    op0 = krylov_amd.CsrOperator(A)
+    assert not op0.layout()["rs"]
+    _bits(op0 @ xa, A @ xa)
+
+
+# ------------------------------------------------------------ renumbering
+@pytest.fixture(scope="module")
+def perm104():
+    """The 15-point stencil 104^3 (n = 1,124,864: x over 8 MB) under a random
+    symmetric permutation: scattered columns, narrow level structure."""
+    from krylov_amd import problems
+
+    return problems.permuted_sym(problems.stencil15_3d(104), 11)
+
+
+@pytest.fixture(scope="module")
+def op104(perm104):
+    import krylov_amd
+
+    return krylov_amd.CsrOperator(perm104)
+
+
+def test_renumbered_operator_layout_and_spmv(perm104, op104, monkeypatch):
+    """The permuted stencil is renumbered (rank-sorted image: its slot
+    columns span more than a uint16 delta), kry_spmv is bitwise SciPy's in the
+    caller's numbering for k = 1 and block RHS, and with KRY_RENUMBER=0 the
+    column-blocked image takes it instead (same bits)."""
+    import krylov_amd
+
+    lay = op104.layout()
+    assert lay["renumbered"] and lay["rs"] and lay["col_blocks"] == 0 and not lay["dia"]
+    assert 100 < lay["rcm_levels"] < 2000
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal(perm104.shape[0]) * np.exp2(rng.integers(-20, 20, perm104.shape[0]))
+    ref = perm104 @ x
+    _bits(op104 @ x, ref)
+    X = rng.standard_normal((perm104.shape[0], 4))
+    _bits(op104 @ X, perm104 @ X)
+    monkeypatch.setenv("KRY_RENUMBER", "0")
+    cb = krylov_amd.CsrOperator(perm104)
+    lay0 = cb.layout()
+    assert not lay0["renumbered"] and lay0["col_blocks"] > 0
+    _bits(cb @ x, ref)
+
+
+def test_renumbered_cg_gmres_minres_match_oracle(perm104, op104):
+    """CG, GMRES(30) and MINRES on the renumbered operator against the oracle
+    on the caller's matrix: histories within 1e-10 rel (early steps of a
+    well-conditioned run, no cancellation regime), iterates in the caller's
+    numbering."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+
+    b = np.random.default_rng(3).standard_normal(perm104.shape[0])
+    for name, kw in (("cg", dict(maxiter=40)), ("gmres", dict(maxiter=30)), ("minres", dict(maxiter=40))):
+        _, info = getattr(krylov_amd, name)(op104, b, tol=0.0, atol=0.0, **kw)
+        _, ref = getattr(K, name)(perm104, b, tol=0.0, atol=0.0, **kw)
+        assert info.numsteps == ref.numsteps
+        np.testing.assert_allclose(np.asarray(info.resnorms)[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+        x, xr = np.asarray(info.xk), np.asarray(ref.xk)
+        np.testing.assert_allclose(x, xr, rtol=0, atol=1e-10 * np.abs(xr).max())
+
+
+def test_renumbered_cg_converges_like_unrenumbered(perm104, op104, monkeypatch):
+    """CG to tol 1e-8 on the renumbered operator takes the same steps as on the
+    column-blocked one (no renumbering) and as the oracle; the history agrees
+    with the oracle's to the parity tolerance over the stable part (later
+    entries are in the cancellation regime, where every valid summation order
+    gives another rounding)."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+
+    b = np.ones(perm104.shape[0])
+    x1, i1 = krylov_amd.cg(op104, b, tol=1e-8)
+    monkeypatch.setenv("KRY_RENUMBER", "0")
+    x0, i0 = krylov_amd.cg(krylov_amd.CsrOperator(perm104), b, tol=1e-8)
+    _, ref = K.cg(perm104, b, tol=1e-8)
+    assert i1.success and i1.numsteps == i0.numsteps == ref.numsteps
+    h1, h0, hr = (np.asarray(i.resnorms) for i in (i1, i0, ref))
+    np.testing.assert_allclose(h1[:60], hr[:60], rtol=1e-10)
+    np.testing.assert_allclose(h0[:60], hr[:60], rtol=1e-10)
+    assert np.linalg.norm(b - perm104 @ x1) <= 1e-8 * np.linalg.norm(b) * 1.01
+
+
+def test_renumbered_preconditioners_weights_x0_callback(perm104, op104):
+    """A Jacobi M (scipy, built like the operator), a weighted inner product
+    (weights moved into the operator's numbering), a nonzero x0 and a callback
+    (iterates and residuals back in the caller's numbering), CG and GMRES
+    against the oracle."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+
+    n = perm104.shape[0]
+    Mj = scipy.sparse.diags(1.0 / perm104.diagonal()).tocsr()
+    w = np.random.default_rng(5).uniform(0.5, 2.0, n)
+    x0 = np.random.default_rng(6).standard_normal(n)
+    b = np.ones(n)
+    for name, kw in (("cg", dict(M=Mj)), ("gmres", dict(Ml=Mj)), ("gmres", dict(Mr=Mj))):
+        calls, ocalls = [], []
+        cb = lambda x, r: calls.append((np.array(x, copy=True), np.array(r, dtype=np.float64)))  # noqa: E731
+        ocb = lambda x, r: ocalls.append((np.array(x, copy=True), np.array(r, dtype=np.float64)))  # noqa: E731
+        inner = krylov_amd.WeightedInner(w)
+        _, info = getattr(krylov_amd, name)(op104, b, x0=x0, inner=inner, tol=0.0, atol=0.0, maxiter=12,
+                                             callback=cb, **kw)
+        _, ref = getattr(K, name)(perm104, b, x0=x0, inner=inner, tol=0.0, atol=0.0, maxiter=12, callback=ocb, **kw)
+        assert info.numsteps == ref.numsteps
+        np.testing.assert_allclose(np.asarray(info.resnorms)[:-1], np.asarray(ref.resnorms)[:-1], rtol=1e-10)
+        assert len(calls) == len(ocalls)
+        for (gx, gr), (ox, orr) in zip(calls, ocalls):
+            np.testing.assert_allclose(gx, ox, rtol=0, atol=1e-10 * max(np.abs(ox).max(), 1.0))
+            np.testing.assert_allclose(gr, orr, rtol=0, atol=1e-9 * max(np.abs(orr).max(), 1.0))
+
+
+def test_renumbered_preconditioner_mismatch_refused(perm104, op104, monkeypatch):
+    """A CsrOperator preconditioner that does not carry the operator's
+    renumbering is refused (ValueError), not applied in the wrong numbering."""
+    import krylov_amd
+
+    M = krylov_amd.CsrOperator(scipy.sparse.diags(1.0 / perm104.diagonal()).tocsr())
+    assert not M.renumbered
+    with pytest.raises(ValueError):
+        krylov_amd.cg(op104, np.ones(perm104.shape[0]), M=M, maxiter=3)
+    Ml = krylov_amd.CsrOperator(scipy.sparse.diags(1.0 / perm104.diagonal()).tocsr(), like=op104)
+    assert Ml.renumbered
+    _, info = krylov_amd.cg(op104, np.ones(perm104.shape[0]), M=Ml, tol=0.0, maxiter=3)
+    assert info.numsteps == 3
+
+
+def test_renumbered_arnoldi_basis_and_restart_chain(perm104, op104):
+    """The Arnoldi basis comes back in the caller's numbering (A V_m = V_{m+1}
+    H with the caller's matrix on the host), and gmres_restarted chains its
+    iterate through kry_gmres_xk_device (caller's numbering) exactly as the
+    oracle's x0 chaining."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+
+    n = perm104.shape[0]
+    v = np.random.default_rng(7).standard_normal(n)
+    V, H, _, _ = krylov_amd.arnoldi(op104, v, 8)
+    Vm = np.stack(V[:8], axis=1)
+    Vm1 = np.stack(V[:9], axis=1)
+    lhs = perm104 @ Vm
+    np.testing.assert_allclose(lhs, Vm1 @ np.asarray(H)[:9, :8], rtol=0, atol=1e-11 * np.abs(lhs).max())
+    b = np.ones(n)
+    x, infos = krylov_amd.gmres_restarted(op104, b, restart=10, tol=1e-6, max_cycles=3)
+    xo = np.zeros(n)
+    bn = np.linalg.norm(b)
+    steps = []
+    for _ in range(3):
+        _, info = K.gmres(perm104, b, x0=xo, maxiter=10, tol=1e-6 * bn / max(np.linalg.norm(b - perm104 @ xo), 1e-300))
+        steps.append(info.numsteps)
+        xo = info.xk
+        if info.success:
+            break
+    assert [i.numsteps for i in infos] == steps
+    np.testing.assert_allclose(x, xo, rtol=0, atol=1e-9 * np.abs(xo).max())
+
+
+def test_renumbered_bicgstab_matches_oracle(perm104, op104):
+    """The device-resident scalar chain (bicgstab) keeps its vectors in the
+    operator's numbering (kry_csr_permute in, out) and follows the oracle."""
+    import krylov_amd
+    from oracle import krylov_ref as K
+
+    b = np.ones(perm104.shape[0])
+    _, info = krylov_amd.bicgstab(op104, b, tol=0.0, atol=0.0, maxiter=10)
+    _, ref = K.bicgstab(perm104, b, tol=0.0, atol=0.0, maxiter=10)
+    assert info.numsteps == ref.numsteps
+    np.testing.assert_allclose(np.asarray(info.resnorms), np.asarray(ref.resnorms), rtol=1e-9)
+    x, xr = np.asarray(info.xk), np.asarray(ref.xk)
+    np.testing.assert_allclose(x, xr, rtol=0, atol=1e-9 * np.abs(xr).max())
+
+
+@pytest.mark.parametrize("case", ["grid", "stencil104", "components", "refused"])
+def test_device_rcm_equals_host_order(case, perm104):
+    """The renumbering kry_csr_create runs on the device (kry_rcm_device:
+    level-synchronous claim / counting sort by parent / per-parent sort) is
+    the host definition's order (kry_rcm_plan, pinned against a pure-Python
+    restatement in tests/test_abi.py) node for node, with the same level
+    count; refusal (a level wider than the limit) agrees too."""
+    import ctypes
+
+    from krylov_amd import _lib, problems
+    from krylov_amd.device import get_context
+
+    wlimit = 0
+    if case == "grid":
+        A = problems.permuted_sym(problems.poisson2d(300), 2)
+    elif case == "stencil104":
+        A = perm104
+    elif case == "components":
+        A = problems.permuted_sym(scipy.sparse.block_diag([problems.poisson2d(40), scipy.sparse.identity(5),
+                                                            problems.poisson2d(30)]).tocsr(), 3)
+    else:
+        A = problems.random_nonsym(300_000, per_row=6, seed=7)
+        wlimit = 5000
+    ip, ix = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+    host = _lib.rcm_plan(ip, ix, wlimit)
+    info = np.zeros(2, dtype=np.int64)
+    perm = np.zeros(A.shape[0], dtype=np.int32)
+    _lib.check(_lib.lib.kry_rcm_device(get_context().handle, A.shape[0], ix.shape[0], _lib.ptr(ip), _lib.ptr(ix),
+                                       wlimit, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _lib.ptr(perm)))
+    if case == "refused":
+        assert host is None and info[0] == 0
+        return
+    assert info[0] == 1 and host is not None
+    np.testing.assert_array_equal(perm, host[0])
+    assert info[1] == host[1]

@@ -496,11 +496,15 @@ def test_cg_preferred_chunk(monkeypatch):
     assert chunk() == 32
 
 
-@pytest.mark.parametrize("case", ["Mr", "block3", "householder"])
+@pytest.mark.parametrize("case", ["Mr", "block3", "householder", "x0", "Ml", "weighted", "callback"])
 def test_restarted_gmres_variants_match_oracle_chaining(case):
     """gmres_restarted with a right preconditioner, with a 3-column block
-    (per-column tol = 1e-8 ||b_c|| / ||b_c - A x_c||) and with Householder
-    Arnoldi, against the same x0-chaining of the oracle (restart 15)."""
+    (per-column tol = 1e-8 ||b_c|| / ||b_c - A x_c||), with Householder
+    Arnoldi, from a nonzero x0 (the first cycle's x_in), with a left
+    preconditioner (criterion 1e-8 ||Ml b|| / ||Ml (b - A x_c)||), with a
+    WeightedInner (both norms in <., .>_w, device kry_dot) and with a callback
+    (the host download of each cycle's x_in), against the same x0-chaining of
+    the oracle (restart 15)."""
     import krylov_amd
     from oracle import krylov_ref as K
     from tests import solver_cases
@@ -509,20 +513,35 @@ def test_restarted_gmres_variants_match_oracle_chaining(case):
     R = q["R"]
     kw, okw = {}, {}
     b = np.ones(R.shape[0])
+    xo = None
+    norm = lambda v: np.linalg.norm(v, axis=0)  # noqa: E731
+    calls, ocalls = [], []
     if case == "Mr":
         kw = okw = {"Mr": q["RMj"]}
     elif case == "block3":
         b = np.random.default_rng(21).standard_normal((R.shape[0], 3))
-    else:
+    elif case == "householder":
         kw = okw = {"ortho": "householder"}
+    elif case == "x0":
+        xo = np.random.default_rng(22).standard_normal(R.shape[0])
+        kw = {"x0": xo.copy()}
+    elif case == "Ml":
+        kw = okw = {"Ml": q["RMj"]}
+        norm = lambda v: np.linalg.norm(q["RMj"] @ v, axis=0)  # noqa: E731
+    elif case == "weighted":
+        w = np.random.default_rng(23).uniform(0.5, 2.0, R.shape[0])
+        kw = okw = {"inner": krylov_amd.WeightedInner(w)}
+        norm = lambda v: np.sqrt(v @ (w * v))  # noqa: E731
+    else:
+        kw = {"callback": lambda x, r: calls.append((np.array(x, copy=True), np.array(r, dtype=np.float64)))}
+        okw = {"callback": lambda x, r: ocalls.append((np.array(x, copy=True), np.array(r, dtype=np.float64)))}
     x, infos = krylov_amd.gmres_restarted(R, b, restart=15, tol=1e-8, max_cycles=12, **kw)
     # the oracle, chained the same way
-    xo = np.zeros_like(b)
-    bnorm = np.linalg.norm(b, axis=0)
+    xo = np.zeros_like(b) if xo is None else xo
+    bnorm = norm(b)
     hist, steps = [], []
     for _ in range(12):
-        _, info = K.gmres(R, b, x0=xo, maxiter=15, tol=1e-8 * bnorm / np.maximum(np.linalg.norm(b - R @ xo, axis=0), 1e-300),
-                          **okw)
+        _, info = K.gmres(R, b, x0=xo, maxiter=15, tol=1e-8 * bnorm / np.maximum(norm(b - R @ xo), 1e-300), **okw)
         hist.extend(np.asarray(info.resnorms, dtype=np.float64))
         steps.append(info.numsteps)
         xo = info.xk
@@ -533,4 +552,26 @@ def test_restarted_gmres_variants_match_oracle_chaining(case):
     ref = np.array(hist)
     assert got.shape == ref.shape
     np.testing.assert_allclose(got[:-1], ref[:-1], rtol=1e-9)
+    if case == "callback":
+        assert len(calls) == len(ocalls) > 0
+        for (gx, gr), (ox, orr) in zip(calls, ocalls):
+            # the residual b - A x_c comes from cancellation against b (= ones): an absolute bound
+            np.testing.assert_allclose(gr, orr, rtol=1e-8, atol=1e-12)
+            np.testing.assert_allclose(gx, ox, rtol=1e-8, atol=1e-10 * max(np.abs(ox).max(), 1.0))
     np.testing.assert_allclose(x, xo, rtol=1e-8, atol=1e-10 * np.abs(xo).max())
+
+
+@pytest.mark.gpu
+def test_restarted_gmres_zero_cycles_returns_x0():
+    """max_cycles = 0 runs no cycle: the iterate is x0 (zeros without one),
+    with no Info, not None."""
+    import krylov_amd
+    from tests import solver_cases
+
+    R = solver_cases.inputs()["R"]
+    b = np.ones(R.shape[0])
+    x, infos = krylov_amd.gmres_restarted(R, b, max_cycles=0)
+    assert infos == [] and x.shape == b.shape and not np.any(x)
+    x0 = np.linspace(0.0, 1.0, R.shape[0])
+    x, infos = krylov_amd.gmres_restarted(R, b, x0=x0, max_cycles=0)
+    assert infos == [] and np.array_equal(x, x0) and x is not x0

@@ -37,9 +37,13 @@ def test_plan_tests_under_sanitizer(kind):
     subprocess.run(["make", "-s", "-C", CSRC, "sanitize"], check=True)
     lib = os.path.join(CSRC, "build", "san", f"libkrylov_host_{kind}.so")
     env = dict(os.environ)
+    # libstdc++ preloaded beside the sanitizer runtime: ASan resolves the real
+    # __cxa_throw when it starts, and the plan entry points throw (rejected
+    # CSR input) from a library loaded later by ctypes
+    cxx = _runtime("libstdc++.so")
     env.update({
         "KRYLOV_LIB": lib,
-        "LD_PRELOAD": runtime,
+        "LD_PRELOAD": runtime + (" " + cxx if cxx else ""),
         "ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1",
         "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1",
         "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1",

@@ -63,6 +63,19 @@ def _worker(rank, world, port, outdir, which):
         eng = E.HostCG(P, B[:, rank * kl:(rank + 1) * kl], lay, allreduce)
         out["success"], out["k"], res = drive(eng, lay, allreduce, 1e-8, 1e-15, P.shape[0], np.float64)
         out["res"], out["x"] = np.array(res), eng.xk()
+    elif which == "cg_uneven":
+        # 8 columns over 3 ranks as krylov_amd.multi splits them: 3 device
+        # columns each, the last rank's third a zero column outside the layout
+        P = problems.poisson2d(64)
+        B = d["poisson64_B"]
+        kcs = [3, 3, 2]
+        Bl = B[:, 3 * rank:3 * rank + kcs[rank]]
+        if kcs[rank] < 3:
+            Bl = np.concatenate([Bl, np.zeros((B.shape[0], 3 - kcs[rank]))], axis=1)
+        lay = ShardLayout(3, 3, rank, world, kcs)
+        eng = E.HostCG(P, Bl, lay, allreduce)
+        out["success"], out["k"], res = drive(eng, lay, allreduce, 1e-8, 1e-15, P.shape[0], np.float64)
+        out["res"], out["x"] = np.array(res), eng.xk()[:, :kcs[rank]]
     elif which == "gmres":
         R = problems.random_nonsym(5000)
         B = d["rand5k_B3"]
@@ -104,6 +117,18 @@ def test_sharded_cg_reproduces_block_cg_bitwise(tmp_path, world):
     for o in outs:
         assert bool(o["success"]) and int(o["k"]) == int(d["cg_poisson64_blk8_numsteps"])
         np.testing.assert_array_equal(o["res"], d["cg_poisson64_blk8_resnorms"])  # global history on every rank
+    np.testing.assert_array_equal(np.concatenate([o["x"] for o in outs], axis=1), d["cg_poisson64_blk8_xk"])
+
+
+def test_sharded_cg_uneven_split_reproduces_block_cg(tmp_path):
+    """8 columns over 3 ranks (3 + 3 + 2 real, the last rank padded with a zero
+    column that the layout leaves out of the history and the stop rule, as
+    krylov_amd.multi splits a block): the block-CG fixture bit for bit."""
+    d = np.load(os.path.join(HERE, "golden", "solvers.npz"))
+    outs = _spawn(tmp_path, "cg_uneven", 3)
+    for o in outs:
+        assert bool(o["success"]) and int(o["k"]) == int(d["cg_poisson64_blk8_numsteps"])
+        np.testing.assert_array_equal(o["res"], d["cg_poisson64_blk8_resnorms"])
     np.testing.assert_array_equal(np.concatenate([o["x"] for o in outs], axis=1), d["cg_poisson64_blk8_xk"])
 
 
@@ -163,6 +188,12 @@ def test_shard_layout_padding_and_global_vectors():
     assert np.all(np.isinf(crit[[3, 7, 11]]))
     with pytest.raises(ValueError):
         ShardLayout(2, 1, 0, 2)
+    # an uneven split: rank r's first kcs[r] device columns are real
+    lu = ShardLayout(3, 4, 1, 3, kcs=[3, 3, 2])
+    np.testing.assert_array_equal(lu.real, [0, 1, 2, 4, 5, 6, 8, 9])
+    assert np.all(np.isinf(lu.criterion_full(np.zeros(8))[[3, 7, 10, 11]]))
+    with pytest.raises(ValueError):
+        ShardLayout(3, 4, 0, 3, kcs=[3, 4, 1])
 
 
 def test_file_rendezvous_threads(tmp_path):
