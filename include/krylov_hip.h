@@ -111,6 +111,11 @@ int kry_csr_create_like(kry_ctx *ctx, const kry_csr *like, int64_t n, int64_t nn
  * back (0), for callers that keep their own device vectors in the operator's
  * numbering (kry_prog_*). KRY_RENUMBER=0 disables renumbering. */
 int kry_csr_permute(kry_ctx *ctx, const kry_csr *A, const kry_vec *src, kry_vec *dst, int to_operator);
+/* Byte comparison of two operators' SELL-64 and diagonal-offset images and
+ * their sizes (kry_version() >= 104; tests: kry_csr_create builds those images
+ * on the device for int32 CSR, KRY_DEVICE_BUILD=0 on the host, and the two
+ * must be identical): out[0] = number of differing items, out[1] = bitmask. */
+int kry_csr_compare(const kry_csr *A, const kry_csr *B, int64_t *out);
 /* kry_spmv with x and y already in the operator's numbering (kry_csr_permute);
  * the same as kry_spmv for an operator that is not renumbered. */
 int kry_spmv_op(kry_ctx *ctx, kry_csr *A, kry_vec *x, kry_vec *y);

@@ -68,6 +68,7 @@ _SIGNATURES = {
     "kry_csr_destroy": [_vp],
     "kry_csr_create_like": [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _int, _int, _pvp],
     "kry_csr_permute": [_vp, _vp, _vp, _vp, _int],
+    "kry_csr_compare": [_vp, _vp, _ip64],
     "kry_spmv_op": [_vp, _vp, _vp, _vp],
     "kry_rcm_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, ctypes.c_int64, _ip64, _vp],
     "kry_rs_plan": [ctypes.c_int64, ctypes.c_int64, _vp, _vp, _int, _ip64, _vp, _vp],

@@ -498,7 +498,20 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::v
   hipStream_t st = A->ctx->stream;
   const int64_t n = A->n, nnz = A->nnz;
   UploadTrace tr;
-  check_csr(n, nnz, ip, ix);
+  // the device build (int32 CSR; KRY_DEVICE_BUILD=0: the host builders):
+  // 1 = SELL-64 and DIA built on the device, nothing else to do (stencils:
+  // the metric); 2 / 3 = SELL-64 built, no DIA / DIA left to the host
+  // builder; 0 = nothing built (scattered, the renumbering path below)
+  int dres = 0;
+  if constexpr (sizeof(I) == 4) {
+    if (!like_perm && n > 0 && nnz > 0 && !env_off("KRY_DEVICE_BUILD")) {
+      DeviceCsrFlags df;
+      dres = device_image_build(A, ip, ix, dv, !env_off("KRY_RENUMBER"), &df);
+      tr.mark("device build (H2D + SELL-64 + DIA)");
+      if (dres == 1) return;
+    }
+  }
+  if (dres == 0) check_csr(n, nnz, ip, ix);  // validated on the device otherwise
   std::vector<int32_t> own;
   const std::vector<int32_t> *perm = like_perm;
   if (perm) {
@@ -550,44 +563,46 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::v
     KRY_HIP(hipStreamSynchronize(st));
     tr.mark("renumbered CSR + perm H2D");
   }
-  std::vector<int64_t> sptr;
-  std::vector<int32_t> width;
-  sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
-  A->max_width = 0;
-  for (int32_t w : width) A->max_width = std::max(A->max_width, w);
-  hvec<I> sidx;
-  hvec<MV> sval;
-  sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
-  tr.mark("SELL-64 plan + fill");
-  A->sptr = dev_alloc(sptr.size() * 8);
-  A->swidth = dev_alloc(width.size() * 4 + 4);
-  // compact image unless disabled (KRY_SELL_COMPACT=0) or impossible
-  const char *cenv = getenv("KRY_SELL_COMPACT");
-  hvec<uint16_t> sdelta;
-  std::vector<int32_t> scbase;
-  A->compact = sizeof(I) == 4 && !(cenv && atoi(cenv) == 0) && A->nslots > 0 &&
-               compact_fill(sptr, width, sidx, sdelta, scbase);
-  if (A->compact) {
-    A->sdelta = dev_alloc(sdelta.size() * 2);
-    A->scbase = dev_alloc(scbase.size() * 4);
-    KRY_HIP(hipMemcpyAsync(A->sdelta, sdelta.data(), sdelta.size() * 2, hipMemcpyHostToDevice, st));
-    KRY_HIP(hipMemcpyAsync(A->scbase, scbase.data(), scbase.size() * 4, hipMemcpyHostToDevice, st));
-  } else {
-    A->sidx = dev_alloc(sidx.size() * sizeof(I));
-    KRY_HIP(hipMemcpyAsync(A->sidx, sidx.data(), sidx.size() * sizeof(I), hipMemcpyHostToDevice, st));
+  if (dres < 2) {  // SELL-64 on the host (the device build made it otherwise)
+    std::vector<int64_t> sptr;
+    std::vector<int32_t> width;
+    sell_plan(n, ip, &sptr, &width, &A->nslices, &A->nslots, &A->nirregular);
+    A->max_width = 0;
+    for (int32_t w : width) A->max_width = std::max(A->max_width, w);
+    hvec<I> sidx;
+    hvec<MV> sval;
+    sell_fill(n, ip, ix, dv, sptr, width, sidx, sval);
+    tr.mark("SELL-64 plan + fill");
+    A->sptr = dev_alloc(sptr.size() * 8);
+    A->swidth = dev_alloc(width.size() * 4 + 4);
+    // compact image unless disabled (KRY_SELL_COMPACT=0) or impossible
+    const char *cenv = getenv("KRY_SELL_COMPACT");
+    hvec<uint16_t> sdelta;
+    std::vector<int32_t> scbase;
+    A->compact = sizeof(I) == 4 && !(cenv && atoi(cenv) == 0) && A->nslots > 0 &&
+                 compact_fill(sptr, width, sidx, sdelta, scbase);
+    if (A->compact) {
+      A->sdelta = dev_alloc(sdelta.size() * 2);
+      A->scbase = dev_alloc(scbase.size() * 4);
+      KRY_HIP(hipMemcpyAsync(A->sdelta, sdelta.data(), sdelta.size() * 2, hipMemcpyHostToDevice, st));
+      KRY_HIP(hipMemcpyAsync(A->scbase, scbase.data(), scbase.size() * 4, hipMemcpyHostToDevice, st));
+    } else {
+      A->sidx = dev_alloc(sidx.size() * sizeof(I));
+      KRY_HIP(hipMemcpyAsync(A->sidx, sidx.data(), sidx.size() * sizeof(I), hipMemcpyHostToDevice, st));
+    }
+    A->sval = dev_alloc(sval.size() * sizeof(MV));
+    KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
+    if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
+    KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
+    KRY_HIP(hipStreamSynchronize(st));
+    release_later(sidx);
+    release_later(sval);
+    release_later(sdelta);
+    tr.mark("compact image + H2D");
   }
-  A->sval = dev_alloc(sval.size() * sizeof(MV));
-  KRY_HIP(hipMemcpyAsync(A->sptr, sptr.data(), sptr.size() * 8, hipMemcpyHostToDevice, st));
-  if (!width.empty()) KRY_HIP(hipMemcpyAsync(A->swidth, width.data(), width.size() * 4, hipMemcpyHostToDevice, st));
-  KRY_HIP(hipMemcpyAsync(A->sval, sval.data(), sval.size() * sizeof(MV), hipMemcpyHostToDevice, st));
-  KRY_HIP(hipStreamSynchronize(st));
-  release_later(sidx);
-  release_later(sval);
-  release_later(sdelta);
-  tr.mark("compact image + H2D");
   // diagonal-offset image for structured single-RHS SpMVs (KRY_SPMV_DIA=0 disables)
   const char *denv = getenv("KRY_SPMV_DIA");
-  if (!(denv && atoi(denv) == 0)) {
+  if (dres != 2 && !(denv && atoi(denv) == 0)) {
     DiaHost<MV> dh;
     if (dia_build(n, ip, ix, dv, A->nslots, dh)) {
       A->dia = true;
@@ -681,7 +696,7 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::v
     }
     tr.mark("rank-sorted image + H2D");
   }
-  if (A->nirregular > 0) {
+  if (A->nirregular > 0 && !A->indptr) {
     A->indptr = dev_alloc((n + 1) * sizeof(I));
     A->indices = dev_alloc((nnz + 1) * sizeof(I));
     A->data = dev_alloc((nnz + 1) * sizeof(MV));
@@ -761,6 +776,64 @@ int kry_csr_create_like(kry_ctx *ctx, const kry_csr *like, int64_t n, int64_t nn
   KRY_API_BEGIN
   KRY_REQUIRE(out && like, KRY_EINVAL, "null argument");
   *out = csr_create(ctx, n, nnz, indptr, indices, data, dtype, itype, like);
+  KRY_API_END
+}
+
+// Byte comparison of two operators' SELL-64 and DIA images (tests: the
+// device-built image against the host builders'): out[0] = the number of
+// differing fields / buffers, out[1] = a bitmask of which (bit i = the i-th
+// item of the list below).
+int kry_csr_compare(const kry_csr *A, const kry_csr *B, int64_t *out) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(A && B && out, KRY_EINVAL, "null argument");
+  KRY_HIP(hipSetDevice(A->ctx->device));
+  KRY_HIP(hipDeviceSynchronize());
+  int64_t nd = 0, mask = 0;
+  int item = 0;
+  auto note = [&](bool differ) {
+    if (differ) {
+      ++nd;
+      mask |= int64_t(1) << item;
+    }
+    ++item;
+  };
+  const int64_t scal[][2] = {{A->nslices, B->nslices}, {A->nslots, B->nslots}, {A->nirregular, B->nirregular},
+                             {A->max_width, B->max_width}, {A->compact, B->compact}, {A->dia, B->dia},
+                             {A->dia_nslices, B->dia_nslices}, {A->dia_nslots, B->dia_nslots},
+                             {A->dia_max_width, B->dia_max_width}};
+  for (auto &p : scal) note(p[0] != p[1]);
+  auto buf = [&](const void *a, const void *b, size_t bytes) {
+    if (!a || !b) {
+      note(a != b);
+      return;
+    }
+    std::vector<char> ha(bytes), hb(bytes);
+    if (bytes) {
+      KRY_HIP(hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost));
+      KRY_HIP(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
+    }
+    note(bytes && std::memcmp(ha.data(), hb.data(), bytes) != 0);
+  };
+  if (nd == 0) {
+    const size_t ds = dsize(A->dtype), is = isize(A->itype);
+    buf(A->sptr, B->sptr, (A->nslices + 1) * 8);
+    buf(A->swidth, B->swidth, A->nslices * 4);
+    buf(A->sval, B->sval, (A->nslots + 256) * ds);
+    buf(A->sidx, B->sidx, A->compact ? 0 : (A->nslots + 256) * is);
+    buf(A->sdelta, B->sdelta, A->compact ? (A->nslots + 256) * 2 : 0);
+    buf(A->scbase, B->scbase, A->compact ? (A->nslots / kSlice + 16) * 4 : 0);
+    const int64_t dc = A->dia_nslots / kDiaSlice + kDiaPad;
+    buf(A->dia_sptr, B->dia_sptr, A->dia ? (A->dia_nslices + 1) * 8 : 0);
+    buf(A->dia_width, B->dia_width, A->dia ? A->dia_nslices * 4 : 0);
+    buf(A->dia_off, B->dia_off, A->dia ? dc * 4 : 0);
+    buf(A->dia_mask, B->dia_mask, A->dia ? dc * 16 : 0);
+    buf(A->dia_val, B->dia_val, A->dia ? (A->dia_nslots + 256) * ds : 0);
+    buf(A->indptr, B->indptr, A->nirregular ? (A->n + 1) * is : 0);
+    buf(A->indices, B->indices, A->nirregular ? A->nnz * is : 0);
+    buf(A->data, B->data, A->nirregular ? A->nnz * ds : 0);
+  }
+  out[0] = nd;
+  out[1] = mask;
   KRY_API_END
 }
 

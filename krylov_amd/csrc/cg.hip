@@ -1578,6 +1578,10 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   } else if (persistent) {
     cgp_commit(s, done);
   } else if (s->comm && c.status == KRY_ECOMM) {
+    // the healthy rank's state has moved past the recorded history (the
+    // step's update kernels ran before the global check stopped it): the
+    // solver refuses further runs until kry_*_start
+    s->started = false;
     throw Error{KRY_ECOMM, "CG: another rank's in-launch exchange failed at step " + std::to_string(done) +
                                " of this run call; every rank stopped before it"};
   } else if (upd && c.status == KRY_EDEVICE && s->comm) {
@@ -1588,6 +1592,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     // (post_fault), which all stopped before it
     s->upd_nv = 0;
     ++s->upd_fallbacks;
+    s->started = false;  // refuse further runs until kry_*_start (the state is past the history)
     throw Error{KRY_EDEVICE, "CG: the one-launch update's exchange timed out at step " + std::to_string(done) +
                                  " (a block was not resident); every rank of the communicator stopped before it"};
   } else if (upd && c.status == KRY_EDEVICE) {

@@ -1796,15 +1796,21 @@ int kry_gmres_run(kry_gmres *s, int32_t max_steps, int32_t *steps_done, double *
   };
   Ctrl c;
   int done = run_chunk(max_steps, resnorms, &c);
-  if (s->comm && c.status == KRY_ECOMM)
+  if (s->comm && c.status == KRY_ECOMM) {
+    // the healthy rank's state has moved past the recorded history (the
+    // step's update kernels ran before the global check stopped it): the
+    // solver refuses further runs until kry_*_start
+    s->started = false;
     throw Error{KRY_ECOMM, "GMRES: another rank's in-launch exchange failed at step " + std::to_string(done) +
                                " of this run call; every rank stopped before it"};
+  }
   if (c.status == KRY_EDEVICE && s->mgsp_E > 0 && s->comm) {
     // one allreduce per step on every rank: no rank may rerun part of a chunk
     // alone (see kry_cg_run); the step's allreduce carried the fault to every
     // rank (post_fault), which all stopped before it
     s->mgsp_E = 0;
     ++s->mgsp_fallbacks;
+    s->started = false;  // refuse further runs until kry_*_start (the state is past the history)
     throw Error{KRY_EDEVICE, "GMRES: the persistent MGS exchange timed out at step " + std::to_string(done) +
                                  " (a block was not resident); every rank of the communicator stopped before it"};
   }

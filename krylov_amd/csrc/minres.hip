@@ -909,15 +909,21 @@ int kry_minres_run(kry_minres *s, int32_t max_steps, int32_t *steps_done, double
   Ctrl c;
   int done = run_steps(max_steps, resnorms, &c);
   const bool upd = s->upd_used;
-  if (s->comm && c.status == KRY_ECOMM)
+  if (s->comm && c.status == KRY_ECOMM) {
+    // the healthy rank's state has moved past the recorded history (the
+    // step's update kernels ran before the global check stopped it): the
+    // solver refuses further runs until kry_*_start
+    s->started = false;
     throw Error{KRY_ECOMM, "MINRES: another rank's in-launch exchange failed at step " + std::to_string(done) +
                                " of this run call; every rank stopped before it"};
+  }
   if (upd && c.status == KRY_EDEVICE && s->comm) {
     // one allreduce per step on every rank: no rank may rerun part of a chunk
     // alone (see kry_cg_run); the step's allreduce carried the fault to every
     // rank (post_fault), which all stopped before it
     s->upd_nv = 0;
     ++s->upd_fallbacks;
+    s->started = false;  // refuse further runs until kry_*_start (the state is past the history)
     throw Error{KRY_EDEVICE, "MINRES: the one-launch step tail's exchange timed out at step " + std::to_string(done) +
                                  " (a block was not resident); every rank of the communicator stopped before it"};
   }

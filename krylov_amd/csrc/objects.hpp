@@ -153,6 +153,18 @@ void load_in(const kry_csr *A, const void *src, void *dst, int k, size_t esize, 
 // The get form: solver storage (operator numbering) to a host buffer in the
 // caller's numbering (through a temporary device block when renumbered).
 void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st);
+// Device-side image build (device_build.hip; int32 CSR): uploads the CSR
+// arrays, validates them, builds SELL-64 (+ compact) and the DIA image.
+// Returns 0: nothing built (scattered and renumber_candidates: the
+// renumbering path takes over); 1: SELL-64 and DIA built; 2: SELL-64 built,
+// no DIA (refused as dia_build refuses); 3: SELL-64 built, the DIA decision
+// left to the host builder (a slice beyond the kernel's LDS capacity).
+struct DeviceCsrFlags {
+  bool strictly_sorted = false, sorted = false, scattered = false;
+};
+template <typename MV>
+int device_image_build(kry_csr *A, const int32_t *ip, const int32_t *ix, const MV *dv, bool renumber_candidates,
+                       DeviceCsrFlags *out);
 // Reverse Cuthill-McKee on the device over device CSR arrays (renumber.hip):
 // 1 built, 0 refused (a level wider than wlimit), -1 gave up (too many
 // components: use the host order, host_image.hpp rcm_order, the same order).

@@ -49,6 +49,11 @@ CASES = {
     "cg_w20_weighted": ("shifted_lap3d_weighted(20)", 1e-8, "weighted"),
     # round 4: the positive definite weighted case (make_golden.make_weighted_spd)
     "cg_w20spd_weighted": ("shifted_lap3d_weighted(20, sigma=0.0)", 1e-8, "weighted"),
+    # round 5: the metric matrix under a random symmetric permutation (the
+    # renumbered path's case, tests/golden/permuted.npz): its rows sum in a
+    # scattered order, and its history is more sensitive to the inner
+    # product's order than the stencil-ordered metric's
+    "perm_cg": ("permuted_sym(problems.stencil15_3d(216), 0)", 1e-8, "default"),
 }
 SMALL_CASES = ("cg_w20_weighted", "cg_w20spd_weighted")
 VARIANTS = {
@@ -119,12 +124,18 @@ def run_one(case, variant, out_path):
 
 
 def main():
-    only = sys.argv[1:]
+    """Usage: make_selfnoise.py [--jobs J] [case ...]: the missing variants of
+    the named cases (all by default), J processes at a time."""
+    args = sys.argv[1:]
+    jobs = 1
+    if args[:1] == ["--jobs"]:
+        jobs, args = int(args[1]), args[2:]
+    only = args
     out = {}
     path = os.path.join(HERE, "selfnoise.npz")
     if os.path.exists(path):
         out.update(dict(np.load(path)))
-    tmp = os.path.join(HERE, "_selfnoise_tmp.npy")
+    todo = []
     for case in CASES:
         if only and case not in only:
             continue
@@ -133,11 +144,20 @@ def main():
                 continue
             if variant in SMALL_ONLY and case not in SMALL_CASES:
                 continue
+            todo.append((case, variant, env))
+    for i in range(0, len(todo), jobs):
+        procs = []
+        for case, variant, env in todo[i:i + jobs]:
+            tmp = os.path.join(HERE, f"_selfnoise_tmp_{case}_{variant}.npy")
             e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", **env)
-            subprocess.check_call([sys.executable, __file__, "--one", case, variant, tmp], env=e)
+            procs.append((case, variant, tmp, subprocess.Popen([sys.executable, __file__, "--one", case, variant, tmp],
+                                                               env=e)))
+        for case, variant, tmp, pr in procs:
+            if pr.wait() != 0:
+                raise RuntimeError(f"{case} {variant} failed")
             out[f"{case}_{variant}"] = np.load(tmp)
             os.remove(tmp)
-            np.savez_compressed(path, **out)
+        np.savez_compressed(path, **out)
     print("written", path)
 
 

@@ -40,11 +40,15 @@ def test_devices_single_gpu_equals_block_solve(method):
         _bits(x2, x1)
 
 
-def test_devices_vector_rhs_and_x0():
-    """A 1-D b keeps scalar history entries; x0 is split like b."""
+def test_devices_vector_rhs_and_x0(monkeypatch):
+    """A 1-D b keeps scalar history entries; x0 is split like b. (One column
+    on one device would take the persistent small-n CG loop, which sums its
+    inner products in another order and cannot carry the per-step allreduce:
+    KRY_CG_PERSIST=0 puts the plain solve on the same launch-per-pass path.)"""
     import krylov_amd
     from krylov_amd import problems
 
+    monkeypatch.setenv("KRY_CG_PERSIST", "0")
     P = problems.poisson2d(64)
     b = np.ones(P.shape[0])
     x0 = np.linspace(-1.0, 1.0, P.shape[0])
