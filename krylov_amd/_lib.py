@@ -387,7 +387,7 @@ def _shutdown():
     lib.kry_mem_release()
     for f in reversed(ctxs):
         _release(f)
-    maps = os.environ.get("KRY_EXIT_MAPS")  # diagnostics: the address map at exit (tools/gpu_exit_bisect.sh)
+    maps = os.environ.get("KRY_EXIT_MAPS")  # diagnostics: the address map at exit (archive:gpu_exit_bisect.sh)
     if maps:
         with open("/proc/self/maps") as src, open(maps, "w") as dst:
             dst.write(src.read())

@@ -676,7 +676,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(const int64_t *__restr
 // otherwise the second value is an 8-B load behind one wave-level branch per
 // round, skipped by waves whose lanes all paired. Against SELL-64 that is
 // half the memory instructions per nonzero with the same 10 bytes
-// (tools/sellp_bench: 0.297 against 0.352 ms on the metric matrix). Each row
+// (archive:sellp_bench: 0.297 against 0.352 ms on the metric matrix). Each row
 // is summed from 0 in stored order, a hole or padding slot dropped by a
 // select, never added: bitwise csr_matvec, for unsorted rows, duplicates
 // and explicit zeros too. One slice per wave (grid over the slices).
@@ -906,7 +906,7 @@ __global__ __launch_bounds__(kBlock) void spmv_rs_kernel(const int64_t *__restri
 // grid covers the slices, kMaxGridBlk blocks at most): the waves resident on
 // an XCD then work on neighbouring slices together, so the x rows a slot
 // column at offset +-o reads again were fetched by a neighbouring wave
-// moments before and are L2 hits (tools/dia_blk_bench: x fetched ~1x from
+// moments before and are L2 hits (archive:dia_blk_bench: x fetched ~1x from
 // HBM, against ~3x with 2.4 contiguous slices per wave at 8192 blocks).
 // The epilogue is the lane-group kernel's row<CPL>.
 template <typename V, typename MV, int CPL, int NG, class Src, class Epi>
@@ -1164,7 +1164,7 @@ __device__ __forceinline__ void lartg(T f, T g, T &c, T &s, T &r) {
 // pass's gathers read whole contiguous rows (k * 8 bytes each). Same slot
 // order, same per-(row, column) sequential sum, so the result is bitwise the
 // lane-per-row kernel's (and csr_matvecs'). CPL = 4 measured 0.53 ms against
-// 0.80 ms for one column per lane on cfg4 (k = 8, tools/spmv_bench block).
+// 0.80 ms for one column per lane on cfg4 (k = 8, archive:spmv_bench block).
 template <typename V, typename MV, typename I, int CPL, int UNR, bool D16, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_sell_lg_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
@@ -1466,7 +1466,7 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
   KRY_REQUIRE(k >= 1 && k <= kMaxCols && is_pow2(k), KRY_EUNSUPPORTED, "k must be a power of two <= 256");
   int grid;
   if (k == 1 && A->sp) {
-    // one slice per wave (tools/sellp_bench: 0.32 ms against 0.36 ms at 8192
+    // one slice per wave (archive:sellp_bench: 0.32 ms against 0.36 ms at 8192
     // blocks of 2.4 slices per wave on the metric matrix); partial buffers
     // hold kMaxGridBlk rows for k = 1
     grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGridBlk, (A->sp_nslices + 3) / 4));

@@ -267,7 +267,7 @@ struct BufSeg {
   // __builtin_amdgcn_raw_buffer_store_b128 hipcc (ROCm 7.2, gfx950) may let a
   // VALU overwrite the store's data VGPRs in the very next instruction, before
   // the 16-byte store has read them (seen as corrupted lanes 12-15 of every 16
-  // in one element: tools/cgu_debug.py); for global stores it keeps the wait
+  // in one element: archive:cgu_debug.py); for global stores it keeps the wait
   // states.
   // The element offset is built from an opaque zero (a volatile s_mov):
   // otherwise LLVM hoists the NV per-granule offsets of an epilogue that

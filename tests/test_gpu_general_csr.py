@@ -106,9 +106,12 @@ def test_permuted_metric_cg_to_convergence(permuted, permuted_op):
     own CG on the same (permuted) matrix (tests/golden/permuted.npz,
     tests/golden/make_permuted.py): the same step count and success, the
     history within 1e-10 rel or 2x the reference's own summation-order noise
-    of the metric CG (tests/golden/selfnoise.npz: the same iteration in another
-    basis), the final explicit residual within 64 eps (||b|| + ||A||_1 ||x||),
-    and x's size-independent summaries equal to the metric solution's."""
+    on this matrix (tests/golden/selfnoise.npz "perm_cg": its CG under 1 / 2 /
+    4 / N OpenBLAS threads, pairwise, extended and fsum inner products; the
+    permuted-order SpMV makes this CG far more order-sensitive than the
+    metric's: 2.1e-4 at the last steps against 3e-9), the final explicit
+    residual within 64 eps (||b|| + ||A||_1 ||x||), and x's size-independent
+    summaries equal to the metric solution's."""
     import os
 
     import krylov_amd
@@ -122,7 +125,7 @@ def test_permuted_metric_cg_to_convergence(permuted, permuted_op):
     ref = F["perm_cg_resnorms"]
     got = np.asarray(info.resnorms)
     assert info.success and info.numsteps == int(F["perm_cg_numsteps"]) == int(M["metric_cg_numsteps"])
-    tol = np.maximum(1e-10, H.NOISE_FACTOR * H.selfnoise_envelope("metric_cg", M["metric_cg_resnorms"]))
+    tol = np.maximum(1e-10, H.NOISE_FACTOR * H.selfnoise_envelope("perm_cg", ref))
     dev = np.abs(got[:-1] - ref[:-1]) / np.abs(ref[:-1])
     print(f"\npermuted metric CG (renumbered): {info.numsteps} steps, history max rel {dev.max():.2e} "
           f"({(dev / tol).max():.2f} of the tolerance)")

@@ -1,7 +1,8 @@
 """End-to-end (host-array boundary) timing of the user-facing solvers on the
 metric matrix: krylov_amd.cg / gmres called with numpy b, returning numpy x,
 against the device-resident iteration rate the bench reports. Splits out the
-per-call pieces: Problem (b upload), the solve, the x download.
+per-call pieces: Problem (b upload), the solve, the x download, and (round 5)
+a cProfile of one call by own time (ctypes calls count in their caller).
 
     python3 tools/e2e_time.py [steps]
 """
@@ -89,5 +90,47 @@ def main(steps=200):
               ", ".join(f"{k} {1e3 * v:.1f}" for k, v in sorted(acc.items(), key=lambda kv: -kv[1])), flush=True)
 
 
+def profile_calls(steps_list=(20, 200)):
+    import cProfile
+    import pstats
+
+    import krylov_amd
+    from krylov_amd import problems
+
+    M = problems.stencil15_3d(216)
+    A = krylov_amd.CsrOperator(M)
+    b = np.ones(M.shape[0])
+    for steps in steps_list:
+        for _ in range(2):
+            krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
+            ts.append(time.perf_counter() - t0)
+        # the device rate of the same chunks without the host boundary
+        prob = krylov_amd._helpers.Problem(A, b, None, None)
+        st = sys.modules["krylov_amd.cg"]._CGState(prob)
+        st.start()
+        st.set_criterion(np.zeros(1))
+        A.ctx.synchronize()
+        t0 = time.perf_counter()
+        k = 0
+        while k < steps:
+            k += len(st.run(min(st.preferred_chunk(), steps - k)))
+        dev = time.perf_counter() - t0
+        del st, prob
+        print(f"cg maxiter={steps}: calls {', '.join(f'{1e3 * t:.1f}' for t in ts)} ms; chunked device loop "
+              f"{1e3 * dev:.1f} ms -> fixed {1e3 * (float(np.median(ts)) - dev):.1f} ms", flush=True)
+        pr = cProfile.Profile()
+        pr.enable()
+        krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stdout).sort_stats("tottime").print_stats(14)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "profile":
+        profile_calls()
+        sys.exit(0)
     main(int(sys.argv[1]) if len(sys.argv) > 1 else 200)

@@ -1,14 +1,13 @@
 #!/bin/bash
-# Counter passes over tools/dia_blk_bench (DIA_BLK_LDS=1: the library's block
-# DIA SpMV, the slot-major probe and the LDS-window variants, cfg4's Poisson
-# 3163^2 at k = 8), one small group per rocprofv3 run under its own limit;
-# stop at the first failing pass. tools/pmc_dia_blk_summary.py -> per-kernel
-# means per dispatch.
+# Counter passes over tools/dia_blk_probe (the library's block DIA SpMV, the
+# slot-major probe with and without shuffled values and x loads, the copy
+# floor; cfg4's Poisson 3163^2 at k = 8), one small group per rocprofv3 run
+# under its own limit; stop at the first failing pass.
+# tools/pmc_dia_blk_summary.py -> per-kernel means per dispatch.
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_dia_blk
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-export DIA_BLK_LDS=1
-BIN=$GRAFT_REPO_ROOT/tools/dia_blk_bench
+BIN=$GRAFT_REPO_ROOT/tools/dia_blk_probe
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
            "SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU" \

@@ -1,6 +1,5 @@
-"""Summarise tools/pmc_dia_blk.sh: per kernel of tools/dia_blk_bench (the
-library's block DIA SpMV, the slot-major probe, the LDS-window variants and
-the copy floor), the mean of every counter per dispatch, and derived rates:
+"""Summarise tools/pmc_dia_blk.sh: per kernel of tools/dia_blk_probe (the
+library's block DIA SpMV, the slot-major probe variants and the copy floor), the mean of every counter per dispatch, and derived rates:
 VMEM instructions per slice, TA busy share, L2 hit rate, HBM bytes (FETCH_SIZE
 x 2, the gfx950 correction for 16-B streaming reads, MI355X_MICROARCH.md
 "HBM"; WRITE_SIZE as is) against the kernel's compulsory bytes."""
@@ -24,7 +23,7 @@ def main(out):
                 acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {}
     for kern, cs in acc.items():
-        short = kern.split("(")[0][:90]
+        short = kern.split("(")[0][:90] if "slot_major" not in kern else kern[:kern.index(">") + 1]
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         d = {"kernel": kern[:200], "dispatches": max(len(v) for v in cs.values()), "counters": m}
         if "SQ_INSTS_VMEM_RD" in m and "SQ_WAVES" in m:

@@ -1,7 +1,7 @@
 """Scan hipcc's gfx950 assembly for a 16/12-byte vector store whose data
 VGPRs the very next VALU instruction overwrites (no wait state between).
 hipcc 7.2 emitted that after __builtin_amdgcn_raw_buffer_store_b128 (the
-store then reads some lanes' new values: tools/cgu_debug.py); BufSeg stores
+store then reads some lanes' new values: archive:cgu_debug.py); BufSeg stores
 therefore use global stores. Usage: python tools/store_hazard_scan.py [src.hip ...]
 (default: every krylov_amd/csrc/*.hip); prints hits per kernel, exit 1 if any."""
 import glob
