@@ -79,7 +79,8 @@ def image_bytes_k1(layout, n, nnz, vectors=2, vb=8):
                 f"pair_slots*(8+2) + pair_slots/128*4 + slices*12 + {vt}")
     if layout.get("rs"):
         rs = layout["rs_slots"]
-        kname = "spmv_rs_kernel" + (" (renumbered)" if layout.get("renumbered") else "")
+        kname = ("spmv_rs_kernel" if os.environ.get("KRY_SPMV_RS1") == "0" else "spmv_rs1_kernel") + (
+            " (renumbered)" if layout.get("renumbered") else "")
         return (kname, rs * (8 + 4) + (n + 127) // 128 * 12 + v,
                 f"rs_slots*(8+4) (values + column/rank words) + slices*12 + {vt}")
     slots, slices = layout["slots"], layout["slices"]
@@ -483,6 +484,9 @@ def run_end_to_end(A_host, steps):
     PCIe-inclusive rate DESIGN.md (d) quotes. Median of 3 after a warm-up."""
     import krylov_amd
 
+    from krylov_amd import _helpers
+    from krylov_amd.cg import _CGState
+
     A = krylov_amd.CsrOperator(A_host)
     b = np.ones(A.n)
     out = {}
@@ -491,17 +495,39 @@ def run_end_to_end(A_host, steps):
         ("gmres30", lambda: krylov_amd.gmres(A, b, tol=0.0, atol=0.0, maxiter=30), 30),
     ):
         run()
-        ts = []
+        ts, keep = [], []
         for _ in range(3):
             t0 = time.perf_counter()
-            _, info = run()
+            r = run()
             ts.append(time.perf_counter() - t0)
-            assert info.numsteps == iters
+            assert r[1].numsteps == iters
+            keep.append(r)  # the caller's x outlives the call: its release is not the solver's cost
+        t0 = time.perf_counter()
+        del keep, r
+        out[f"{label}_result_free_ms"] = 1e3 * (time.perf_counter() - t0) / 3
         t = float(np.median(ts))
         out[f"{label}_it_per_s"] = iters / t
         out[f"{label}_call_ms"] = 1e3 * t
+    # the same CG chunks without the host-array boundary (b already on the
+    # device, no x download): the call's fixed cost is the difference
+    prob = _helpers.Problem(A, b, None, None)
+    st = _CGState(prob)
+    dev = []
+    for _ in range(3):
+        st.start()
+        st.set_criterion(np.zeros(1))
+        A.ctx.synchronize()
+        t0 = time.perf_counter()
+        k = 0
+        while k < steps:
+            k += len(st.run(min(st.preferred_chunk(), steps - k)))
+        dev.append(time.perf_counter() - t0)
+    del st, prob
+    out["cg_device_loop_ms"] = 1e3 * float(np.median(dev))
+    out["cg_fixed_ms"] = out["cg_call_ms"] - out["cg_device_loop_ms"]
     out["includes"] = ("b upload (H2D), solver state setup, per-chunk host syncs, x download (D2H); the operator "
-                       "is uploaded once before (CsrOperator)")
+                       "is uploaded once before (CsrOperator); cg_fixed_ms = the call minus the same chunked "
+                       "device loop; the caller's x is released after the timing (result_free_ms)")
     # the operator upload itself (kry_csr_create: one H2D of the CSR arrays,
     # the SELL-64 and DIA images built on the device), median of 3
     del A

@@ -893,6 +893,87 @@ __global__ __launch_bounds__(kBlock) void spmv_rs_kernel(const int64_t *__restri
   }
 }
 
+// The same rank-sorted image, one row per lane (the default since round 5;
+// KRY_SPMV_RS1=0 selects the paired kernel above): a wave takes half a slice
+// (64 rows: row r of the half is image slot r, so the column-word, value and
+// x loads of a slot column stay contiguous 4-, 8- and 8-byte runs), and the
+// run's products need 16 x 64 doubles of LDS per wave instead of 2 x 16 x 64:
+// five blocks of four waves per CU instead of two (the paired kernel's
+// occupancy is set by its 66 KB of LDS per block). UNR = 16 puts a whole
+// run's loads in flight. Same products, same stored-order sums: bitwise the
+// paired kernel and csr_matvec. Renumbered permuted metric: 0.561 -> 0.499
+// ms per SpMV at four blocks per CU (tools/rs_ab.py,
+// profiles/r05_rs_ab.txt).
+template <typename V, typename MV, int UNR, class Src, class Epi>
+__global__ __launch_bounds__(kBlock) void spmv_rs1_kernel(const int64_t *__restrict__ sptr,
+                                                          const int *__restrict__ swidth,
+                                                          const uint32_t *__restrict__ colrank,
+                                                          const MV *__restrict__ val, int64_t nslices, int64_t n,
+                                                          Src src, Epi epi, double *__restrict__ part,
+                                                          const Ctrl *ctrl, int step) {
+  static_assert(kRsRun % UNR == 0, "a run is a whole number of unrolled rounds");
+  if (halted(ctrl, step)) return;
+  // 32 KB (fp64): five blocks per CU; the block reduction reuses it
+  __shared__ __attribute__((aligned(16))) V prod[kBlock / 64][kRsRun][64];
+  static_assert(sizeof(prod) >= kBlock * sizeof(double), "the reduction fits the product buffer");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const auto bs = src.template bind<1>(0);
+  V(*pw)[64] = prod[wid];
+  double dacc = 0.0;
+  for (int64_t hs = (int64_t)g * 4 + wid; hs < 2 * nslices; hs += W) {
+    const int64_t s = hs >> 1;
+    const int q = (int)(hs & 1) * 64 + lane;  // the row's slot within the slice
+    const int w = swidth[s];
+    const int64_t base = sptr[s];
+    const int64_t row = s * kPairSlice + q;
+    const uint32_t *cr = colrank + base + q;
+    const MV *cv = val + base + q;
+    V acc = V(0);
+    for (int r0 = 0; r0 < w; r0 += kRsRun) {
+      const int re = w < r0 + kRsRun ? w : r0 + kRsRun;
+      int nv = 0;
+      for (int j0 = r0; j0 < re; j0 += UNR) {
+        uint32_t d[UNR];
+        MV a[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (j0 + u < re) {
+            d[u] = __builtin_nontemporal_load(cr + (int64_t)(j0 + u) * kPairSlice);
+            a[u] = __builtin_nontemporal_load(cv + (int64_t)(j0 + u) * kPairSlice);
+          } else {
+            d[u] = 0xFFFFFFFFu;
+            a[u] = MV(0);
+          }
+        }
+        V xv[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const bool v = d[u] != 0xFFFFFFFFu;
+          xv[u] = bs(v ? (int64_t)(d[u] & 0x0FFFFFFFu) : 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (d[u] != 0xFFFFFFFFu) pw[d[u] >> 28][lane] = (V)a[u] * xv[u];
+          nv += d[u] != 0xFFFFFFFFu ? 1 : 0;
+        }
+      }
+      for (int k = 0; k < nv; ++k) acc = acc + pw[k][lane];  // the run in stored order
+    }
+    if (row < n) dacc += epi(row, 0, acc, bs(row, 0));
+  }
+  if (part != nullptr) {
+    double *red = reinterpret_cast<double *>(&prod[0][0][0]);
+    __syncthreads();  // every wave is done with its products
+    red[tid] = dacc;
+    block_tree_reduce(red, kBlock, 1);
+    if (tid == 0) part[g] = red[0];
+  }
+}
+
 // ------------------------------ diagonal-offset SpMV, block RHS (k = 2..8)
 // The same SELL-128/DIA image for k right-hand sides stored row-major
 // (n x k): for a slot column of offset o the x rows of the slice's rows are
@@ -908,6 +989,17 @@ __global__ __launch_bounds__(kBlock) void spmv_rs_kernel(const int64_t *__restri
 // column at offset +-o reads again were fetched by a neighbouring wave
 // moments before and are L2 hits (archive:dia_blk_bench: x fetched ~1x from
 // HBM, against ~3x with 2.4 contiguous slices per wave at 8192 blocks).
+// Round 5, the x window: the slice's own x rows (every row < n, mask or
+// not) and the two rows just outside it are loaded once per slice into the
+// wave's LDS window; the slot columns of offset -1, 0 and +1 (the
+// near-diagonal runs of a 2-D / 3-D stencil) and the epilogue's p read their
+// runs from it (ds_read_b128) instead of three more 1 KB runs per group
+// through L1 / L2. cfg4 (5-point Poisson 3163^2, k = 8): 0.458 -> 0.372 ms
+// per launch (tools/dia_blk_probe.hip, profiles/r05_dia_blk_probe.txt). The
+// values and their order are unchanged: a window row holds the same x the
+// direct load would return. Each wave reads only its own window (no
+// barrier: a wave's LDS accesses execute in order; compiler-only barriers
+// keep a read of a neighbour lane's row below the write of it).
 // The epilogue is the lane-group kernel's row<CPL>.
 template <typename V, typename MV, int CPL, int NG, class Src, class Epi>
 __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__restrict__ sptr,
@@ -919,15 +1011,30 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__r
                                                               const Ctrl *ctrl, int step) {
   constexpr int RPG = kDiaSlice / NG;  // rows per group
   constexpr int LPR = 64 / RPG;        // lanes per row (k / CPL)
+  constexpr int WROWS = kDiaSlice + 2;  // window rows 128 s - 1 .. 128 s + 128
+  typedef V vec_t __attribute__((ext_vector_type(CPL)));
   if (halted(ctrl, step)) return;
   __shared__ double red[kBlock * CPL];
+  __shared__ vec_t win[kBlock / 64][WROWS * LPR];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int rl0 = lane / LPR, c0 = (lane % LPR) * CPL;
+  const int rl0 = lane / LPR, cl = lane % LPR, c0 = cl * CPL;
   const int64_t W = (int64_t)gridDim.x * 4;
   const auto bs = src.template bind<CPL>(c0);
+  vec_t *wn = win[wid];
+  auto wput = [&](int wr, const V(&t)[CPL]) {
+    vec_t v;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) v[c] = t[c];
+    wn[wr * LPR + cl] = v;
+  };
+  auto wget = [&](int wr, V(&t)[CPL]) {
+    const vec_t v = wn[wr * LPR + cl];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) t[c] = v[c];
+  };
   double dacc[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) dacc[c] = 0.0;
@@ -935,11 +1042,33 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__r
     const int w = swidth[s];
     const int64_t base = sptr[s];
     const int64_t cb = base / kDiaSlice;
+    const int64_t r0 = s * kDiaSlice;
     V acc[NG][CPL];
 #pragma unroll
     for (int r = 0; r < NG; ++r)
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc[r][c] = V(0);
+    {
+      // the window (rows clamped below n: a row >= n is never read through
+      // a set mask bit, nor stored); lanes < LPR add row r0 - 1, the next
+      // LPR lanes row r0 + 128 (clamped to [0, n))
+      V t[NG][CPL], h[CPL];
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int64_t row = r0 + r * RPG + rl0;
+        bs.row(row < n ? row : n - 1, t[r]);
+      }
+      const int64_t hr = lane < LPR ? (r0 > 0 ? r0 - 1 : 0) : (r0 + kDiaSlice < n ? r0 + kDiaSlice : n - 1);
+      bs.row(hr, h);
+      // LDS accesses of one wave execute in order, so a lane's read of a
+      // neighbour's row sees its write; only the compiler must not move one
+      // across the other (the previous slice's reads stay above the writes)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < NG; ++r) wput(r * RPG + rl0 + 1, t[r]);
+      if (lane < 2 * LPR) wput(lane < LPR ? 0 : WROWS - 1, h);
+      asm volatile("" ::: "memory");
+    }
     for (int j = 0; j < w; ++j) {
       const int off = doff[cb + j];  // wave-uniform: scalar loads
       const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
@@ -952,8 +1081,13 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__r
         const int rl = r * RPG + rl0;
         a[r] = (V)cv[rl];
         on[r] = ((((rl & 1) ? m1 : m0) >> (rl >> 1)) & 1u) != 0;  // mask word (rl & 1), bit (rl >> 1)
-        const int64_t row = s * kDiaSlice + rl;
-        bs.row(on[r] ? row + off : 0, xv[r]);
+      }
+      if (off >= -1 && off <= 1) {  // wave-uniform branch around all the groups' runs
+#pragma unroll
+        for (int r = 0; r < NG; ++r) wget(r * RPG + rl0 + 1 + off, xv[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) bs.row(on[r] ? r0 + r * RPG + rl0 + off : 0, xv[r]);
       }
 #pragma unroll
       for (int r = 0; r < NG; ++r)
@@ -966,10 +1100,10 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_blk_kernel(const int64_t *__r
     }
 #pragma unroll
     for (int r = 0; r < NG; ++r) {
-      const int64_t row = s * kDiaSlice + r * RPG + rl0;
+      const int64_t row = r0 + r * RPG + rl0;
       if (row < n) {
         V xi[CPL];
-        bs.row(row, xi);
+        wget(r * RPG + rl0 + 1, xi);
         epi.template row<CPL>(row, c0, acc[r], xi, dacc);
       }
     }
@@ -1453,6 +1587,14 @@ inline bool dia_blk_off() {
 // SpMV is bound by the random x gathers, so a source that computes on every
 // gathered value (SrcScaled's division) costs more than a pass forming the
 // vector first.
+// The rank-sorted image's kernel: one row per lane with sixteen slot
+// columns' loads in flight (default, KRY_SPMV_RS1=2), eight (1), or the
+// paired two-rows-per-lane kernel (0); tools/rs_ab.py.
+inline int rs1_on() {
+  const char *e = getenv("KRY_SPMV_RS1");  // read per launch: the tests switch it within one process
+  return e ? atoi(e) : 2;
+}
+
 template <typename I>
 inline bool spmv_column_blocked(const kry_csr *A, int k) {
   return sizeof(I) == 4 && k == 1 && !A->dia && A->cb_nb > 0;
@@ -1474,6 +1616,21 @@ void launch_spmv(const kry_csr *A, int k, Src src, Epi epi, double *part, int *g
                        static_cast<const int64_t *>(A->sp_sptr), static_cast<const int *>(A->sp_width),
                        static_cast<const int *>(A->sp_cbase), static_cast<const uint32_t *>(A->sp_delta),
                        static_cast<const MV *>(A->sp_val), A->sp_nslices, A->n, src, epi, part, ctrl, step);
+    KRY_HIP(hipGetLastError());
+    if (grid_out) *grid_out = grid;
+    return;
+  }
+  if (k == 1 && A->rs && rs1_on()) {
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGridBlk, (2 * A->rs_nslices + 3) / 4));
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, static_cast<const int64_t *>(A->rs_sptr),
+                         static_cast<const int *>(A->rs_width), static_cast<const uint32_t *>(A->rs_colrank),
+                         static_cast<const MV *>(A->rs_val), A->rs_nslices, A->n, src, epi, part, ctrl, step);
+    };
+    if (rs1_on() == 2)
+      go(spmv_rs1_kernel<V, MV, 16, Src, Epi>);
+    else
+      go(spmv_rs1_kernel<V, MV, 8, Src, Epi>);
     KRY_HIP(hipGetLastError());
     if (grid_out) *grid_out = grid;
     return;

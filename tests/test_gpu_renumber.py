@@ -56,15 +56,18 @@ def _adversarial(dtype, seed=0, n=200_003, long_rows=True):
     return A, x
 
 
+@pytest.mark.parametrize("rs1", ["0", "1", "2"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_rs_image_bitwise_adversarial(dtype):
+def test_rs_image_bitwise_adversarial(dtype, rs1, monkeypatch):
     """Slot columns wider than a uint16 delta (random columns over 200k) keep
     the paired image out: the rank-sorted image takes
     the matrix, and its SpMV is SciPy's csr_matvec bit for bit (stored-order
     sums through runs of 16, duplicates, explicit zeros, empty rows, rows of
-    up to 70 entries = 5 runs); block RHS stay on SELL-64, bitwise too."""
+    up to 70 entries = 5 runs); block RHS stay on SELL-64, bitwise too.
+    KRY_SPMV_RS1=1 / 2: the one-row-per-lane kernel over the same image."""
     import krylov_amd
 
+    monkeypatch.setenv("KRY_SPMV_RS1", rs1)
     A, x = _adversarial(dtype)
     assert not A.has_sorted_indices
     op = krylov_amd.CsrOperator(A)

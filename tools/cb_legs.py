@@ -3,7 +3,7 @@
 n = 2e6; the column-blocked spmv_cbp_kernel) or on the metric matrix under a
 random symmetric permutation (bench.py's spmv_unstructured): "permuted" as
 given (KRY_RENUMBER=0: column-blocked), "permuted_rs" renumbered at upload
-(round 5: the rank-sorted spmv_rs_kernel, plus the two row permutations of
+(round 5: the rank-sorted spmv_rs1_kernel, plus the two row permutations of
 kry_spmv). x uploaded and y downloaded per call (the counters are per kernel).
 
     python3 tools/cb_legs.py cfg3|permuted|permuted_rs [REPS]

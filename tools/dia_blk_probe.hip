@@ -272,6 +272,107 @@ __global__ __launch_bounds__(256) void slot_rowdpp(const int64_t *__restrict__ s
   if (tid < K) part[(int64_t)g * K + tid] = red[tid];
 }
 
+// LDS window (round 5), the library's coalesced layout (lane l: row l >> 2 of
+// each 16-row group, column pair l & 3). The slice's offset-0 x window is
+// loaded once into registers (every row < n, mask or not) and written to the
+// wave's own LDS window together with the rows just outside the slice; the
+// -1 / +1 slot columns read their x runs from it (ds_read_b128 at +-64 B),
+// and the epilogue's p is the register window. No barrier: each wave reads
+// only its own window (s_waitcnt on LDS). MODE bit 1: shuffled nt values.
+template <int MODE>
+__global__ __launch_bounds__(256) void slot_ldswin(const int64_t *__restrict__ sptr, const int *__restrict__ swidth,
+                                                   const int *__restrict__ doff, const uint64_t *__restrict__ dmask,
+                                                   const double *__restrict__ val, int64_t nslices, int64_t n,
+                                                   const double *__restrict__ x, double *__restrict__ y,
+                                                   double *__restrict__ part) {
+  constexpr bool SHUF = (MODE & 1) != 0;
+  constexpr int WROWS = kDiaSlice + 2;  // rows r0 - 1 .. r0 + 128
+  __shared__ d2v win[4][WROWS * 4];
+  __shared__ double red[256 * CPL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int rl0 = lane / LPR, cp = lane % LPR, c0 = cp * CPL;
+  d2v *W = win[wid];
+  double dacc[CPL] = {0.0, 0.0};
+  for (int64_t s = (int64_t)g * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+    const int w = swidth[s];
+    const int64_t base = sptr[s], cb = base / kDiaSlice, r0 = s * kDiaSlice;
+    double acc[NG][CPL];
+#pragma unroll
+    for (int r = 0; r < NG; ++r) acc[r][0] = acc[r][1] = 0.0;
+    {
+      // the window: rows r0 .. r0 + 127 (clamped below n) and the halo rows
+      // r0 - 1 (lanes 0..3) and r0 + 128 (lanes 4..7), clamped
+      d2v xc[NG];
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int64_t row = r0 + r * RPG + rl0;
+        xc[r] = *reinterpret_cast<const d2v *>(x + (row < n ? row : n - 1) * K + c0);
+      }
+      const int64_t hr = lane < 4 ? (r0 > 0 ? r0 - 1 : 0) : (r0 + kDiaSlice < n ? r0 + kDiaSlice : n - 1);
+      const d2v h = *reinterpret_cast<const d2v *>(x + hr * K + c0);
+      if (lane < 8) W[(lane < 4 ? 0 : WROWS - 1) * 4 + cp] = h;
+#pragma unroll
+      for (int r = 0; r < NG; ++r) W[(r * RPG + rl0 + 1) * 4 + cp] = xc[r];
+    }
+    for (int j = 0; j < w; ++j) {
+      const int off = doff[cb + j];
+      const uint64_t m0 = dmask[2 * (cb + j)], m1 = dmask[2 * (cb + j) + 1];
+      double a[NG];
+      d2v xv[NG];
+      bool on[NG];
+      d2v vv;
+      if (SHUF) vv = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(val + base + (int64_t)j * kDiaSlice) + lane);
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const int rl = r * RPG + rl0;
+        if (!SHUF) a[r] = val[base + (int64_t)j * kDiaSlice + rl];
+        on[r] = (((rl & 1) ? m1 : m0) >> (rl >> 1) & 1u) != 0;
+      }
+      if (off >= -1 && off <= 1) {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) xv[r] = W[(r * RPG + rl0 + 1 + off) * 4 + cp];
+      } else {
+#pragma unroll
+        for (int r = 0; r < NG; ++r)
+          xv[r] = *reinterpret_cast<const d2v *>(x + (on[r] ? r0 + r * RPG + rl0 + off : 0) * K + c0);
+      }
+      if (SHUF) {
+#pragma unroll
+        for (int r = 0; r < NG; ++r) {
+          const int rl = r * RPG + rl0;
+          const double lo = __shfl(vv.x, rl >> 1), hi = __shfl(vv.y, rl >> 1);
+          a[r] = (rl & 1) ? hi : lo;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NG; ++r) {
+        const double t0 = acc[r][0] + a[r] * xv[r].x, t1 = acc[r][1] + a[r] * xv[r].y;
+        acc[r][0] = on[r] ? t0 : acc[r][0];
+        acc[r][1] = on[r] ? t1 : acc[r][1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NG; ++r) {
+      const int64_t row = r0 + r * RPG + rl0;
+      if (row < n) {
+        d2v v;
+        v.x = acc[r][0];
+        v.y = acc[r][1];
+        __builtin_nontemporal_store(v, reinterpret_cast<d2v *>(y + row * K + c0));
+        const d2v q = W[(r * RPG + rl0 + 1) * 4 + cp];
+        dacc[0] += q.x * acc[r][0];
+        dacc[1] += q.y * acc[r][1];
+      }
+    }
+  }
+  red[tid * CPL] = dacc[0];
+  red[tid * CPL + 1] = dacc[1];
+  block_tree_reduce(red, 256 * CPL, K);
+  if (tid < K) part[(int64_t)g * K + tid] = red[tid];
+}
+
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 3163;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -364,6 +465,16 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(got.data(), y, n * K * 8, hipMemcpyDeviceToHost));                                            \
     if (memcmp(got.data(), ref.data(), n * K * 8) != 0) printf("  !! %s differs from the library\n", NAME);   \
   }
+#define LW(MODE, NAME)                                                                                         \
+  {                                                                                                            \
+    timeit(NAME, [&] {                                                                                         \
+      hipLaunchKernelGGL((slot_ldswin<MODE>), dim3(full), dim3(256), 0, st, (const int64_t *)A->dia_sptr,      \
+                         (const int *)A->dia_width, (const int *)A->dia_off, (const uint64_t *)A->dia_mask,   \
+                         (const double *)A->dia_val, A->dia_nslices, n, (const double *)x, y, part);          \
+    });                                                                                                        \
+    CK(hipMemcpy(got.data(), y, n * K * 8, hipMemcpyDeviceToHost));                                            \
+    if (memcmp(got.data(), ref.data(), n * K * 8) != 0) printf("  !! %s differs from the library\n", NAME);   \
+  }
   for (int rep = 0; rep < 2; ++rep) {
     timeit("library spmv_dia_blk (EpiApDot)", library);
     timeit("floor: p read + Ap write", [&] {
@@ -375,6 +486,8 @@ int main(int argc, char **argv) {
     SM(3, "slot-major, shuffled nt values, no x", false);
     RD(0, "row-per-lane layout");
     RD(4, "row-per-lane layout, -1/0/+1 x by DPP");
+    LW(0, "LDS window, -1/0/+1 x from registers");
+    LW(1, "LDS window + shuffled nt values");
   }
   CK(hipFree(part));
   KC(kry_vec_destroy(xv));

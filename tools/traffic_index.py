@@ -59,9 +59,9 @@ def main():
     sd = next(v for k, v in mg.items() if "EpiStoreDot" in k)
     idx["gmres_metric"] = {"mgs": entry(METRIC, mgsl["fetch_bytes_mean"] + mgsl["write_bytes_mean"], "r03_pmc_mgsl.json"),
                            "spmv": entry(METRIC, sd["fetch_bytes_mean"] + sd["write_bytes_mean"], "r03_pmc_mgsl.json")}
-    db = load("r04_pmc_dia_blk.json")
+    db = load("r05_pmc_dia_blk.json")
     idx["cfg4"] = {"spmv": entry(CFG4, kernel_row(db, "void kry::spmv_dia_blk_kernel")["hbm_bytes"],
-                                 "r04_pmc_dia_blk.json")}
+                                 "r05_pmc_dia_blk.json")}
     c5 = load("r04_pmc_cfg5.json")
     idx["cfg5"] = {"spmv": entry(CFG5, kernel_row(c5, "void kry::spmv_dia_kernel<double, float, 8, kry::SrcPlain<double>, "
                                                   "kry::EpiLanczos")["hbm_bytes_corrected"], "r04_pmc_cfg5.json"),
