@@ -484,9 +484,6 @@ def run_end_to_end(A_host, steps):
     PCIe-inclusive rate DESIGN.md (d) quotes. Median of 3 after a warm-up."""
     import krylov_amd
 
-    from krylov_amd import _helpers
-    from krylov_amd.cg import _CGState
-
     A = krylov_amd.CsrOperator(A_host)
     b = np.ones(A.n)
     out = {}
@@ -508,26 +505,19 @@ def run_end_to_end(A_host, steps):
         t = float(np.median(ts))
         out[f"{label}_it_per_s"] = iters / t
         out[f"{label}_call_ms"] = 1e3 * t
-    # the same CG chunks without the host-array boundary (b already on the
-    # device, no x download): the call's fixed cost is the difference
-    prob = _helpers.Problem(A, b, None, None)
-    st = _CGState(prob)
-    dev = []
-    for _ in range(3):
-        st.start()
-        st.set_criterion(np.zeros(1))
-        A.ctx.synchronize()
-        t0 = time.perf_counter()
-        k = 0
-        while k < steps:
-            k += len(st.run(min(st.preferred_chunk(), steps - k)))
-        dev.append(time.perf_counter() - t0)
-    del st, prob
-    out["cg_device_loop_ms"] = 1e3 * float(np.median(dev))
-    out["cg_fixed_ms"] = out["cg_call_ms"] - out["cg_device_loop_ms"]
+    # the call's fixed cost: the call minus its own chunked device loop
+    # (krylov_amd.cg.last_timing: the host clock around the kry_cg_run calls)
+    cgmod = sys.modules["krylov_amd.cg"]
+    fixed = []
+    for _ in range(5):
+        r = krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
+        lt = cgmod.last_timing
+        fixed.append(lt["call_ms"] - lt["chunks_ms"])
+        del r
+    out["cg_fixed_ms"] = float(np.median(fixed))
     out["includes"] = ("b upload (H2D), solver state setup, per-chunk host syncs, x download (D2H); the operator "
-                       "is uploaded once before (CsrOperator); cg_fixed_ms = the call minus the same chunked "
-                       "device loop; the caller's x is released after the timing (result_free_ms)")
+                       "is uploaded once before (CsrOperator); cg_fixed_ms = the call minus its own chunked device "
+                       "loop (median of 5); the caller's x is released after the timing (result_free_ms)")
     # the operator upload itself (kry_csr_create: one H2D of the CSR arrays,
     # the SELL-64 and DIA images built on the device), median of 3
     del A

@@ -9,6 +9,7 @@ residual norms satisfy the criterion, so the host sees exactly the
 iterations the reference performs.
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -16,6 +17,13 @@ from . import _helpers, _lib
 from ._helpers import Info, Problem
 from .device import HostOut
 from ._lib import check, lib
+
+
+# host-clock split of the last cg() call on the device path: the whole call
+# and the part spent inside the chunked device loop (kry_cg_run calls); the
+# difference is the call's fixed cost at the host-array boundary (bench.py
+# end_to_end)
+last_timing = {}
 
 
 class _CGState:
@@ -121,6 +129,8 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
 
         return solve("cg", A, b, devices, x0=x0, tol=tol, atol=atol, maxiter=maxiter, callback=callback, M=M,
                      Ml=Ml)
+    t_call = time.perf_counter()
+    t_run = 0.0
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter
@@ -149,7 +159,9 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         if k == maxiter:
             break
         steps = 1 if (callback is not None or lanczos is not None) else min(chunk, maxiter - k)
+        t0 = time.perf_counter()
         hist = st.run(steps)
+        t_run += time.perf_counter() - t0
         for row in hist:
             resnorms.append(prob.colvals(row))
             if lanczos is not None:
@@ -168,6 +180,7 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         "axpy": 2 + 2 * k,
     }
     arnoldi = lanczos.result(k) if lanczos is not None else None
+    last_timing.update(call_ms=1e3 * (time.perf_counter() - t_call), chunks_ms=1e3 * t_run)
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, arnoldi=arnoldi)
 
 

@@ -932,6 +932,7 @@ __global__ __launch_bounds__(kBlock) void spmv_rs1_kernel(const int64_t *__restr
     const int64_t row = s * kPairSlice + q;
     const uint32_t *cr = colrank + base + q;
     const MV *cv = val + base + q;
+    const V xi = bs(row < n ? row : 0, 0);  // the epilogue's x, in flight with the run's loads
     V acc = V(0);
     for (int r0 = 0; r0 < w; r0 += kRsRun) {
       const int re = w < r0 + kRsRun ? w : r0 + kRsRun;
@@ -961,9 +962,15 @@ __global__ __launch_bounds__(kBlock) void spmv_rs1_kernel(const int64_t *__restr
           nv += d[u] != 0xFFFFFFFFu ? 1 : 0;
         }
       }
-      for (int k = 0; k < nv; ++k) acc = acc + pw[k][lane];  // the run in stored order
+      // the run in stored order: all sixteen LDS reads issued together (the
+      // slots past the run's nv entries are read and dropped), then the adds
+      V t[kRsRun];
+#pragma unroll
+      for (int k = 0; k < kRsRun; ++k) t[k] = pw[k][lane];
+#pragma unroll
+      for (int k = 0; k < kRsRun; ++k) acc = k < nv ? acc + t[k] : acc;
     }
-    if (row < n) dacc += epi(row, 0, acc, bs(row, 0));
+    if (row < n) dacc += epi(row, 0, acc, xi);
   }
   if (part != nullptr) {
     double *red = reinterpret_cast<double *>(&prod[0][0][0]);

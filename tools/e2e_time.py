@@ -129,8 +129,55 @@ def profile_calls(steps_list=(20, 200)):
         pstats.Stats(pr, stream=sys.stdout).sort_stats("tottime").print_stats(14)
 
 
+def phases(steps=200, calls=5):
+    """cg()'s sequence restated with a clock between its phases, the
+    results kept alive as bench.py's end_to_end leg keeps them."""
+    import krylov_amd
+    from krylov_amd import _helpers, problems
+    from krylov_amd.cg import _CGState
+    from krylov_amd.device import HostOut
+
+    M = problems.stencil15_3d(216)
+    A = krylov_amd.CsrOperator(M)
+    b = np.ones(M.shape[0])
+    keep, rows = [], []
+    for c in range(calls + 1):
+        t = [time.perf_counter()]
+        prob = _helpers.Problem(A, b, None, None)
+        t.append(time.perf_counter())
+        st = _CGState(prob)
+        t.append(time.perf_counter())
+        xo = HostOut((prob.n, prob.kpad), prob.dtype)
+        t.append(time.perf_counter())
+        st.start()
+        t.append(time.perf_counter())
+        st.set_criterion(np.zeros(1))
+        chunk = st.preferred_chunk()
+        k = 0
+        while k < steps:
+            k += len(st.run(min(chunk, steps - k)))
+        t.append(time.perf_counter())
+        x = xo.take()
+        t.append(time.perf_counter())
+        st.get(0, out=x)
+        t.append(time.perf_counter())
+        del st, prob
+        t.append(time.perf_counter())
+        keep.append(x)
+        if c:
+            rows.append(np.diff(t) * 1e3)
+    names = ["Problem (b upload)", "_CGState", "HostOut", "start", "chunks", "HostOut.take", "get (x D2H)", "destructors"]
+    med = np.median(np.array(rows), axis=0)
+    print(f"cg maxiter={steps} phases, median of {calls} (ms): " + ", ".join(f"{n} {v:.2f}" for n, v in zip(names, med))
+          + f"; total {med.sum():.2f}, outside the chunks {med.sum() - med[4]:.2f}", flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "profile":
         profile_calls()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "phases":
+        phases(200)
+        phases(20)
         sys.exit(0)
     main(int(sys.argv[1]) if len(sys.argv) > 1 else 200)
