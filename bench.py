@@ -508,13 +508,16 @@ def run_end_to_end(A_host, steps):
     # the call's fixed cost: the call minus its own chunked device loop
     # (krylov_amd.cg.last_timing: the host clock around the kry_cg_run calls)
     cgmod = sys.modules["krylov_amd.cg"]
-    fixed = []
+    fixed, parts = [], []
+    names = ("problem_ms", "setup_start_ms", "loop_host_ms", "get_ms", "finish_ms")
     for _ in range(5):
         r = krylov_amd.cg(A, b, tol=0.0, atol=0.0, maxiter=steps)
-        lt = cgmod.last_timing
+        lt = dict(cgmod.last_timing)
         fixed.append(lt["call_ms"] - lt["chunks_ms"])
+        parts.append([lt[nm] for nm in names])
         del r
     out["cg_fixed_ms"] = float(np.median(fixed))
+    out["cg_fixed_parts_ms"] = {nm: float(v) for nm, v in zip(names, np.median(np.array(parts), axis=0))}
     out["includes"] = ("b upload (H2D), solver state setup, per-chunk host syncs, x download (D2H); the operator "
                        "is uploaded once before (CsrOperator); cg_fixed_ms = the call minus its own chunked device "
                        "loop (median of 5); the caller's x is released after the timing (result_free_ms)")
@@ -803,7 +806,8 @@ def compact(full, idx=None):
         legs["bicgstab_cfg3"] = {"it_per_s": _r(b["it_per_s"]), **_kroof(b["roofline"], t, src)}
     e = full.get("end_to_end")
     if e:
-        legs["end_to_end"] = {k: _r(v) for k, v in e.items() if k != "includes"}
+        legs["end_to_end"] = {k: ({kk: _r(vv, 3) for kk, vv in v.items()} if isinstance(v, dict) else _r(v))
+                              for k, v in e.items() if k != "includes"}
     c2 = full.get("cfg2")
     if c2:
         r = c2["roofline"]

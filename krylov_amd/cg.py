@@ -132,12 +132,14 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     t_call = time.perf_counter()
     t_run = 0.0
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
+    t_prob = time.perf_counter()
     N = prob.A.shape[0]
     maxiter = N if maxiter is None else maxiter
 
     st = _CGState(prob)
     x_out = HostOut((prob.n, prob.kpad), prob.dtype)  # pages faulted in while the device iterates
     rho0 = st.start()
+    t_start = time.perf_counter()
     chunk = st.preferred_chunk()
     rn0 = _norm_from_sq(prob, rho0)
     if callback is not None:
@@ -170,7 +172,9 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         if callback is not None and len(hist):
             callback(prob.unpad_vec(st.get(0), prob.r0_dtype), prob.unpad_vec(st.get(1), prob.r0_dtype))
 
+    t_loop = time.perf_counter()
     xk = prob.unpad_vec(st.get(0, out=x_out.take()), prob.r0_dtype)
+    t_get = time.perf_counter()
     num_operations = {
         "A": 1 + k,
         "M": 2 + k,
@@ -180,7 +184,10 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
         "axpy": 2 + 2 * k,
     }
     arnoldi = lanczos.result(k) if lanczos is not None else None
-    last_timing.update(call_ms=1e3 * (time.perf_counter() - t_call), chunks_ms=1e3 * t_run)
+    t_end = time.perf_counter()
+    last_timing.update(call_ms=1e3 * (t_end - t_call), chunks_ms=1e3 * t_run, problem_ms=1e3 * (t_prob - t_call),
+                       setup_start_ms=1e3 * (t_start - t_prob), loop_host_ms=1e3 * (t_loop - t_start - t_run),
+                       get_ms=1e3 * (t_get - t_loop), finish_ms=1e3 * (t_end - t_get))
     return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, arnoldi=arnoldi)
 
 

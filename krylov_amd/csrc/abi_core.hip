@@ -264,17 +264,42 @@ void load_in(const kry_csr *A, const void *src, void *dst, int k, size_t esize, 
   permute_rows(A, src, dst, k, esize, true, st);
 }
 
+bool env_off(const char *name) {
+  const char *e = getenv(name);
+  return e && atoi(e) == 0;
+}
+
+void host_xfer(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
+  constexpr size_t kPinMin = size_t(4) << 20;
+  static const bool pin = !env_off("KRY_HOST_PIN");
+  void *host = kind == hipMemcpyHostToDevice ? const_cast<void *>(src) : dst;
+  bool reg = false;
+  if (pin && bytes >= kPinMin) {
+    if (hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess)
+      reg = true;
+    else
+      (void)hipGetLastError();  // already registered, or not registrable: pageable
+  }
+  try {
+    KRY_HIP(hipMemcpyAsync(dst, src, bytes, kind, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  } catch (...) {
+    if (reg) (void)hipHostUnregister(host);
+    throw;
+  }
+  if (reg) KRY_HIP(hipHostUnregister(host));
+}
+
 void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st) {
   const size_t bytes = (size_t)A->n * k * esize;
   if (!A->renumbered) {
-    KRY_HIP(hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, st));
+    host_xfer(host, src, bytes, hipMemcpyDeviceToHost, st);
     return;
   }
   void *tmp = dev_alloc(bytes + 16);
   try {
     permute_rows(A, src, tmp, k, esize, false, st);
-    KRY_HIP(hipMemcpyAsync(host, tmp, bytes, hipMemcpyDeviceToHost, st));
-    KRY_HIP(hipStreamSynchronize(st));
+    host_xfer(host, tmp, bytes, hipMemcpyDeviceToHost, st);
   } catch (...) {
     dev_free(tmp);
     throw;
@@ -484,10 +509,6 @@ uint64_t perm_fingerprint(const std::vector<int32_t> &p) {
   return h;
 }
 
-bool env_off(const char *name) {
-  const char *e = getenv(name);
-  return e && atoi(e) == 0;
-}
 
 // like_perm: build P A P^T with another operator's renumbering (a
 // preconditioner of a renumbered operator); otherwise renumber when the
@@ -527,8 +548,8 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::v
         void *dip = dev_alloc((size_t)(n + 1) * 4);
         void *dix = dev_alloc((size_t)std::max<int64_t>(nnz, 1) * 4);
         try {
-          KRY_HIP(hipMemcpyAsync(dip, ip, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-          if (nnz) KRY_HIP(hipMemcpyAsync(dix, ix, (size_t)nnz * 4, hipMemcpyHostToDevice, st));
+          host_xfer(dip, ip, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st);
+          if (nnz) host_xfer(dix, ix, (size_t)nnz * 4, hipMemcpyHostToDevice, st);
           r = rcm_order_device(A->ctx, n, static_cast<const int32_t *>(dip), static_cast<const int32_t *>(dix), wlimit,
                                own, &A->rcm_levels);
         } catch (...) {
@@ -700,10 +721,10 @@ void csr_upload(kry_csr *A, const I *ip, const I *ix, const MV *dv, const std::v
     A->indptr = dev_alloc((n + 1) * sizeof(I));
     A->indices = dev_alloc((nnz + 1) * sizeof(I));
     A->data = dev_alloc((nnz + 1) * sizeof(MV));
-    KRY_HIP(hipMemcpyAsync(A->indptr, ip, (n + 1) * sizeof(I), hipMemcpyHostToDevice, st));
+    host_xfer(A->indptr, ip, (n + 1) * sizeof(I), hipMemcpyHostToDevice, st);
     if (nnz) {
-      KRY_HIP(hipMemcpyAsync(A->indices, ix, nnz * sizeof(I), hipMemcpyHostToDevice, st));
-      KRY_HIP(hipMemcpyAsync(A->data, dv, nnz * sizeof(MV), hipMemcpyHostToDevice, st));
+      host_xfer(A->indices, ix, nnz * sizeof(I), hipMemcpyHostToDevice, st);
+      host_xfer(A->data, dv, nnz * sizeof(MV), hipMemcpyHostToDevice, st);
     }
   }
   KRY_HIP(hipStreamSynchronize(st));  // host staging vectors die at return
@@ -894,16 +915,14 @@ int kry_vec_destroy(kry_vec *v) {
 int kry_vec_upload(kry_vec *v, const void *host) {
   KRY_API_BEGIN
   KRY_REQUIRE(v && host, KRY_EINVAL, "null argument");
-  KRY_HIP(hipMemcpyAsync(v->d, host, v->bytes(), hipMemcpyHostToDevice, v->ctx->stream));
-  KRY_HIP(hipStreamSynchronize(v->ctx->stream));
+  host_xfer(v->d, host, v->bytes(), hipMemcpyHostToDevice, v->ctx->stream);
   KRY_API_END
 }
 
 int kry_vec_download(kry_vec *v, void *host) {
   KRY_API_BEGIN
   KRY_REQUIRE(v && host, KRY_EINVAL, "null argument");
-  KRY_HIP(hipMemcpyAsync(host, v->d, v->bytes(), hipMemcpyDeviceToHost, v->ctx->stream));
-  KRY_HIP(hipStreamSynchronize(v->ctx->stream));
+  host_xfer(host, v->d, v->bytes(), hipMemcpyDeviceToHost, v->ctx->stream);
   KRY_API_END
 }
 

@@ -299,9 +299,9 @@ int device_image_build(kry_csr *A, const int32_t *ip, const int32_t *ix, const M
   KRY_REQUIRE(ip[0] == 0 && (int64_t)ip[n] == nnz, KRY_EINVAL, "indptr must start at 0 and end at nnz");
   // the caller's CSR, once
   Tmp dip((size_t)(n + 1) * 4 + 16), dix((size_t)nnz * 4 + 16), ddv((size_t)nnz * sizeof(MV) + 16);
-  KRY_HIP(hipMemcpyAsync(dip.p, ip, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-  KRY_HIP(hipMemcpyAsync(dix.p, ix, (size_t)nnz * 4, hipMemcpyHostToDevice, st));
-  KRY_HIP(hipMemcpyAsync(ddv.p, dv, (size_t)nnz * sizeof(MV), hipMemcpyHostToDevice, st));
+  host_xfer(dip.p, ip, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st);
+  host_xfer(dix.p, ix, (size_t)nnz * 4, hipMemcpyHostToDevice, st);
+  host_xfer(ddv.p, dv, (size_t)nnz * sizeof(MV), hipMemcpyHostToDevice, st);
   Tmp small(256);
   KRY_HIP(hipMemsetAsync(small.p, 0, 256, st));
   unsigned *flags = small.as<unsigned>();

@@ -153,6 +153,15 @@ void load_in(const kry_csr *A, const void *src, void *dst, int k, size_t esize, 
 // The get form: solver storage (operator numbering) to a host buffer in the
 // caller's numbering (through a temporary device block when renumbered).
 void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st);
+// A synchronous host <-> device copy; from 4 MB on through the caller's
+// pages pinned in place for the copy (hipHostRegister), so the DMA engine
+// reads / writes them directly at the link rate instead of a pageable copy
+// staged through a bounce buffer by host memcpy (28-56 GB/s by box). Pages
+// that cannot be registered take the pageable path. KRY_HOST_PIN=0: always
+// pageable.
+void host_xfer(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hipStream_t st);
+// true when the environment variable is set to 0 (a default-on switch turned off)
+bool env_off(const char *name);
 // Device-side image build (device_build.hip; int32 CSR): uploads the CSR
 // arrays, validates them, builds SELL-64 (+ compact) and the DIA image.
 // Returns 0: nothing built (scattered and renumber_candidates: the

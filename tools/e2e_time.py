@@ -138,7 +138,14 @@ def phases(steps=200, calls=5):
     from krylov_amd.device import HostOut
 
     M = problems.stencil15_3d(216)
-    A = krylov_amd.CsrOperator(M)
+    cs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        A = krylov_amd.CsrOperator(M)
+        A.ctx.synchronize()
+        cs.append(time.perf_counter() - t0)
+    print(f"CsrOperator (kry_csr_create) median of 3: {1e3 * float(np.median(cs)):.1f} ms "
+          f"(KRY_HOST_PIN={os.environ.get('KRY_HOST_PIN', '1')})", flush=True)
     b = np.ones(M.shape[0])
     keep, rows = [], []
     for c in range(calls + 1):
