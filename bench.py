@@ -517,7 +517,13 @@ def run_end_to_end(A_host, steps):
         parts.append([lt[nm] for nm in names])
         del r
     out["cg_fixed_ms"] = float(np.median(fixed))
-    out["cg_fixed_parts_ms"] = {nm: float(v) for nm, v in zip(names, np.median(np.array(parts), axis=0))}
+    med = dict(zip(names, np.median(np.array(parts), axis=0)))
+    out["cg_fixed_parts_ms"] = {nm: float(v) for nm, v in med.items()}
+    # the box's host link, from the two 80 MB copies of the call (b in, x out):
+    # the fixed cost net of them is what the library spends itself
+    out["h2d_gbs"] = b.nbytes / (med["problem_ms"] * 1e6)
+    out["d2h_gbs"] = b.nbytes / (med["get_ms"] * 1e6)
+    out["cg_fixed_net_of_copies_ms"] = out["cg_fixed_ms"] - med["problem_ms"] - med["get_ms"]
     out["includes"] = ("b upload (H2D), solver state setup, per-chunk host syncs, x download (D2H); the operator "
                        "is uploaded once before (CsrOperator); cg_fixed_ms = the call minus its own chunked device "
                        "loop (median of 5); the caller's x is released after the timing (result_free_ms)")
