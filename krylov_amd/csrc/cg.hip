@@ -1330,35 +1330,22 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       ProfScope ps(s->ctx, PROF_OTHER);
       constexpr int W = Vec16<V>::W;
       const int G = grid_for((N + W - 1) / W, kBlock * 2);
-      // Every block of the yp / p pass re-reduces the r pass's <r, r>
-      // partials: stage the PB = kCgUpdateGrid rows to kAlphaStage first (into
-      // partA, free once alpha is formed), so each of the G blocks reads 8 KB
-      // instead of 64 KB (k = 8). cfg4: the p pass 403 -> ~350 us, as fast as
-      // the r pass (profiles/r05_cfg4_kernel_stats.csv). KRY_RHO_STAGE=0: off.
-      static const bool rho_stage = !env_off("KRY_RHO_STAGE");
-      const double *pB = partB;
-      if (rho_stage && PB > 4 * kAlphaStage) {
-        hipLaunchKernelGGL(partial_stage_kernel, dim3(kAlphaStage), dim3(kBlock), 0, st, partB, PB, k, partA, s->ctrl,
-                           step);
-        pB = partA;
-        PB = kAlphaStage;
-      }
       if (D) {
         if (s->scalar_f32)
           hipLaunchKernelGGL((cg_pdefer_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
-                             ring, D, static_cast<const V *>(s->r), pB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
+                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
                              step, gb, s->col_offset, s->total_k);
         else
           hipLaunchKernelGGL((cg_pdefer_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
-                             ring, D, static_cast<const V *>(s->r), pB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
+                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
                              step, gb, s->col_offset, s->total_k);
       } else if (s->scalar_f32)
         hipLaunchKernelGGL((cg_yp_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
-                           static_cast<const V *>(s->r), pB, PB, s->scal, s->hist, s->ctrl, step, gb,
+                           static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
                            s->col_offset, s->total_k);
       else
         hipLaunchKernelGGL((cg_yp_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
-                           static_cast<const V *>(s->r), pB, PB, s->scal, s->hist, s->ctrl, step, gb,
+                           static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
                            s->col_offset, s->total_k);
       KRY_HIP(hipGetLastError());
     } else {  // alpha kernel, update pass, [z = M r], one-block rho kernel, p pass

@@ -24,7 +24,7 @@ def main(out, compulsory):
                 acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {}
     for kern, cs in acc.items():
-        short = kern.split("(")[0][:90]
+        short = kern.replace("(anonymous namespace)::", "").split("(")[0][:90]
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         d = {"kernel": kern[:200], "dispatches": max(len(v) for v in cs.values()), "counters": m}
         if "SQ_INSTS_VMEM_RD" in m and "SQ_WAVES" in m:
