@@ -10,7 +10,10 @@ krylov_amd.distributed.cg / gmres / minres. The parent then checks:
 - at tol = 1e-8, that both ranks stop at the step of the 16-column block
   solve (the global stop rule over both ranks' columns) with its history to
   1e-12.
-If RCCL refuses two ranks on one device, the script says so and exits 3.
+If RCCL refuses two ranks on one device, the script says so and exits 3:
+RCCL does ("Duplicate GPU detected", gpurun r05t, profiles/r05_rccl_2rank.txt),
+so on the pool's one-GPU boxes the real cross-rank sum cannot run; on a node
+with two GPUs, KRY_2RANK_DEVICES=0,1 puts the ranks on two devices.
 
     python3 tools/rccl_2rank.py            (parent: spawns the two ranks)
 """
@@ -39,7 +42,8 @@ def worker(rank, path, out):
     from krylov_amd import distributed
 
     P, B = problem()
-    comm = distributed.ShardComm.from_file(path, rank, 2, device=0)
+    devs = [int(d) for d in os.environ.get("KRY_2RANK_DEVICES", "0,0").split(",")]
+    comm = distributed.ShardComm.from_file(path, rank, 2, device=devs[rank])
     for c, (method, kw) in enumerate(CASES):
         _, info = getattr(distributed, method)(P, np.ascontiguousarray(B[:, 8 * rank:8 * rank + 8]), comm, **kw)
         np.save(f"{out}_{c}_{rank}_x.npy", np.asarray(info.xk))
