@@ -506,3 +506,35 @@ def test_multi_solve_triangular_errors():
     with pytest.raises(ValueError):
         krylov_amd.multi_solve_triangular(nan, y)
     np.testing.assert_array_equal(krylov_amd.multi_solve_triangular(bad, np.zeros((4, 1))), np.zeros((4, 1)))
+
+
+def test_host_transfers_pinned_in_place_and_fallback():
+    """Large host <-> device copies go through the caller's pages pinned in
+    place (host_xfer: hipHostRegister for the copy, then unregistered).
+    Round trips are bitwise for a pageable array, a view that starts inside
+    a page, an array that is already page-locked (torch pinned memory:
+    registration fails, the plain copy runs), and a read-only array; the
+    same host array can be copied again afterwards (it was unregistered)."""
+    import torch
+
+    import krylov_amd
+    from krylov_amd.device import DeviceVector
+
+    ctx = krylov_amd.CsrOperator(scipy.sparse.identity(8, format="csr")).ctx
+    n = 1_000_003  # 8 MB: above the 4 MB pinning threshold
+    rng = np.random.default_rng(5)
+    base = rng.standard_normal(n + 3)
+    pinned = torch.empty(n, dtype=torch.float64, pin_memory=True).numpy()
+    pinned[:] = rng.standard_normal(n)
+    ro = rng.standard_normal(n)
+    ro.setflags(write=False)
+    for src in (base[:n].copy(), base[3:], pinned, ro):
+        v = DeviceVector(ctx, n, 1, np.float64)
+        v.upload(src.reshape(n, 1))
+        out = np.empty((n, 1))
+        v.to_host(out)
+        np.testing.assert_array_equal(out[:, 0].view(np.uint64), np.ascontiguousarray(src).view(np.uint64))
+        v.upload(src.reshape(n, 1))  # again: the pages were unregistered after the first copy
+        back = np.full((n, 1), np.nan)
+        v.to_host(back)
+        np.testing.assert_array_equal(back.view(np.uint64), out.view(np.uint64))
