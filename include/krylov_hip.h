@@ -428,6 +428,13 @@ int kry_comm_create(kry_ctx *ctx, int32_t nranks, int32_t rank, const void *id12
  * ranks of SURVEY §8(e) when the caller has one process for the node. */
 int kry_comm_create_all(kry_ctx **ctxs, int32_t n, kry_comm **out);
 int kry_comm_destroy(kry_comm *c);
+/* Abort a communicator, from any thread, while a collective on it may be
+ * pending (ncclCommAbort; kry_version() >= 105): that and every later
+ * collective fail, so a solver waiting on a rank that will not come stops
+ * with KRY_ECOMM. kry_comm_destroy still releases the handle. No reference
+ * counterpart: the devices=[...] driver aborts every device's communicator
+ * when one device's thread fails. */
+int kry_comm_abort(kry_comm *c);
 /* in-place sum over ranks of `count` host doubles (setup-time exchanges) */
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);
 int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k);

@@ -126,6 +126,7 @@ _SIGNATURES = {
     "kry_comm_unique_id": [_vp],
     "kry_comm_create": [_vp, _i32, _i32, _vp, _pvp],
     "kry_comm_destroy": [_vp],
+    "kry_comm_abort": [_vp],
     "kry_comm_create_all": [_vp, _i32, _vp],
     "kry_comm_allreduce": [_vp, _dp, _i32],
     "kry_cg_attach_comm": [_vp, _vp, _i32, _i32],

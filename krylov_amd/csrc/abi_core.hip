@@ -396,7 +396,7 @@ extern "C" {
 // 103: the per-step allreduces of the sharded solvers carry a fault count
 // (CG total_k + 1, GMRES / MINRES total_k + 2 values); kry_cg_defer_info,
 // kry_gmres_xk_device.
-int kry_version(void) { return 104; }
+int kry_version(void) { return 105; }
 
 int kry_device_count(int *count) {
   KRY_API_BEGIN

@@ -728,12 +728,27 @@ struct CgpBufs {
   double *Sout;              // scalar slots after a clean chunk
 };
 
-template <typename V, typename S, typename MV, typename I, bool D16, int SPW>
+// The SELL-128/DIA image for the persistent loop's SpMV (round 5; DIA = true):
+// a wave's SPW SELL-64 slices are SPW / 2 DIA slices of the same rows, lane l
+// owning rows 2l, 2l + 1 of each; one 16-B value load per slot column and no
+// index stream, against a 2-B delta and an 8-B value load per row.
+template <typename MV>
+struct CgpDia {
+  const int64_t *sptr;
+  const int *width;
+  const int *off;
+  const uint64_t *mask;
+  const MV *val;
+  int64_t nslices;
+};
+
+template <typename V, typename S, typename MV, typename I, bool D16, int SPW, bool DIA = false>
 __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
     const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
     int64_t nslices, int64_t n, CgpBufs<V> B, double *hist, unsigned *words, Ctrl *ctrl, int max_steps,
-    unsigned long long *tbuf, int fault_step) {
+    unsigned long long *tbuf, int fault_step, CgpDia<MV> Dg) {
+  static_assert(!DIA || SPW % 2 == 0, "a DIA slice is two SELL-64 slices");
   if (halted(ctrl, 0)) return;
   // optional phase trace (tbuf != null, KRY_CGP_TRACE): thread 0's wall-clock
   // split of an iteration into SpMV / all-gather #1 wait / r update / store
@@ -809,54 +824,101 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     // that r_t(j) + omega p_{t-1}(j), the owner's operations
     const V *Pprev = t == 1 ? B.Pin : ((t & 1) ? B.Pb : B.Pa);  // holds p_{t-1} (t >= 1)
     double pap = 0.0;
+    // x of global row c for the SpMV: this block's p_t from LDS, another
+    // block's formed as the owner does (r_t(c) + omega p_{t-1}(c))
+    auto xval = [&](int64_t c) -> V {
+      const int64_t lc = c - row0;
+      if ((uint64_t)lc < (uint64_t)ROWS) return ps[lc];
+      if (t == 0) return B.Pin[c];
+      const V rj = ld_wt(B.Rs + c), pj = ld_wt(Pprev + c);
+      const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
+      return rj + tt;
+    };
+    if constexpr (DIA) {
+      constexpr int UNRD = SPW == 4 ? 2 : 3;  // slot columns per round (more spill at 128 VGPRs)
+#pragma unroll 1
+      for (int q = 0; q < SPW / 2; ++q) {
+        const int64_t sd = s0 / 2 + q;
+        const int la = wid * SPW * 64 + q * 128 + 2 * lane;  // local row of the lane's first row
+        const int64_t ra = row0 + la;
+        V acc0 = V(0), acc1 = V(0);
+        if (sd < Dg.nslices) {
+          const int w = Dg.width[sd];
+          const int64_t base = Dg.sptr[sd], cb = base / kDiaSlice;
+          const MV *cv = Dg.val + base + 2 * lane;
+          for (int j0 = 0; j0 < w; j0 += UNRD) {
+            int off[UNRD];
+            bool on0[UNRD], on1[UNRD];
+            MV a[UNRD][2];
 #pragma unroll
-    for (int i = 0; i < SPW; ++i) {
-      const int64_t sl = s0 + i;
-      V acc = V(0);
-      if (sl < nslices) {
-        const int w = swidth[sl];
-        const int64_t base = sptr[sl];
-        for (int j0 = 0; j0 < w; j0 += UNR) {
-          I col[UNR];
-          V a[UNR];
-#pragma unroll
-          for (int u = 0; u < UNR; ++u) {
-            const bool in = j0 + u < w;
-            if constexpr (D16) {
-              const unsigned d = in ? (unsigned)sdelta[base + (int64_t)(j0 + u) * 64 + lane] : 0xFFFFu;
-              const int b = in ? scbase[(base >> 6) + j0 + u] : 0;
-              col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
-            } else {
-              col[u] = in ? sidx[base + (int64_t)(j0 + u) * 64 + lane] : I(-1);
+            for (int u = 0; u < UNRD; ++u) {
+              const bool in = j0 + u < w;
+              off[u] = in ? Dg.off[cb + j0 + u] : 0;
+              const uint64_t m0 = in ? Dg.mask[2 * (cb + j0 + u)] : 0, m1 = in ? Dg.mask[2 * (cb + j0 + u) + 1] : 0;
+              on0[u] = ((m0 >> lane) & 1u) != 0;
+              on1[u] = ((m1 >> lane) & 1u) != 0;
+              if (in) {
+                pload<MV>(cv + (int64_t)(j0 + u) * kDiaSlice, a[u]);
+              } else {
+                a[u][0] = MV(0);
+                a[u][1] = MV(0);
+              }
             }
-            a[u] = in ? (V)sval[base + (int64_t)(j0 + u) * 64 + lane] : V(0);
+#pragma unroll
+            for (int u = 0; u < UNRD; ++u) {  // ascending offsets: csr_matvec's order for sorted rows
+              if (on0[u]) {
+                const V pr = (V)a[u][0] * xval(ra + off[u]);
+                acc0 = acc0 + pr;
+              }
+              if (on1[u]) {
+                const V pr = (V)a[u][1] * xval(ra + 1 + off[u]);
+                acc1 = acc1 + pr;
+              }
+            }
           }
-          V xv[UNR];
-#pragma unroll
-          for (int u = 0; u < UNR; ++u) {
-            const int64_t lc = (int64_t)col[u] - row0;
-            if ((uint64_t)lc < (uint64_t)ROWS) {
-              xv[u] = ps[lc];
-            } else if (col[u] < 0) {
-              xv[u] = V(0);
-            } else if (t == 0) {
-              xv[u] = B.Pin[col[u]];
-            } else {
-              const V rj = ld_wt(B.Rs + col[u]), pj = ld_wt(Pprev + col[u]);
-              const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
-              xv[u] = rj + tt;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < UNR; ++u)
-            if (col[u] >= 0) {
-              const V pr = a[u] * xv[u];
-              acc = acc + pr;
-            }
         }
-        if (sl * 64 + lane < n) pap += dterm((double)ps[lr0 + 64 * i], (double)acc);
+        aps[la] = acc0;
+        aps[la + 1] = acc1;
+        if (ra < n) pap += dterm((double)ps[la], (double)acc0);
+        if (ra + 1 < n) pap += dterm((double)ps[la + 1], (double)acc1);
       }
-      aps[i * kCgpBlock + tid] = acc;
+    } else {
+#pragma unroll
+      for (int i = 0; i < SPW; ++i) {
+        const int64_t sl = s0 + i;
+        V acc = V(0);
+        if (sl < nslices) {
+          const int w = swidth[sl];
+          const int64_t base = sptr[sl];
+          for (int j0 = 0; j0 < w; j0 += UNR) {
+            I col[UNR];
+            V a[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+              const bool in = j0 + u < w;
+              if constexpr (D16) {
+                const unsigned d = in ? (unsigned)sdelta[base + (int64_t)(j0 + u) * 64 + lane] : 0xFFFFu;
+                const int b = in ? scbase[(base >> 6) + j0 + u] : 0;
+                col[u] = d != 0xFFFFu ? I(b + (int)d) : I(-1);
+              } else {
+                col[u] = in ? sidx[base + (int64_t)(j0 + u) * 64 + lane] : I(-1);
+              }
+              a[u] = in ? (V)sval[base + (int64_t)(j0 + u) * 64 + lane] : V(0);
+            }
+            V xv[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) xv[u] = col[u] < 0 ? V(0) : xval(col[u]);
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+              if (col[u] >= 0) {
+                const V pr = a[u] * xv[u];
+                acc = acc + pr;
+              }
+          }
+          if (sl * 64 + lane < n) pap += dterm((double)ps[lr0 + 64 * i], (double)acc);
+        }
+        aps[lr0 + 64 * i] = acc;  // by local row (the DIA form's layout)
+      }
     }
     if (faulty && t == fault_step) return;
     if (!exchange(pap, t, 0, false)) return;
@@ -867,7 +929,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
       const int64_t row = (s0 + i) * 64 + lane;
-      const V t2 = a * aps[i * kCgpBlock + tid];
+      const V t2 = a * aps[lr0 + 64 * i];
       r[i] = r[i] - t2;  // cg.py:200
       if (s0 + i < nslices && row < n) {
         st_wt(B.Rs + row, r[i]);
@@ -978,7 +1040,12 @@ void cg_start_impl(kry_cg *s) {
 template <typename V, typename S, typename MV, typename I, bool D16>
 bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   const kry_csr *A = s->A;
-  auto kern_for = [](int spw) {
+  // the SpMV over the DIA image when there is one and a wave's slices pair
+  // up (SPW even); KRY_CGP_DIA=0: the SELL image as before round 5
+  const bool dia_ok = A->dia && !env_off("KRY_CGP_DIA");
+  auto kern_for = [&](int spw) {
+    if (dia_ok && spw == 2) return cg_persist_kernel<V, S, MV, I, D16, 2, true>;
+    if (dia_ok && spw == 4) return cg_persist_kernel<V, S, MV, I, D16, 4, true>;
     switch (spw) {
       case 1: return cg_persist_kernel<V, S, MV, I, D16, 1>;
       case 2: return cg_persist_kernel<V, S, MV, I, D16, 2>;
@@ -1039,8 +1106,11 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   double *hist = s->hist;
   unsigned *words = s->cgp_words;
   Ctrl *ctrl = s->ctrl;
-  void *args[] = {&a_sptr, &a_swidth, &a_sidx, &a_sdelta, &a_scbase, &a_sval, &nsl, &n,
-                  &bufs,   &hist,     &words,  &ctrl,     &max_steps, &tb,    &fault_step};
+  CgpDia<MV> dg{static_cast<const int64_t *>(A->dia_sptr), static_cast<const int *>(A->dia_width),
+                static_cast<const int *>(A->dia_off), static_cast<const uint64_t *>(A->dia_mask),
+                static_cast<const MV *>(A->dia_val), A->dia ? A->dia_nslices : 0};
+  void *args[] = {&a_sptr, &a_swidth, &a_sidx, &a_sdelta, &a_scbase, &a_sval, &nsl,        &n,
+                  &bufs,   &hist,     &words,  &ctrl,     &max_steps, &tb,    &fault_step, &dg};
   hipError_t le;
   {
     // A plain launch, as for cg_upd_kernel: residency is the occupancy check

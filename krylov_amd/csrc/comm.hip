@@ -90,9 +90,25 @@ int kry_comm_destroy(kry_comm *c) {
   if (!c) return KRY_OK;
   (void)hipSetDevice(c->ctx->device);
   (void)hipStreamSynchronize(c->ctx->stream);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->comm && !c->aborted) (void)ncclCommDestroy(c->comm);
   dev_free(c->dbuf);
   delete c;
+  KRY_API_END
+}
+
+// Abort the communicator (ncclCommAbort), callable from another thread while
+// a collective on it is pending: the pending and every later collective
+// fails (the solvers then stop with KRY_ECOMM) instead of waiting for a rank
+// that will not come. The single-process multi-GPU driver calls it on every
+// device's communicator when one device's thread fails.
+int kry_comm_abort(kry_comm *c) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(c, KRY_EINVAL, "null communicator");
+  if (c->comm && !c->aborted) {
+    c->aborted = true;
+    (void)hipSetDevice(c->ctx->device);
+    KRY_NCCL(ncclCommAbort(c->comm));
+  }
   KRY_API_END
 }
 
@@ -101,6 +117,7 @@ int kry_comm_destroy(kry_comm *c) {
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count) {
   KRY_API_BEGIN
   KRY_REQUIRE(c && host && count >= 0, KRY_EINVAL, "bad argument");
+  KRY_REQUIRE(!c->aborted, KRY_ECOMM, "the communicator was aborted");
   if (count == 0) return KRY_OK;
   KRY_HIP(hipSetDevice(c->ctx->device));
   hipStream_t st = c->ctx->stream;

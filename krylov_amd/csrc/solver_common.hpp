@@ -14,6 +14,7 @@ struct kry_comm {
   int nranks = 1, rank = 0;
   double *dbuf = nullptr;  // scratch for host allreduces
   int dbuf_len = 0;
+  bool aborted = false;  // kry_comm_abort ran: destroy skips ncclCommDestroy
 };
 
 namespace kry {

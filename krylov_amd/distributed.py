@@ -113,6 +113,13 @@ class ShardComm:
         check(lib.kry_comm_allreduce(self.handle, _lib.dptr(v), v.size))
         return v
 
+    def abort(self):
+        """Abort the communicator (kry_comm_abort): a collective pending on it
+        in another thread, and every later one, fails with KRY_ECOMM instead
+        of waiting for a rank that will not come. ``close()`` still releases
+        it."""
+        check(lib.kry_comm_abort(self.handle))
+
     def close(self):
         self._fin()
 

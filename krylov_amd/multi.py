@@ -24,7 +24,10 @@ the residual norms per iteration, xk gathered into X[:, 8g:8g+8]".
 ``A``: a scipy.sparse matrix or dense array (uploaded once per device, the
 uploads in parallel threads), or a list of ``CsrOperator``, one per device
 in ``devices`` order. Callbacks and preconditioners are not taken on this
-path (NotImplementedError), as on the multi-process sharded path.
+path (NotImplementedError), as on the multi-process sharded path. If one
+device's thread fails, every communicator is aborted (kry_comm_abort), so
+the others stop at their next collective instead of waiting for it, and
+that first error is raised.
 """
 import threading
 
@@ -104,11 +107,24 @@ def solve(method, A, B, devices, x0=None, **kw):
     out = [None] * D
     errs = [None] * D
 
+    abort_lock = threading.Lock()
+    aborted = []
+
     def run(g):
         try:
             out[g] = fn(ops[g], local(B2, g), comms[g], x0=None if X0 is None else local(X0, g), kcs=kcs, **kw)
         except BaseException as e:  # noqa: BLE001 - re-raised below
             errs[g] = e
+            # the other devices may be waiting in a collective this one will
+            # never join: abort every communicator so they fail too
+            with abort_lock:
+                if not aborted:
+                    aborted.append(g)
+                    for c in comms:
+                        try:
+                            c.abort()
+                        except RuntimeError:
+                            pass
 
     th = [threading.Thread(target=run, args=(g,), name=f"krylov_amd-dev{d}") for g, d in enumerate(devices)]
     for t in th:
@@ -117,9 +133,8 @@ def solve(method, A, B, devices, x0=None, **kw):
         t.join()
     for c in comms:
         c.close()
-    bad = [e for e in errs if e is not None]
-    if bad:
-        raise bad[0]
+    if aborted:  # the device that failed first, not the peers it stopped
+        raise errs[aborted[0]]
     info = out[0][1]
     xk = np.concatenate([np.asarray(out[g][1].xk).reshape(B2.shape[0], -1)[:, :kcs[g]] for g in range(D)], axis=1)
     xk = xk.reshape(B.shape)

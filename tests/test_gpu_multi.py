@@ -76,3 +76,24 @@ def test_devices_argument_errors():
     ops = [krylov_amd.CsrOperator(P, device=0)]
     _, info = krylov_amd.cg(ops, B, devices=[0], tol=1e-8)
     assert info.success
+
+
+def test_devices_abort_on_failure_and_aborted_comm_refuses():
+    """A device thread that fails aborts every communicator (kry_comm_abort),
+    so no other device waits forever in a collective it will not get; the
+    first error is raised. An aborted communicator refuses later collectives
+    with KRY_ECOMM (RuntimeError) and still closes."""
+    import krylov_amd
+    from krylov_amd import distributed, problems
+
+    P = problems.poisson2d(32)
+    B = np.ones((P.shape[0], 2))
+    with pytest.raises(TypeError):
+        krylov_amd.cg(P, B, devices=[0], maxiter="many")
+    (comm,) = distributed.ShardComm.all_devices([0])
+    comm.abort()
+    with pytest.raises(RuntimeError):
+        comm.allreduce(np.ones(3))
+    comm.close()
+    _, info = krylov_amd.cg(P, B, devices=[0], tol=1e-8)  # a fresh communicator works
+    assert info.success
