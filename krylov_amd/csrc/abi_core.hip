@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <atomic>
 #include <climits>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -269,25 +270,65 @@ bool env_off(const char *name) {
   return e && atoi(e) == 0;
 }
 
+// Ranges of host memory this library has registered for in-flight copies,
+// with their users: threads copying the same array (the devices=[...] driver
+// uploads one CSR to every device in parallel) share one registration, and a
+// range overlapping a registered one waits until that is released, so no
+// thread's DMA ever runs on pages another thread has just unregistered.
+namespace {
+struct HostReg {
+  size_t end;
+  int users;
+};
+std::mutex host_reg_mu;
+std::condition_variable host_reg_cv;
+std::map<uintptr_t, HostReg> host_regs;
+
+bool overlaps_other(uintptr_t a, uintptr_t e) {
+  for (const auto &kv : host_regs)
+    if (kv.first < e && a < kv.second.end && !(kv.first == a && kv.second.end == e)) return true;
+  return false;
+}
+}  // namespace
+
 void host_xfer(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
   constexpr size_t kPinMin = size_t(4) << 20;
   static const bool pin = !env_off("KRY_HOST_PIN");
   void *host = kind == hipMemcpyHostToDevice ? const_cast<void *>(src) : dst;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(host), e = a + bytes;
   bool reg = false;
   if (pin && bytes >= kPinMin) {
-    if (hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess)
+    std::unique_lock<std::mutex> lk(host_reg_mu);
+    host_reg_cv.wait(lk, [&] { return !overlaps_other(a, e); });
+    auto it = host_regs.find(a);
+    if (it != host_regs.end() && it->second.end == e) {
+      ++it->second.users;
       reg = true;
-    else
-      (void)hipGetLastError();  // already registered, or not registrable: pageable
+    } else if (hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess) {
+      host_regs[a] = HostReg{e, 1};
+      reg = true;
+    } else {
+      (void)hipGetLastError();  // locked by its owner (e.g. pinned memory), or not lockable: pageable
+    }
   }
+  auto release = [&] {
+    if (!reg) return;
+    std::lock_guard<std::mutex> lk(host_reg_mu);
+    auto it = host_regs.find(a);
+    if (--it->second.users == 0) {
+      (void)hipHostUnregister(host);
+      host_regs.erase(it);
+      host_reg_cv.notify_all();
+    }
+  };
   try {
     KRY_HIP(hipMemcpyAsync(dst, src, bytes, kind, st));
     KRY_HIP(hipStreamSynchronize(st));
   } catch (...) {
-    if (reg) (void)hipHostUnregister(host);
+    release();
     throw;
   }
-  if (reg) KRY_HIP(hipHostUnregister(host));
+  release();
 }
 
 void store_out(const kry_csr *A, const void *src, void *host, int k, size_t esize, hipStream_t st) {

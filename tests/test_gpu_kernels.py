@@ -512,10 +512,10 @@ def test_host_transfers_pinned_in_place_and_fallback():
     """Large host <-> device copies go through the caller's pages pinned in
     place (host_xfer: hipHostRegister for the copy, then unregistered).
     Round trips are bitwise for a pageable array, a view that starts inside
-    a page, an array that is already page-locked (torch pinned memory:
+    a page, an array that is already page-locked (hipHostMalloc:
     registration fails, the plain copy runs), and a read-only array; the
     same host array can be copied again afterwards (it was unregistered)."""
-    import torch
+    import ctypes
 
     import krylov_amd
     from krylov_amd.device import DeviceVector
@@ -524,7 +524,11 @@ def test_host_transfers_pinned_in_place_and_fallback():
     n = 1_000_003  # 8 MB: above the 4 MB pinning threshold
     rng = np.random.default_rng(5)
     base = rng.standard_normal(n + 3)
-    pinned = torch.empty(n, dtype=torch.float64, pin_memory=True).numpy()
+    # page-locked host memory from the HIP runtime the library itself uses
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the soname the library links (not torch's bundled copy)
+    hp = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(hp), ctypes.c_size_t(n * 8), ctypes.c_uint(0)) == 0
+    pinned = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_double)), shape=(n,))
     pinned[:] = rng.standard_normal(n)
     ro = rng.standard_normal(n)
     ro.setflags(write=False)
@@ -538,3 +542,41 @@ def test_host_transfers_pinned_in_place_and_fallback():
         back = np.full((n, 1), np.nan)
         v.to_host(back)
         np.testing.assert_array_equal(back.view(np.uint64), out.view(np.uint64))
+    del pinned
+    hip.hipHostFree(hp)
+
+
+def test_host_transfers_concurrent_same_and_overlapping_arrays():
+    """Threads copying the same host array (the devices=[...] driver uploads
+    one CSR to every device at once) share one page-lock; a range overlapping
+    one in flight waits for its release. Four contexts on device 0, each
+    driven by its own thread, upload and download the same array and two
+    overlapping views of it, several times: every round trip is bitwise."""
+    import threading
+
+    from krylov_amd.device import Context, DeviceVector
+
+    n = 2_000_000  # 16 MB
+    src = np.random.default_rng(9).standard_normal(n + 8)
+    views = [src[:n], src[:n], src[4:n + 4], src[8:n + 8]]
+    errs = []
+
+    def work(t):
+        try:
+            ctx = Context(0)
+            for _ in range(5):
+                v = DeviceVector(ctx, n, 1, np.float64)
+                v.upload(views[t].reshape(n, 1))
+                out = np.empty((n, 1))
+                v.to_host(out)
+                assert np.array_equal(out[:, 0].view(np.uint64), views[t].view(np.uint64))
+                v.close()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
