@@ -720,6 +720,21 @@ __device__ __forceinline__ V ld_wt(const V *p) {
         __hip_atomic_load(reinterpret_cast<const unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// &base[idx] as a uniform 64-bit base plus a 32-bit byte offset (the
+// persistent loop's n <= 1 M rows): the store/load then takes the base in
+// SGPRs and one VGPR of offset, where a 64-bit per-lane address costs two
+// VGPRs per row and was spilled and reloaded (a reload's vmcnt wait then
+// serialised the write-through stores behind it)
+template <typename T>
+__device__ __forceinline__ T *at32(T *base, int64_t idx) {
+  return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (size_t)((unsigned)idx * (unsigned)sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ const T *at32(const T *base, int64_t idx) {
+  return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) +
+                                     (size_t)((unsigned)idx * (unsigned)sizeof(T)));
+}
+
 template <typename V>
 struct CgpBufs {
   const V *Yin, *Rin, *Pin;  // chunk-start state (never written)
@@ -740,27 +755,43 @@ struct CgpDia {
   const uint64_t *mask;
   const MV *val;
   int64_t nslices;
+  int span;  // max |offset| over the image (WR > 0: the LDS halo's rows per side)
 };
 
-template <typename V, typename S, typename MV, typename I, bool D16, int SPW, bool DIA = false>
+// The register-resident DIA form (WR > 0): the wave's values stay in
+// registers for the whole chunk (a 5-point stencil: 2 x 5 x 2 values per lane
+// at SPW = 4, 40 VGPRs for fp64) instead of being re-read every iteration,
+// and the SpMV's x comes from LDS alone: the block's own p_t rows and, formed
+// at the top of every iteration by one coalesced pass of the whole block, the
+// span rows on either side (a halo of at most kCgpHalo rows per side). A
+// matrix with wider slices or a larger span takes the streamed form (WR = 0).
+constexpr int kCgpWr = 5;
+constexpr int kCgpHalo = 3072;
+
+template <typename V, typename S, typename MV, typename I, bool D16, int SPW, bool DIA = false, int WR = 0>
 __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t *__restrict__ sptr, const int *__restrict__ swidth, const I *__restrict__ sidx,
     const uint16_t *__restrict__ sdelta, const int *__restrict__ scbase, const MV *__restrict__ sval,
     int64_t nslices, int64_t n, CgpBufs<V> B, double *hist, unsigned *words, Ctrl *ctrl, int max_steps,
     unsigned long long *tbuf, int fault_step, CgpDia<MV> Dg) {
   static_assert(!DIA || SPW % 2 == 0, "a DIA slice is two SELL-64 slices");
+  static_assert(WR == 0 || DIA, "register-resident values are the DIA form's");
   if (halted(ctrl, 0)) return;
   // optional phase trace (tbuf != null, KRY_CGP_TRACE): thread 0's wall-clock
   // split of an iteration into SpMV / all-gather #1 wait / r update / store
   // drain / all-gather #2 wait / y and p update
-  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+  // (in LDS: per-lane registers for one thread's counters cost 14 VGPRs
+  // across the whole loop)
+  __shared__ unsigned long long tacc[7];  // 6 phases, then the last mark
   auto tmark = [&](int k) {
     if (tbuf && threadIdx.x == 0) {
       const unsigned long long now = wall_clock64();
-      if (k >= 0) tacc[k] += now - tlast;
-      tlast = now;
+      if (k >= 0) tacc[k] += now - tacc[6];
+      tacc[6] = now;
     }
   };
+  if (tbuf && threadIdx.x == 0)
+    for (int k = 0; k < 7; ++k) tacc[k] = 0;
   constexpr int UNR = 5;  // a 5-point row in one round of loads; 8 spills at 128 VGPRs
   constexpr int ROWS = SPW * kCgpBlock;  // rows of this block: [row0, row0 + ROWS)
   __shared__ double wsum[kCgpWaves];
@@ -769,9 +800,11 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   // LDS: y and Ap of the block's rows (r stays in registers) and p_t of the
   // block's rows by local row, so that in-block columns (most of a banded
   // matrix's) are gathered from LDS; SPW = 4 doubles is 96 KB of 160
-  __shared__ V ys[ROWS], aps[ROWS], ps[ROWS];
+  // WR > 0: ps holds the halo too, own row lr at ps[po + lr] (po = span)
+  __shared__ V ys[ROWS], aps[ROWS], ps[ROWS + (WR > 0 ? 2 * kCgpHalo : 0)];
+  const int po = WR > 0 ? Dg.span : 0;
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(words + 16);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = gridDim.x;
   // fault injection (tests): the last block stops publishing at iteration
   // fault_step, as a block that never became resident would
@@ -785,9 +818,40 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
     const bool own = s0 + i < nslices && row < n;
-    ys[i * kCgpBlock + tid] = own ? B.Yin[row] : V(0);
-    r[i] = own ? B.Rin[row] : V(0);
-    ps[lr0 + 64 * i] = own ? B.Pin[row] : V(0);
+    ys[i * kCgpBlock + tid] = own ? *at32(B.Yin, row) : V(0);
+    r[i] = own ? *at32(B.Rin, row) : V(0);
+    ps[po + lr0 + 64 * i] = own ? *at32(B.Pin, row) : V(0);
+  }
+  // WR > 0: the wave's DIA values, slot offsets and lane masks, loaded once
+  // per chunk: pair q's slot column u in ar[q][u] (holes and columns past the
+  // slice's width are 0), its offset in aoff[q][u] (wave-uniform), row 2l + h
+  // present in bit 2 (q WR + u) + h of abits
+  constexpr int NQ = WR > 0 ? SPW / 2 : 1, NU = WR > 0 ? WR : 1;
+  MV ar[NQ][NU][2];
+  int aoff[NQ][NU];
+  unsigned abits = 0;
+  if constexpr (WR > 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int64_t sd = s0 / 2 + q;
+      const int w = sd < Dg.nslices ? Dg.width[sd] : 0;
+      const int64_t base = w > 0 ? Dg.sptr[sd] : 0, cb = base / kDiaSlice;
+      const MV *cv = Dg.val + base + 2 * lane;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const bool in = u < w;
+        aoff[q][u] = in ? Dg.off[cb + u] : 0;
+        const uint64_t m0 = in ? Dg.mask[2 * (cb + u)] : 0, m1 = in ? Dg.mask[2 * (cb + u) + 1] : 0;
+        abits |= (unsigned)((m0 >> lane) & 1u) << (2 * (q * NU + u));
+        abits |= (unsigned)((m1 >> lane) & 1u) << (2 * (q * NU + u) + 1);
+        if (in) {
+          pload<MV>(cv + (int64_t)u * kDiaSlice, ar[q][u]);
+        } else {
+          ar[q][u][0] = MV(0);
+          ar[q][u][1] = MV(0);
+        }
+      }
+    }
   }
   S rho = (S)B.Sin[S_RHO];
   const double crit = B.Sin[S_CRIT];
@@ -828,13 +892,56 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     // block's formed as the owner does (r_t(c) + omega p_{t-1}(c))
     auto xval = [&](int64_t c) -> V {
       const int64_t lc = c - row0;
-      if ((uint64_t)lc < (uint64_t)ROWS) return ps[lc];
-      if (t == 0) return B.Pin[c];
-      const V rj = ld_wt(B.Rs + c), pj = ld_wt(Pprev + c);
+      if ((uint64_t)lc < (uint64_t)ROWS) return ps[po + lc];
+      if (t == 0) return *at32(B.Pin, c);
+      const V rj = ld_wt(at32(B.Rs, c)), pj = ld_wt(at32(Pprev, c));
       const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
       return rj + tt;
     };
-    if constexpr (DIA) {
+    if constexpr (WR > 0) {
+      // the halo: rows [row0 - span, row0) and [row0 + ROWS, row0 + ROWS +
+      // span) of p_t, formed as xval forms them
+      for (int h = tid; h < 2 * po; h += kCgpBlock) {
+        const int64_t c = h < po ? row0 - po + h : row0 + ROWS + (h - po);
+        if (c < 0 || c >= n) continue;
+        V v;
+        if (t == 0) {
+          v = *at32(B.Pin, c);
+        } else {
+          const V rj = ld_wt(at32(B.Rs, c)), pj = ld_wt(at32(Pprev, c));
+          const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
+          v = rj + tt;
+        }
+        ps[h < po ? h : po + ROWS + (h - po)] = v;
+      }
+      __syncthreads();
+      // opaque per iteration, so that the 2 NQ NU LDS addresses and lane
+      // masks are formed here and not held in registers across the loop
+      int lb = po + wid * SPW * 64 + 2 * lane;
+      unsigned ab = abits;
+      asm volatile("" : "+v"(lb), "+v"(ab));
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int la = wid * SPW * 64 + q * 128 + 2 * lane;  // local row of the lane's first row
+        const int64_t ra = row0 + la;
+        V acc0 = V(0), acc1 = V(0);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {  // ascending offsets, as the streamed form below
+          if ((ab >> (2 * (q * NU + u))) & 1u) {
+            const V pr = (V)ar[q][u][0] * ps[lb + q * 128 + aoff[q][u]];
+            acc0 = acc0 + pr;
+          }
+          if ((ab >> (2 * (q * NU + u) + 1)) & 1u) {
+            const V pr = (V)ar[q][u][1] * ps[lb + q * 128 + 1 + aoff[q][u]];
+            acc1 = acc1 + pr;
+          }
+        }
+        aps[la] = acc0;
+        aps[la + 1] = acc1;
+        if (ra < n) pap += dterm((double)ps[po + la], (double)acc0);
+        if (ra + 1 < n) pap += dterm((double)ps[po + la + 1], (double)acc1);
+      }
+    } else if constexpr (DIA) {
       constexpr int UNRD = SPW == 4 ? 2 : 3;  // slot columns per round (more spill at 128 VGPRs)
 #pragma unroll 1
       for (int q = 0; q < SPW / 2; ++q) {
@@ -879,8 +986,8 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
         }
         aps[la] = acc0;
         aps[la + 1] = acc1;
-        if (ra < n) pap += dterm((double)ps[la], (double)acc0);
-        if (ra + 1 < n) pap += dterm((double)ps[la + 1], (double)acc1);
+        if (ra < n) pap += dterm((double)ps[po + la], (double)acc0);
+        if (ra + 1 < n) pap += dterm((double)ps[po + la + 1], (double)acc1);
       }
     } else {
 #pragma unroll
@@ -915,7 +1022,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
                 acc = acc + pr;
               }
           }
-          if (sl * 64 + lane < n) pap += dterm((double)ps[lr0 + 64 * i], (double)acc);
+          if (sl * 64 + lane < n) pap += dterm((double)ps[po + lr0 + 64 * i], (double)acc);
         }
         aps[lr0 + 64 * i] = acc;  // by local row (the DIA form's layout)
       }
@@ -926,13 +1033,17 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     alpha = rho / safe<S>(pAp);  // cg.py:183-185
     const V a = (V)(double)alpha;
     double rr = 0.0;
+    // the rows' store offsets are formed here each iteration from an opaque
+    // lane index: hoisted out of the loop they were spilled (see at32)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
-      const int64_t row = (s0 + i) * 64 + lane;
+      const int64_t row = (s0 + i) * 64 + ln;
       const V t2 = a * aps[lr0 + 64 * i];
       r[i] = r[i] - t2;  // cg.py:200
       if (s0 + i < nslices && row < n) {
-        st_wt(B.Rs + row, r[i]);
+        st_wt(at32(B.Rs, row), r[i]);
         rr += dterm((double)r[i], (double)r[i]);
       }
     }
@@ -941,16 +1052,17 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const S om = rrS / safe<S>(rho);
     const V omV = (V)(double)om;
     V *Pnext = (t & 1) ? B.Pb : B.Pa;  // p_{t+1}
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < SPW; ++i) {
-      const int64_t row = (s0 + i) * 64 + lane;
-      const V pv = ps[lr0 + 64 * i];
+      const int64_t row = (s0 + i) * 64 + ln;
+      const V pv = ps[po + lr0 + 64 * i];
       const V t1 = a * pv;
       ys[i * kCgpBlock + tid] = ys[i * kCgpBlock + tid] + t1;  // cg.py:196
       const V tt = omV * pv;
       const V pn = r[i] + tt;  // cg.py:178
-      ps[lr0 + 64 * i] = pn;  // every wave is past this iteration's SpMV (exchange barriers)
-      if (s0 + i < nslices && row < n) st_wt(Pnext + row, pn);
+      ps[po + lr0 + 64 * i] = pn;  // every wave is past this iteration's SpMV (exchange barriers)
+      if (s0 + i < nslices && row < n) st_wt(at32(Pnext, row), pn);
     }
     tmark(5);
     const S nrm = sqrt(rrS);
@@ -981,7 +1093,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
-    if (s0 + i < nslices && row < n) B.Yout[row] = ys[i * kCgpBlock + tid];
+    if (s0 + i < nslices && row < n) *at32(B.Yout, row) = ys[i * kCgpBlock + tid];
   }
 }
 
@@ -1037,13 +1149,37 @@ void cg_start_impl(kry_cg *s) {
 // iterations per chunk); CUs held by another stream or process can still keep
 // a block from becoming resident, which the bounded exchanges and the host's
 // rerun (kry_cg_run) cover.
+// The DIA image's largest |offset| (the register-resident form's halo),
+// read back once per operator; concurrent first callers compute the same value.
+static int dia_span_of(const kry_csr *A, hipStream_t st) {
+  int sp = __atomic_load_n(&A->dia_span, __ATOMIC_ACQUIRE);
+  if (sp >= 0) return sp;
+  const int64_t ncol = A->dia_nslots / kDiaSlice;
+  std::vector<int> off((size_t)ncol);
+  if (ncol > 0) {
+    KRY_HIP(hipMemcpyAsync(off.data(), A->dia_off, (size_t)ncol * 4, hipMemcpyDeviceToHost, st));
+    KRY_HIP(hipStreamSynchronize(st));
+  }
+  sp = 0;
+  for (int o : off) sp = std::max(sp, o < 0 ? -o : o);
+  __atomic_store_n(const_cast<int *>(&A->dia_span), sp, __ATOMIC_RELEASE);
+  return sp;
+}
+
 template <typename V, typename S, typename MV, typename I, bool D16>
 bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   const kry_csr *A = s->A;
   // the SpMV over the DIA image when there is one and a wave's slices pair
   // up (SPW even); KRY_CGP_DIA=0: the SELL image as before round 5
   const bool dia_ok = A->dia && !env_off("KRY_CGP_DIA");
+  // its values held in registers for the chunk and x from LDS when every
+  // slice is at most kCgpWr slot columns wide and the offsets span at most
+  // kCgpHalo rows; KRY_CGP_WR=0: the streamed form
+  const bool wr_ok = dia_ok && A->dia_max_width <= kCgpWr && !env_off("KRY_CGP_WR") &&
+                     dia_span_of(A, s->ctx->stream) <= kCgpHalo;
   auto kern_for = [&](int spw) {
+    if (wr_ok && spw == 2) return cg_persist_kernel<V, S, MV, I, D16, 2, true, kCgpWr>;
+    if (wr_ok && spw == 4) return cg_persist_kernel<V, S, MV, I, D16, 4, true, kCgpWr>;
     if (dia_ok && spw == 2) return cg_persist_kernel<V, S, MV, I, D16, 2, true>;
     if (dia_ok && spw == 4) return cg_persist_kernel<V, S, MV, I, D16, 4, true>;
     switch (spw) {
@@ -1108,7 +1244,7 @@ bool cgp_launch_t(kry_cg *s, int max_steps, bool decide_only) {
   Ctrl *ctrl = s->ctrl;
   CgpDia<MV> dg{static_cast<const int64_t *>(A->dia_sptr), static_cast<const int *>(A->dia_width),
                 static_cast<const int *>(A->dia_off), static_cast<const uint64_t *>(A->dia_mask),
-                static_cast<const MV *>(A->dia_val), A->dia ? A->dia_nslices : 0};
+                static_cast<const MV *>(A->dia_val), A->dia ? A->dia_nslices : 0, wr_ok ? A->dia_span : 0};
   void *args[] = {&a_sptr, &a_swidth, &a_sidx, &a_sdelta, &a_scbase, &a_sval, &nsl,        &n,
                   &bufs,   &hist,     &words,  &ctrl,     &max_steps, &tb,    &fault_step, &dg};
   hipError_t le;

@@ -74,6 +74,7 @@ struct kry_csr {
   int64_t dia_nslices = 0;
   int64_t dia_nslots = 0;
   int dia_max_width = 0;
+  int dia_span = -1;          // max |offset| over the image; -1 = not computed yet (cg.hip dia_span_of)
   void *dia_sptr = nullptr;   // int64, dia_nslices + 1 (slots; kDiaSlice per slot column)
   void *dia_width = nullptr;  // int32, dia_nslices
   void *dia_off = nullptr;    // int32, dia_nslots / kDiaSlice (+ kDiaPad)

@@ -378,21 +378,24 @@ def test_gmres_persistent_mgs_matches_pass_kernels(monkeypatch, k, ortho):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dia", ["1", "0"])
+@pytest.mark.parametrize("form", ["wr", "dia", "sell"])
 @pytest.mark.parametrize("m,dtype", [(30, np.float64), (300, np.float64), (600, np.float64), (1000, np.float64),
                                      (300, np.float32), (1000, np.float32)])
-def test_cg_persistent_matches_pass_kernels(monkeypatch, m, dtype, dia):
+def test_cg_persistent_matches_pass_kernels(monkeypatch, m, dtype, form):
     """The persistent small-n CG loop (one launch per chunk, two in-launch
     all-gathers per iteration, KRY_CG_PERSIST=2 makes it mandatory) against
     the launch-per-pass path (KRY_CG_PERSIST=0) and the oracle: same step
     count, histories to round-off (the dot products are summed in different
     fixed orders), same iterate. m = 30 is one partly filled block, m = 1000
     the largest size it takes (4 slices per wave), m = 600 two slices per
-    wave: with dia = 1 (the default) the SpMV of an even number of slices
-    per wave reads the DIA image, with 0 the compact SELL-64 image."""
+    wave: the SpMV of an even number of slices per wave reads the DIA image
+    with its values held in registers for the chunk ("wr", the default for a
+    5-point matrix), or re-read every iteration ("dia", KRY_CGP_WR=0), and
+    with KRY_CGP_DIA=0 the compact SELL-64 image ("sell")."""
     import krylov_amd
 
-    monkeypatch.setenv("KRY_CGP_DIA", dia)
+    monkeypatch.setenv("KRY_CGP_DIA", "0" if form == "sell" else "1")
+    monkeypatch.setenv("KRY_CGP_WR", "0" if form == "dia" else "1")
     from krylov_amd import problems
     from oracle import krylov_ref
 
