@@ -341,7 +341,19 @@ def run_cfg2(steps=200, warmup=10):
     r = run_cg_config(P, np.ones(P.shape[0]), steps, warmup)
     lay, n = r.pop("layout"), r["n"]
     t_it = r["us_per_it"] * 1e-6
-    if r["persistent_loop"]:
+    wr = (r["persistent_loop"] and lay["dia"] and os.environ.get("KRY_CGP_DIA", "1") != "0"
+          and os.environ.get("KRY_CGP_WR", "1") != "0")
+    if wr:
+        # register-resident DIA form (round 5): the values are loaded once per
+        # 256-iteration chunk; per iteration each block reads its halo (span =
+        # 1000 rows either side: r_t and p_{t-1}) and stores its r and p rows
+        spw = next(w for w in (1, 2, 4) if -(-lay["slices"] // (16 * w)) <= 256)
+        G, span = -(-lay["slices"] // (16 * spw)), 1000
+        b = lay["dia_slots"] * 8 / 256 + G * 2 * span * 2 * 8 + 2 * n * 8
+        form = ("dia_slots*8/256 (values once per chunk) + G*2*span*2*8 (halo: r_t, p_{t-1}) + 2*n*8 (r and p "
+                "stored); y, Ap, p and the values stay on chip")
+        kern = "cg_persist_kernel (DIA values in registers, x from an LDS halo; one launch per chunk)"
+    elif r["persistent_loop"]:
         slots, slices = lay["slots"], lay["slices"]
         b = slots * (8 + 2) + slots / 64 * 4 + slices * 12 + 3 * n * 8
         form = ("slots*(8+2) + slots/64*4 + slices*12 (compact SELL-64 image) + 3*n*8 (p read once, r and p "
@@ -355,8 +367,8 @@ def run_cfg2(steps=200, warmup=10):
     r["roofline"] = {"bound": "hbm", "achieved": b / t_it / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": b / t_it / 1e9 / HBM_PEAK_GBS, "kernel": kern, "bytes_per_iteration": b,
                      "bytes_formula": form, "ms_per_iteration": 1e3 * t_it,
-                     "note": "latency-bound: two grid-wide exchanges per iteration; PMC 74.8 MB per iteration "
-                             "(profiles/r01_pmc_cfg2.json)"}
+                     "note": "latency-bound: two grid-wide exchanges and one halo exchange per iteration "
+                             "(profiles/r05_cgp_wr_ab.txt phase trace)"}
     return r
 
 

@@ -67,9 +67,9 @@ def main():
                                                   "kry::EpiLanczos")["hbm_bytes_corrected"], "r04_pmc_cfg5.json"),
                    "update": entry(CFG5, c5["kernels"]["void "]["hbm_bytes_corrected"], "r04_pmc_cfg5.json",
                                    "mr_upd_kernel (its name is truncated to 'void ' in the summary)")}
-    c2 = load("r01_pmc_cfg2.json")
+    c2 = load("r05_pmc_cfg2_wr.json")
     idx["cfg2"] = {"iteration": entry(CFG2, c2["read_bytes_per_iteration"] + c2["write_bytes_per_iteration"],
-                                      "r01_pmc_cfg2.json", "per iteration of the persistent loop")}
+                                      "r05_pmc_cfg2_wr.json", "per iteration of the persistent loop")}
     extra = os.path.join(P, "r05_traffic_extra.json")  # newer passes override the ones above
     if os.path.exists(extra):
         with open(extra) as f:
