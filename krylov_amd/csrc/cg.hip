@@ -900,19 +900,22 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     };
     if constexpr (WR > 0) {
       // the halo: rows [row0 - span, row0) and [row0 + ROWS, row0 + ROWS +
-      // span) of p_t, formed as xval forms them
+      // span) of p_t, formed as xval forms them, from the owners' r_t and
+      // the halo's own p_{t-1} (kept in LDS from the previous iteration: the
+      // same bits the owner holds), so p never crosses blocks in the loop
       for (int h = tid; h < 2 * po; h += kCgpBlock) {
         const int64_t c = h < po ? row0 - po + h : row0 + ROWS + (h - po);
         if (c < 0 || c >= n) continue;
+        const int hs = h < po ? h : po + ROWS + (h - po);
         V v;
         if (t == 0) {
           v = *at32(B.Pin, c);
         } else {
-          const V rj = ld_wt(at32(B.Rs, c)), pj = ld_wt(at32(Pprev, c));
-          const V tt = om_prev * pj;  // p = r + omega p (cg.py:178)
+          const V rj = ld_wt(at32(B.Rs, c));
+          const V tt = om_prev * ps[hs];  // p = r + omega p (cg.py:178)
           v = rj + tt;
         }
-        ps[h < po ? h : po + ROWS + (h - po)] = v;
+        ps[hs] = v;
       }
       __syncthreads();
       // opaque per iteration, so that the 2 NQ NU LDS addresses and lane
@@ -1062,7 +1065,8 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       const V tt = omV * pv;
       const V pn = r[i] + tt;  // cg.py:178
       ps[po + lr0 + 64 * i] = pn;  // every wave is past this iteration's SpMV (exchange barriers)
-      if (s0 + i < nslices && row < n) st_wt(at32(Pnext, row), pn);
+      // (WR: no peer reads p; the last p goes out once, after the loop)
+      if (WR == 0 && s0 + i < nslices && row < n) st_wt(at32(Pnext, row), pn);
     }
     tmark(5);
     const S nrm = sqrt(rrS);
@@ -1079,7 +1083,8 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   }
   if (tbuf && tid == 0)
     for (int k = 0; k < 6; ++k) tbuf[blockIdx.x * 8 + k] = tacc[k];
-  // a clean chunk: y to Yout (r and p are already in Rs and Pb), the scalar
+  // a clean chunk: y to Yout (r, and p but in the WR form, are already in
+  // Rs and Pa / Pb), the scalar
   // slots to Sout (the fused path's layout; S_RHO_OLD = the rho alpha used)
   if (blockIdx.x == 0 && tid == 0 && t > 0) {
     B.Sout[S_ALPHA] = (double)alpha;
@@ -1090,10 +1095,14 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     B.Sout[S_CRIT] = crit;
     B.Sout[S_TMP] = B.Sin[S_TMP];
   }
+  V *Plast = ((t - 1) & 1) ? B.Pb : B.Pa;  // p_t, where the iteration that formed it would have stored it
 #pragma unroll
   for (int i = 0; i < SPW; ++i) {
     const int64_t row = (s0 + i) * 64 + lane;
-    if (s0 + i < nslices && row < n) *at32(B.Yout, row) = ys[i * kCgpBlock + tid];
+    if (s0 + i < nslices && row < n) {
+      *at32(B.Yout, row) = ys[i * kCgpBlock + tid];
+      if (WR > 0 && t > 0) *at32(Plast, row) = ps[po + lr0 + 64 * i];
+    }
   }
 }
 

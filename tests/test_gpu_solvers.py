@@ -419,13 +419,16 @@ def test_cg_persistent_matches_pass_kernels(monkeypatch, m, dtype, form):
 
 
 @pytest.mark.gpu
-def test_cg_persistent_chunk_boundaries(monkeypatch):
+@pytest.mark.parametrize("m", [200, 600, 1000])
+def test_cg_persistent_chunk_boundaries(monkeypatch, m):
     """maxiter cut mid-chunk and a callback (one step per launch): the state
-    the persistent loop leaves (y, r, p, scalars) carries across launches."""
+    the persistent loop leaves (y, r, p, scalars) carries across launches.
+    m = 600 and 1000 take the register-resident DIA form, which stores p only
+    at the end of a launch."""
     import krylov_amd
     from krylov_amd import problems
 
-    R = problems.poisson2d(200)
+    R = problems.poisson2d(m)
     A = krylov_amd.CsrOperator(R)
     b = np.random.default_rng(4).standard_normal(R.shape[0])
     out = {}
