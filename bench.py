@@ -345,13 +345,15 @@ def run_cfg2(steps=200, warmup=10):
           and os.environ.get("KRY_CGP_WR", "1") != "0")
     if wr:
         # register-resident DIA form (round 5): the values are loaded once per
-        # 256-iteration chunk; per iteration each block reads its halo (span =
-        # 1000 rows either side: r_t and p_{t-1}) and stores its r and p rows
+        # 256-iteration chunk, and r and p stored once per chunk; per
+        # iteration each block reads its halo's r_t (span = 1000 rows either
+        # side; the halo's p stays in LDS) and stores the r rows within span
+        # of its edges (its neighbours' halos)
         spw = next(w for w in (1, 2, 4) if -(-lay["slices"] // (16 * w)) <= 256)
         G, span = -(-lay["slices"] // (16 * spw)), 1000
-        b = lay["dia_slots"] * 8 / 256 + G * 2 * span * 2 * 8 + 2 * n * 8
-        form = ("dia_slots*8/256 (values once per chunk) + G*2*span*2*8 (halo: r_t, p_{t-1}) + 2*n*8 (r and p "
-                "stored); y, Ap, p and the values stay on chip")
+        b = (lay["dia_slots"] * 8 + 2 * n * 8) / 256 + 2 * (G * 2 * span * 8)
+        form = ("(dia_slots*8 + 2*n*8)/256 (values in, r and p out once per chunk) + 2*G*2*span*8 (halo r_t read, "
+                "edge r rows stored); y, Ap, p and the values stay on chip")
         kern = "cg_persist_kernel (DIA values in registers, x from an LDS halo; one launch per chunk)"
     elif r["persistent_loop"]:
         slots, slices = lay["slots"], lay["slices"]

@@ -1046,7 +1046,10 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
       const V t2 = a * aps[lr0 + 64 * i];
       r[i] = r[i] - t2;  // cg.py:200
       if (s0 + i < nslices && row < n) {
-        st_wt(at32(B.Rs, row), r[i]);
+        // WR: only the rows within span of the block's edges are another
+        // block's halo; the rest go out once, after the loop
+        const int lr = lr0 + 64 * i;
+        if (WR == 0 || lr < po || lr >= ROWS - po) st_wt(at32(B.Rs, row), r[i]);
         rr += dterm((double)r[i], (double)r[i]);
       }
     }
@@ -1101,7 +1104,10 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     const int64_t row = (s0 + i) * 64 + lane;
     if (s0 + i < nslices && row < n) {
       *at32(B.Yout, row) = ys[i * kCgpBlock + tid];
-      if (WR > 0 && t > 0) *at32(Plast, row) = ps[po + lr0 + 64 * i];
+      if (WR > 0 && t > 0) {
+        *at32(Plast, row) = ps[po + lr0 + 64 * i];
+        *at32(B.Rs, row) = r[i];
+      }
     }
   }
 }
