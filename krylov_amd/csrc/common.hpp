@@ -43,7 +43,8 @@ struct Ctrl {
   int32_t stop_at;     // first chunk step that must not run (INT32_MAX = none)
   int32_t invariant;   // Arnoldi / Lanczos invariant flag
   int32_t status;      // device-detected error (KRY_ESINGULAR, ...)
-  int32_t pad;         // (was the round-5 A/B switch of the exchange poll form; the switch is gone)
+  int32_t xchg;        // in-launch exchange poll form: 0 one 16-B load per block pair; 1 the round-4
+                       // form (two 8-B loads, every pair re-read per poll; KRY_XCHG_LEGACY=1, A/B runs only)
 };
 
 // ---------------------------------------------------------- device utils

@@ -124,10 +124,6 @@ __device__ __forceinline__ granule_u4 poll_granule(__amdgpu_buffer_rsrc_t r, int
 // (profiles/r05_xchg_probe.jsonl); two-level (per-XCD) trees and 8 or 32
 // reader blocks were slower (a second hop). The values and their summation
 // order are unchanged (lane l: blocks l, l + 64, ..., then the butterfly).
-// The round-4 poll was kept behind a run-time switch for the A/B of
-// profiles/r05_xchg_ab.txt and then removed: its 64-bit per-pair addresses
-// were live in every kernel that inlines the sweep, and were spilled in the
-// persistent CG loop.
 template <bool AGREE = false>
 __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out,
                                       unsigned spin_limit = kSpinLimit) {
@@ -144,11 +140,25 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
   bool expired = false;
   const unsigned long long t0 = wall_clock64();
   bool committed = false;  // AGREE: another block has committed this exchange
+  const bool legacy = __builtin_amdgcn_readfirstlane(ctrl->xchg) != 0;
   for (;;) {
     asm volatile("" ::: "memory");  // a fresh poll every round: the loads are not hoisted
+    if (legacy) {  // the round-4 poll, for A/B runs: every pair, two 8-B loads
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (!got[i]) g[i] = poll_granule(rs, lane + 64 * i);
+      for (int i = 0; i < 4; ++i) {
+        const int b = lane + 64 * i;
+        got[i] = b >= G;
+        if (b < G) {
+          const unsigned long long lo = __hip_atomic_load(gr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long hi = __hip_atomic_load(gr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          g[i] = granule_u4{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (!got[i]) g[i] = poll_granule(rs, lane + 64 * i);
+    }
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -360,17 +370,25 @@ __device__ __forceinline__ bool all_le(const double *vals, const double *crit, i
 }
 
 template <int D = 0>
-__global__ void ctrl_reset_kernel(Ctrl *c) {
+__global__ void ctrl_reset_kernel(Ctrl *c, int xchg) {
   c->stop_at = INT_MAX;
   c->invariant = 0;
   c->status = 0;
-  c->pad = 0;
+  c->xchg = xchg;
+}
+
+inline int xchg_mode() {
+  static const int m = [] {
+    const char *e = getenv("KRY_XCHG_LEGACY");
+    return e && atoi(e) != 0 ? 1 : 0;
+  }();
+  return m;
 }
 
 // Host helper: reset the control word to "run everything" (a one-thread
 // kernel on the stream: no pageable host copy in the chunk's critical path).
 inline void reset_ctrl(Ctrl *d_ctrl, hipStream_t st) {
-  hipLaunchKernelGGL(ctrl_reset_kernel<0>, dim3(1), dim3(1), 0, st, d_ctrl);
+  hipLaunchKernelGGL(ctrl_reset_kernel<0>, dim3(1), dim3(1), 0, st, d_ctrl, xchg_mode());
   KRY_HIP(hipGetLastError());
 }
 
