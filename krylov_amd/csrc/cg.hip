@@ -860,7 +860,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
   // all-gather of one double per block (fixed-order sum, same in every block);
   // `data`: R / P stores precede it (write-through: drained before the publish)
   auto exchange = [&](double part, int t, int xid, bool data) -> bool {
-    const double bp = block_sum1_t0(part, wsum);
+    const double bp = block_sum1_t0_dpp(part, wsum);
     tmark(xid == 0 ? 0 : 2);
     unsigned long long *gr = gran + (size_t)(xid * 2 + (t & 1)) * 2 * 256;
     const unsigned tag = ((unsigned)(t + 1) << 2) | (unsigned)(xid + 1);
@@ -871,7 +871,7 @@ __global__ __launch_bounds__(kCgpBlock) void cg_persist_kernel(
     }
     if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, bp);
     if (tid < 64) {
-      const bool ok = sweep_partials(gr, G, tag, words, ctrl, &shv[0], spin_limit);
+      const bool ok = sweep_partials<false, true>(gr, G, tag, words, ctrl, &shv[0], spin_limit);
       if (tid == 0) {
         flag = ok ? 1 : 0;
       }

@@ -124,7 +124,34 @@ __device__ __forceinline__ granule_u4 poll_granule(__amdgpu_buffer_rsrc_t r, int
 // (profiles/r05_xchg_probe.jsonl); two-level (per-XCD) trees and 8 or 32
 // reader blocks were slower (a second hop). The values and their summation
 // order are unchanged (lane l: blocks l, l + 64, ..., then the butterfly).
-template <bool AGREE = false>
+// Wave sum of a double by DPP moves (VALU lane exchanges, no LDS round
+// trip): xor 1 and 2 within quads, the half-row and row mirrors, then the
+// row broadcasts 15 and 31; a fixed tree whose total lands in lane 63 and is
+// returned, read back as a wave-uniform value, in every lane. Masked rows
+// add 0 (the update keeps `old` = 0 there).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v = v + dpp_mov_f64<0xB1>(v);        // quad_perm [1, 0, 3, 2]
+  v = v + dpp_mov_f64<0x4E>(v);        // quad_perm [2, 3, 0, 1]
+  v = v + dpp_mov_f64<0x141>(v);       // row_half_mirror
+  v = v + dpp_mov_f64<0x140>(v);       // row_mirror
+  v = v + dpp_mov_f64<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v = v + dpp_mov_f64<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// DPP: the final wave sum by wave_sum_dpp (the persistent CG loop; its sums
+// have their own fixed order) instead of the xor butterfly of shuffles.
+template <bool AGREE = false, bool DPP = false>
 __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl, double *out,
                                       unsigned spin_limit = kSpinLimit) {
   const int lane = threadIdx.x;
@@ -207,8 +234,12 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
     const int b = lane + 64 * i;
     if (b < G) s += __longlong_as_double((long long)(((unsigned long long)g[i].z << 32) | (unsigned long long)g[i].x));
   }
+  if constexpr (DPP) {
+    s = wave_sum_dpp(s);
+  } else {
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  }
   if (lane == 0) *out = s;
   return true;
 }
@@ -229,6 +260,18 @@ __device__ __forceinline__ double block_sum1_t0(double v, double *wsum) {
     s = lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0;
     for (int off = 1; off < (int)(blockDim.x >> 6); off <<= 1) s += __shfl_xor(s, off);
   }
+  return s;
+}
+// block_sum1_t0 with DPP wave sums (the persistent CG loop): every wave's
+// sum by wave_sum_dpp, then wave 0 sums the wave sums the same way; the
+// result is valid in every lane of wave 0
+__device__ __forceinline__ double block_sum1_t0_dpp(double v, double *wsum) {
+  v = wave_sum_dpp(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wsum[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (wv == 0) s = wave_sum_dpp(lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0);
   return s;
 }
 __device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
