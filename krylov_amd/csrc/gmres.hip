@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
       double t = acc[0];
 #pragma unroll
       for (int v = 1; v < W; ++v) t += acc[v];
-      part1 = block_sum1_t0(t, red + kMgsBlock);
+      part1 = block_sum1_t0_dpp(t, red + kMgsBlock);
     } else {
       __syncthreads();
 #pragma unroll
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
       if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
       if (const V *q2 = next_of(p + 1)) ld(q2, vn);
       if (tid < 64) {
-        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
+        const bool ok = sweep_partials<false, true>(gr, G, tag, bar, ctrl, alpha, spin_limit);
         if (tid == 0) flag = ok ? 1 : 0;
       }
       __syncthreads();
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       double t = acc[0];
 #pragma unroll
       for (int v = 1; v < W; ++v) t += acc[v];
-      part1 = block_sum1_t0(t, red + kMgsBlock);
+      part1 = block_sum1_t0_dpp(t, red + kMgsBlock);
     } else {
       __syncthreads();
 #pragma unroll
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
         const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
         if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
         if (tid < 64) {
-          const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
+          const bool ok = sweep_partials<false, true>(gr, G, tag, bar, ctrl, alpha, spin_limit);
           if (tid == 0) flag = ok ? 1 : 0;
         }
         __syncthreads();
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
       if (KC == 0) ld_chunk_sub(sv2, 0, cs[0]);
       ld_chunk(MgslSeg<V>(q2 ? q2 : Vb, e0, N, seg), 0, cn[0]);
       if (tid < 64) {
-        const bool ok = sweep_partials(gr, G, tag, bar, ctrl, alpha, spin_limit);
+        const bool ok = sweep_partials<false, true>(gr, G, tag, bar, ctrl, alpha, spin_limit);
         if (tid == 0) flag = ok ? 1 : 0;
       }
       __syncthreads();
