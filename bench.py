@@ -125,33 +125,106 @@ def gather_ceiling(label):
         return None
 
 
-def dist_setup():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
-        import torch.distributed as dist
+def plan_launch(gpus, env, device_count):
+    """How this process's ranks come about, decided before any GPU work:
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
-        pg = dist
-    return world, rank, local, pg
+    * ``torchrun``: ``WORLD_SIZE`` is set (python -m torch.distributed.run):
+      one rank per process, this process drives device LOCAL_RANK, world =
+      WORLD_SIZE (a ``--gpus`` that disagrees is noted, WORLD_SIZE wins);
+    * ``threads``: ``--gpus N`` > 1 with no launcher: ONE process drives
+      devices 0..N-1, one host thread each, over communicators from one
+      ncclCommInitAll (krylov_amd.multi's path);
+    * ``single``: one GPU (device KRYLOV_DEVICE, default 0).
+
+    ``device_count()`` is called only to check that enough devices are
+    visible; too few raise SystemExit (non-zero), never a silent N = 1."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        rank = int(env.get("RANK", "0"))
+        local = int(env.get("LOCAL_RANK", "0"))
+        have = device_count()
+        if local >= have:
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {have} GPU(s) visible")
+        note = None if gpus == world else f"--gpus {gpus} but WORLD_SIZE {world}; using WORLD_SIZE"
+        return {"mode": "torchrun", "world": world, "rank": rank, "devices": [local], "ranks": [rank], "note": note}
+    if gpus > 1:
+        have = device_count()
+        if have < gpus:
+            raise SystemExit(f"--gpus {gpus} but only {have} GPU(s) visible")
+        return {"mode": "threads", "world": gpus, "rank": 0, "devices": list(range(gpus)),
+                "ranks": list(range(gpus)), "note": None}
+    dev = int(env.get("KRYLOV_DEVICE", "0") or 0)
+    return {"mode": "single", "world": 1, "rank": 0, "devices": [dev], "ranks": [0], "note": None}
 
 
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
+class Job:
+    """The ranks this process drives (plan_launch) and the control plane
+    between processes (torchrun: a gloo group for barriers and the max over
+    ranks; the data path is RCCL)."""
 
+    def __init__(self, plan):
+        self.mode, self.world, self.rank = plan["mode"], plan["world"], plan["rank"]
+        self.devices, self.ranks = plan["devices"], plan["ranks"]
+        self.pg = None
+        if self.mode == "torchrun":
+            import torch.distributed as dist
 
-def allmax(pg, x):
-    if pg is None:
-        return x
-    import torch
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)  # control plane only
+            self.pg = dist
 
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    @property
+    def local(self):
+        """The device of this process's first rank."""
+        return self.devices[0]
+
+    def run_all(self, fn):
+        """fn(i) for every local rank i, concurrently (one host thread per
+        device: the C-ABI calls release the GIL); the first error is raised."""
+        if len(self.devices) == 1:
+            return [fn(0)]
+        import threading
+
+        out, errs = [None] * len(self.devices), []
+
+        def run(i):
+            try:
+                out[i] = fn(i)
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(i,), name=f"bench-dev{d}") for i, d in enumerate(self.devices)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out
+
+    def barrier(self):
+        if self.pg is not None:
+            self.pg.barrier()
+
+    def allmax(self, x):
+        if self.pg is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.pg is not None:
+            self.pg.destroy_process_group()
+
+    @classmethod
+    def single(cls, device=None):
+        dev = int(os.environ.get("KRYLOV_DEVICE", "0") or 0) if device is None else int(device)
+        return cls({"mode": "single", "world": 1, "rank": 0, "devices": [dev], "ranks": [0]})
 
 
 def _cg_state(A, B, comm=None, rank=0, world=1):
@@ -180,41 +253,75 @@ def _iterate(st, k, ncols, chunk=32):
         done += s
 
 
-def run_cg_bench(A_host, B, steps, warmup, world, rank, local, pg, roofline_launches=64, prof_ids=None):
-    """CG on this rank's RHS block B (n or n x k) of A: warmup, then EXACTLY
-    `steps` iterations between barrier + device sync on both sides (max over
-    ranks), then a separate pass of max(steps, roofline_launches) iterations
-    with HIP events around every SpMV launch (the kernel's average launch
-    time; event records add stream time, so this pass is not the timed one)."""
+def comm_ranks(comm):
+    """(nranks, rank) as RCCL itself reports them (kry_comm_info)."""
+    import ctypes
+
+    from krylov_amd import _lib
+
+    n, r = ctypes.c_int32(), ctypes.c_int32()
+    _lib.check(_lib.lib.kry_comm_info(comm.handle, ctypes.byref(n), ctypes.byref(r)))
+    return int(n.value), int(r.value)
+
+
+def run_cg_bench(A_host, rhs_of_rank, steps, warmup, job, repeats=1, roofline_launches=64, prof_ids=None):
+    """CG on every local rank's RHS block (rhs_of_rank(rank): n or n x k) of
+    A: warmup, then `repeats` timed regions of EXACTLY `steps` iterations,
+    each between barrier + device sync on both sides (max over ranks; in one
+    process the threads' common wall clock), then a separate pass of
+    max(steps, roofline_launches) iterations with HIP events around every
+    SpMV launch of the first local rank (the kernel's average launch time;
+    event records add stream time, so this pass is not a timed one)."""
     import krylov_amd
     from krylov_amd import _lib, distributed
     from krylov_amd.device import get_context
+    from krylov_amd.multi import _operators
 
-    ctx = get_context(local)
-    A = krylov_amd.CsrOperator(A_host, device=local)
-    comm = distributed.ShardComm.from_torch(device=local) if pg is not None else None
-    st, ncols = _cg_state(A, B, comm, rank, world)
-    chunk = st.preferred_chunk()
-    _iterate(st, warmup, ncols, chunk)
-    barrier(pg)
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    _iterate(st, steps, ncols, chunk)
-    ctx.synchronize()
-    t1 = time.perf_counter()
-    barrier(pg)
-    elapsed = allmax(pg, t1 - t0)
+    devs = job.devices
+    ctxs = [get_context(d) for d in devs]
+    ops = _operators(A_host, devs) if len(devs) > 1 else [krylov_amd.CsrOperator(A_host, device=devs[0])]
+    if job.mode == "threads":
+        comms = distributed.ShardComm.all_devices(devs)
+    elif job.mode == "torchrun" and job.world > 1:
+        comms = [distributed.ShardComm.from_torch(device=devs[0])]
+    else:
+        comms = [None]
+    rccl = comm_ranks(comms[0]) if comms[0] is not None else None
+    sts = [_cg_state(ops[i], rhs_of_rank(job.ranks[i]), comms[i], job.ranks[i], job.world) for i in range(len(devs))]
+    ncols = sts[0][1]
+    chunk = sts[0][0].preferred_chunk()
+
+    def iterate(k):
+        def one(i):
+            _iterate(sts[i][0], k, ncols, chunk)
+            ctxs[i].synchronize()
+        job.run_all(one)
+
+    iterate(warmup)
+    elapsed = []
+    for _ in range(repeats):
+        job.barrier()
+        for c in ctxs:
+            c.synchronize()
+        t0 = time.perf_counter()
+        iterate(steps)
+        t1 = time.perf_counter()
+        job.barrier()
+        elapsed.append(job.allmax(t1 - t0))
     ids = [_lib.PROF_SPMV] + [i for i in (prof_ids or []) if i != _lib.PROF_SPMV]
-    prof = profiled(ctx, ids, lambda: _iterate(st, max(steps, roofline_launches), ncols, chunk))
+    prof = profiled(ctxs[0], ids, lambda: iterate(max(steps, roofline_launches)))
     cnt, spmv_ms = prof[_lib.PROF_SPMV]
-    defer = st.defer_info()
-    del st
-    if comm is not None:
-        comm.close()
-    layout = A.layout()
-    return {"elapsed": elapsed, "spmv_count": cnt, "spmv_avg_s": spmv_ms / max(cnt, 1) / 1e3, "n": A.n,
-            "nnz": A.nnz, "layout": layout, "rhs": ncols // world, "persistent_loop": chunk == 256, "prof": prof,
-            "prof_iters": max(steps, roofline_launches), "ydefer": defer}
+    defer = sts[0][0].defer_info()
+    del sts
+    for c in comms:
+        if c is not None:
+            c.close()
+    layout = ops[0].layout()
+    med = float(np.median(elapsed))
+    return {"elapsed": med, "elapsed_all": elapsed, "spmv_count": cnt, "spmv_avg_s": spmv_ms / max(cnt, 1) / 1e3,
+            "n": ops[0].n, "nnz": ops[0].nnz, "layout": layout, "rhs": ncols // job.world,
+            "persistent_loop": chunk == 256, "prof": prof, "prof_iters": max(steps, roofline_launches),
+            "ydefer": defer, "rccl_ranks": None if rccl is None else rccl[0]}
 
 
 def spmv_kernel_desc(layout, n):
@@ -684,7 +791,7 @@ def run_spmv_general(A_host, steps):
     prev = os.environ.get("KRY_SPMV_DIA")
     os.environ["KRY_SPMV_DIA"] = "0"
     try:
-        res = run_cg_bench(A_host, np.ones(A_host.shape[0]), steps, 5, 1, 0, 0, None)
+        res = run_cg_bench(A_host, lambda _r: np.ones(A_host.shape[0]), steps, 5, Job.single())
     finally:
         if prev is None:
             del os.environ["KRY_SPMV_DIA"]
@@ -708,7 +815,7 @@ def run_spmv_unstructured(A_host, steps):
 
     B = problems.permuted_sym(A_host, 0)
     n, nnz = B.shape[0], int(B.nnz)
-    res = run_cg_bench(B, np.ones(n), steps, 5, 1, 0, 0, None, roofline_launches=steps)
+    res = run_cg_bench(B, lambda _r: np.ones(n), steps, 5, Job.single(), roofline_launches=steps)
     kname, sb, form = image_bytes_k1(res["layout"], n, nnz)
     roof = hbm_roofline(kname, sb, res["spmv_avg_s"], form, res["spmv_count"],
                         cg_it_per_s=steps / res["elapsed"], matrix="15-point 216^3 under P A P^T, P = "
@@ -774,9 +881,10 @@ def compact(full, idx=None):
     Kernel template names and byte formulas are in profiles/bench_formulas.md
     (FORMULAS); --full-out PATH writes the verbose line as well."""
     idx = traffic_index() if idx is None else idx
-    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-            "vs_baseline", "dtype", "data", "config")
-    out = {k: _r(full[k]) if k in ("value", "ms_per_step") else full[k] for k in keys}
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "repeats", "ms_per_step_min",
+            "ms_per_step_max", "launch", "rccl_ranks", "higher_is_better", "scaling", "vs_baseline", "dtype", "data",
+            "config")
+    out = {k: _r(full[k]) if k.startswith(("value", "ms_per_step")) else full[k] for k in keys if k in full}
     ro = full["roofline"]
     out["roofline"] = {"bound": ro["bound"], "achieved": _r(ro["achieved"]), "peak": ro["peak"], "unit": ro["unit"],
                        "frac": _r(ro["frac"], 3), "traffic": int(ro["traffic"]) if ro.get("traffic") else None,
@@ -795,7 +903,7 @@ def compact(full, idx=None):
         t, src = leg_traffic(idx, "cfg4", "spmv", n, nnz)
         legs["cfg4_sharded"] = {"it_per_s": _r(c4["it_per_s"]), "rhs_it_per_s": _r(c4["rhs_it_per_s"]),
                                 **_kroof(c4["roofline"], t, src), "iter_frac": _r(c4["iteration_roofline"]["frac"], 3),
-                                "ydefer": c4["iteration_roofline"].get("ydefer")}
+                                "ydefer": c4["iteration_roofline"].get("ydefer"), "rccl_ranks": c4.get("rccl_ranks")}
     for leg in ("spmv_general", "spmv_unstructured"):
         r = full.get(leg)
         if r:
@@ -866,12 +974,19 @@ def main():
                     help="also time cfg4 as a plain 8-RHS block CG (and cfg2 / cfg5 under --quick; the full run has them)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--full-out", default=None, help="also write the verbose JSON line (formulas, timings) here")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed regions of --steps iterations each; the line reports their median (min and max beside)")
     args = ap.parse_args()
 
-    world, rank, local, pg = dist_setup()
-    os.environ["KRYLOV_DEVICE"] = str(local)
-    if world > 1 and args.gpus != world:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    from krylov_amd import _lib
+
+    plan = plan_launch(args.gpus, os.environ, _lib.device_count)
+    if plan["note"]:
+        print("note: " + plan["note"], file=sys.stderr)
+    job = Job(plan)
+    world, rank = job.world, job.rank
+    os.environ["KRYLOV_DEVICE"] = str(job.local)
+    repeats = max(1, args.repeats)
 
     from krylov_amd import problems
 
@@ -881,17 +996,15 @@ def main():
     cfg4 = None
     if args.workload == "cfg4" or not args.quick:
         P3 = problems.poisson2d(3163)
-        from krylov_amd import _lib
-
-        cfg4 = run_cg_bench(P3, cfg4_rhs(P3.shape[0], rank), min(args.steps, 40), min(args.warmup, 5), world, rank,
-                            local, pg, roofline_launches=16, prof_ids=[_lib.PROF_UPDATE, _lib.PROF_OTHER])
+        cfg4 = run_cg_bench(P3, lambda r: cfg4_rhs(P3.shape[0], r), min(args.steps, 40), min(args.warmup, 5), job,
+                            repeats=repeats, roofline_launches=16, prof_ids=[_lib.PROF_UPDATE, _lib.PROF_OTHER])
     if args.workload == "cfg4":
         res, hn, hnnz = cfg4, P3.shape[0], int(P3.nnz)
         workload = (f"krylov.cg block CG, 2-D 5-point Poisson 3163^2, {cfg4['rhs']} RHS per GPU (BASELINE cfg4), "
                     "tol=0 fixed iterations")
         steps_timed = min(args.steps, 40)
     else:
-        res = run_cg_bench(A_host, np.ones(n), args.steps, args.warmup, world, rank, local, pg)
+        res = run_cg_bench(A_host, lambda _r: np.ones(n), args.steps, args.warmup, job, repeats=repeats)
         hn, hnnz = n, nnz
         workload = f"krylov.cg, 3-D 15-point stencil {args.m}^3, one RHS per GPU, tol=0 fixed iterations"
         steps_timed = args.steps
@@ -918,6 +1031,11 @@ def main():
         "steps": steps_timed,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * T / steps_timed,
+        "repeats": len(res["elapsed_all"]),
+        "ms_per_step_min": 1e3 * min(res["elapsed_all"]) / steps_timed,
+        "ms_per_step_max": 1e3 * max(res["elapsed_all"]) / steps_timed,
+        "launch": job.mode,
+        "rccl_ranks": res["rccl_ranks"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -931,6 +1049,9 @@ def main():
             "index": "int32",
             "rhs_per_gpu": rhs,
             "parallelism": f"rhs-shard x{world}" + (" (one RCCL resnorm allreduce per iteration)" if world > 1 else ""),
+            "launch": {"torchrun": "one process per GPU (torch.distributed.run)",
+                       "threads": "one process, one host thread per GPU, ncclCommInitAll",
+                       "single": "one GPU"}[job.mode],
         },
         "spmv_gbs": roof["achieved"],
         "spmv_ms": roof["ms_per_launch"],
@@ -947,6 +1068,7 @@ def main():
             "n": c4,
             "nnz": int(P3.nnz),
             "spmv_ms": 1e3 * cfg4["spmv_avg_s"],
+            "rccl_ranks": cfg4["rccl_ranks"],
             "config": "BASELINE cfg4: Poisson 3163^2 block CG, 8 RHS per GPU"
                       + (f", {world} ranks, one RCCL allreduce per iteration" if world > 1
                          else ", one GPU (no communicator attached at N = 1)"),
@@ -990,8 +1112,7 @@ def main():
             with open(args.full_out, "w") as f:
                 f.write(json.dumps(out) + "\n")
         print(json.dumps(compact(out)), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    job.close()
 
 
 if __name__ == "__main__":

@@ -59,6 +59,12 @@ enum {
 /* ---- library / context ------------------------------------------------ */
 int kry_version(void);
 const char *kry_last_error(void);
+/* The build stamp of this library (kry_version() >= 106): the first 16 hex
+ * digits of the sha256 over its HIP/C++ sources, fixed at build time
+ * (csrc/Makefile). Measurements taken on one build (profiles/ PMC passes) are
+ * stamped with it, so a benchmark can tell whether they describe the code it
+ * runs. No reference counterpart. */
+const char *kry_build_id(void);
 int kry_device_count(int *count);
 int kry_ctx_create(int device, kry_ctx **out);
 int kry_ctx_destroy(kry_ctx *ctx);
@@ -435,6 +441,9 @@ int kry_comm_destroy(kry_comm *c);
  * counterpart: the devices=[...] driver aborts every device's communicator
  * when one device's thread fails. */
 int kry_comm_abort(kry_comm *c);
+/* The communicator as RCCL sees it (kry_version() >= 106): *nranks from
+ * ncclCommCount, *rank from ncclCommUserRank; KRY_ECOMM once aborted. */
+int kry_comm_info(kry_comm *c, int32_t *nranks, int32_t *rank);
 /* in-place sum over ranks of `count` host doubles (setup-time exchanges) */
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count);
 int kry_cg_attach_comm(kry_cg *s, kry_comm *c, int32_t col_offset, int32_t total_k);

@@ -12,10 +12,15 @@ import numpy as np
 
 from .sparse import _next_pow2, as_device_operator
 
+# the reference's record (_helpers.py:93-98) plus ``renumbered``: True when
+# the operator's device image runs in a bandwidth-reducing renumbering (RCM,
+# CsrOperator.layout()["renumbered"]), so the solve's summation order differs
+# from the reference's and its history matches only to the reference's own
+# order spread (INTEGRATION.md "Renumbering"; KRY_RENUMBER=0 turns it off).
 Info = namedtuple(
     "IterInfo",
-    ["success", "xk", "numsteps", "resnorms", "num_operations", "arnoldi"],
-    defaults=(None, None),
+    ["success", "xk", "numsteps", "resnorms", "num_operations", "arnoldi", "renumbered"],
+    defaults=(None, None, None),
 )
 
 
@@ -116,7 +121,7 @@ class Problem:
             if _is_identity(op):
                 self.ops[name] = None
                 continue
-            dop = as_device_operator(op, device=self.ctx.device, like=self.A)
+            dop = as_device_operator(op, device=self.ctx.device, like=self.A, ctx=self.ctx)
             if dop.shape != self.A.shape:
                 raise ValueError(f"preconditioner {name} has shape {dop.shape}, the operator {self.A.shape}")
             self.ops[name] = dop

@@ -129,6 +129,7 @@ _SIGNATURES = {
     "kry_comm_abort": [_vp],
     "kry_comm_create_all": [_vp, _i32, _vp],
     "kry_comm_allreduce": [_vp, _dp, _i32],
+    "kry_comm_info": [_vp, _vp, _vp],
     "kry_cg_attach_comm": [_vp, _vp, _i32, _i32],
     "kry_gmres_attach_comm": [_vp, _vp, _i32, _i32],
     "kry_minres_attach_comm": [_vp, _vp, _i32, _i32],
@@ -164,10 +165,20 @@ for _name, _args in _SIGNATURES.items():
 if not HOST_ONLY:
     lib.kry_version.argtypes = []
     lib.kry_version.restype = _int
+    lib.kry_build_id.argtypes = []
+    lib.kry_build_id.restype = ctypes.c_char_p
 lib.kry_last_error.argtypes = []
 lib.kry_last_error.restype = ctypes.c_char_p
 
-EXPORTED = sorted(list(_SIGNATURES) + ["kry_version", "kry_last_error"])
+EXPORTED = sorted(list(_SIGNATURES) + ["kry_version", "kry_last_error", "kry_build_id"])
+
+
+def build_id():
+    """The loaded library's build stamp (kry_build_id: sha256 of its
+    sources, 16 hex digits), or None for the host-only build."""
+    if HOST_ONLY:
+        return None
+    return lib.kry_build_id().decode()
 
 
 def check(rc):

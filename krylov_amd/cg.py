@@ -123,12 +123,12 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     global iterate gathered), the same steps and history as one device.
     """
     if devices is not None:
-        if inner is not None or return_arnoldi:
-            raise NotImplementedError("devices=[...] takes the Euclidean inner product, no return_arnoldi")
+        if return_arnoldi:
+            raise NotImplementedError("devices=[...] does not return the Lanczos relation")
         from .multi import solve
 
         return solve("cg", A, b, devices, x0=x0, tol=tol, atol=atol, maxiter=maxiter, callback=callback, M=M,
-                     Ml=Ml)
+                     Ml=Ml, inner=inner)
     t_call = time.perf_counter()
     t_run = 0.0
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml)
@@ -188,7 +188,8 @@ def cg(A, b, M=None, Ml=None, inner=None, x0=None, tol=1e-5, atol=1.0e-15, maxit
     last_timing.update(call_ms=1e3 * (t_end - t_call), chunks_ms=1e3 * t_run, problem_ms=1e3 * (t_prob - t_call),
                        setup_start_ms=1e3 * (t_start - t_prob), loop_host_ms=1e3 * (t_loop - t_start - t_run),
                        get_ms=1e3 * (t_get - t_loop), finish_ms=1e3 * (t_end - t_get))
-    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, arnoldi=arnoldi)
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, arnoldi=arnoldi,
+                                         renumbered=prob.A.renumbered)
 
 
 class _Lanczos:

@@ -273,20 +273,24 @@ bool env_off(const char *name) {
 // Ranges of host memory this library has registered for in-flight copies,
 // with their users: threads copying the same array (the devices=[...] driver
 // uploads one CSR to every device in parallel) share one registration, and a
-// range overlapping a registered one waits until that is released, so no
-// thread's DMA ever runs on pages another thread has just unregistered.
+// range whose PAGES overlap a registered one's waits until that is released
+// (hipHostRegister / hipHostUnregister pin and unpin whole pages, so two
+// byte-disjoint arrays sharing a page must not register independently), so
+// no thread's DMA ever runs on pages another thread has just unregistered.
 namespace {
 struct HostReg {
-  size_t end;
+  size_t end;         // exact byte range [key, end): what was registered
+  uintptr_t pa, pe;   // the pages it pins
   int users;
 };
 std::mutex host_reg_mu;
 std::condition_variable host_reg_cv;
 std::map<uintptr_t, HostReg> host_regs;
+constexpr uintptr_t kHostPage = 4096;
 
-bool overlaps_other(uintptr_t a, uintptr_t e) {
+bool overlaps_other(uintptr_t a, uintptr_t e, uintptr_t pa, uintptr_t pe) {
   for (const auto &kv : host_regs)
-    if (kv.first < e && a < kv.second.end && !(kv.first == a && kv.second.end == e)) return true;
+    if (kv.second.pa < pe && pa < kv.second.pe && !(kv.first == a && kv.second.end == e)) return true;
   return false;
 }
 }  // namespace
@@ -296,16 +300,17 @@ void host_xfer(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hip
   static const bool pin = !env_off("KRY_HOST_PIN");
   void *host = kind == hipMemcpyHostToDevice ? const_cast<void *>(src) : dst;
   const uintptr_t a = reinterpret_cast<uintptr_t>(host), e = a + bytes;
+  const uintptr_t pa = a & ~(kHostPage - 1), pe = (e + kHostPage - 1) & ~(kHostPage - 1);
   bool reg = false;
   if (pin && bytes >= kPinMin) {
     std::unique_lock<std::mutex> lk(host_reg_mu);
-    host_reg_cv.wait(lk, [&] { return !overlaps_other(a, e); });
+    host_reg_cv.wait(lk, [&] { return !overlaps_other(a, e, pa, pe); });
     auto it = host_regs.find(a);
     if (it != host_regs.end() && it->second.end == e) {
       ++it->second.users;
       reg = true;
     } else if (hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess) {
-      host_regs[a] = HostReg{e, 1};
+      host_regs[a] = HostReg{e, pa, pe, 1};
       reg = true;
     } else {
       (void)hipGetLastError();  // locked by its owner (e.g. pinned memory), or not lockable: pageable
@@ -437,7 +442,12 @@ extern "C" {
 // 103: the per-step allreduces of the sharded solvers carry a fault count
 // (CG total_k + 1, GMRES / MINRES total_k + 2 values); kry_cg_defer_info,
 // kry_gmres_xk_device.
-int kry_version(void) { return 105; }
+int kry_version(void) { return 106; }
+
+#ifndef KRY_BUILD_ID
+#define KRY_BUILD_ID "unknown"
+#endif
+const char *kry_build_id(void) { return KRY_BUILD_ID; }
 
 int kry_device_count(int *count) {
   KRY_API_BEGIN

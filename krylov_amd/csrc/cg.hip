@@ -1605,8 +1605,7 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       // exactly one collective per iteration: the residual-norm vector and the
       // fault count (post_fault)
       inject_peer_fault(s->gbuf, s->total_k + 1, step, st);
-      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 1, ncclDouble, ncclSum, s->comm->comm, st);
-      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      comm_allreduce(s->comm, s->gbuf, s->total_k + 1, st);
       hipLaunchKernelGGL(cg_global_check, dim3(1), dim3(kBlock), 0, st, s->gbuf, s->gcrit, s->total_k, s->hist,
                          s->ctrl, step);
       KRY_HIP(hipGetLastError());

@@ -90,7 +90,7 @@ int kry_comm_destroy(kry_comm *c) {
   if (!c) return KRY_OK;
   (void)hipSetDevice(c->ctx->device);
   (void)hipStreamSynchronize(c->ctx->stream);
-  if (c->comm && !c->aborted) (void)ncclCommDestroy(c->comm);
+  if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
   dev_free(c->dbuf);
   delete c;
   KRY_API_END
@@ -104,11 +104,35 @@ int kry_comm_destroy(kry_comm *c) {
 int kry_comm_abort(kry_comm *c) {
   KRY_API_BEGIN
   KRY_REQUIRE(c, KRY_EINVAL, "null communicator");
-  if (c->comm && !c->aborted) {
-    c->aborted = true;
+  // the flag first: a peer thread's next enqueue fails without touching the
+  // handle; then the lock, so no enqueue is in flight on the handle the abort
+  // frees. A lock not obtained within 10 s means an enqueue is itself blocked
+  // inside RCCL (a connection waiting for a peer): abort anyway, which is
+  // what releases it.
+  if (c->aborted.exchange(true, std::memory_order_acq_rel)) return KRY_OK;
+  bool locked = c->mu.try_lock_for(std::chrono::seconds(10));
+  ncclComm_t h = c->comm;
+  c->comm = nullptr;
+  ncclResult_t r = ncclSuccess;
+  if (h) {
     (void)hipSetDevice(c->ctx->device);
-    KRY_NCCL(ncclCommAbort(c->comm));
+    r = ncclCommAbort(h);
   }
+  if (locked) c->mu.unlock();
+  if (r != ncclSuccess) throw Error{KRY_ECOMM, std::string("ncclCommAbort: ") + ncclGetErrorString(r)};
+  KRY_API_END
+}
+
+int kry_comm_info(kry_comm *c, int32_t *nranks, int32_t *rank) {
+  KRY_API_BEGIN
+  KRY_REQUIRE(c && nranks && rank, KRY_EINVAL, "null argument");
+  std::lock_guard<std::timed_mutex> g(c->mu);
+  KRY_REQUIRE(!c->aborted.load() && c->comm, KRY_ECOMM, "the communicator was aborted");
+  int n = 0, r = 0;
+  KRY_NCCL(ncclCommCount(c->comm, &n));
+  KRY_NCCL(ncclCommUserRank(c->comm, &r));
+  *nranks = n;
+  *rank = r;
   KRY_API_END
 }
 
@@ -117,7 +141,7 @@ int kry_comm_abort(kry_comm *c) {
 int kry_comm_allreduce(kry_comm *c, double *host, int32_t count) {
   KRY_API_BEGIN
   KRY_REQUIRE(c && host && count >= 0, KRY_EINVAL, "bad argument");
-  KRY_REQUIRE(!c->aborted, KRY_ECOMM, "the communicator was aborted");
+  KRY_REQUIRE(!c->aborted.load(), KRY_ECOMM, "the communicator was aborted");
   if (count == 0) return KRY_OK;
   KRY_HIP(hipSetDevice(c->ctx->device));
   hipStream_t st = c->ctx->stream;
@@ -128,7 +152,7 @@ int kry_comm_allreduce(kry_comm *c, double *host, int32_t count) {
     c->dbuf_len = count;
   }
   KRY_HIP(hipMemcpyAsync(c->dbuf, host, (size_t)count * 8, hipMemcpyHostToDevice, st));
-  KRY_NCCL(ncclAllReduce(c->dbuf, c->dbuf, count, ncclDouble, ncclSum, c->comm, st));
+  comm_allreduce(c, c->dbuf, (size_t)count, st);
   KRY_HIP(hipMemcpyAsync(host, c->dbuf, (size_t)count * 8, hipMemcpyDeviceToHost, st));
   KRY_HIP(hipStreamSynchronize(st));
   KRY_API_END

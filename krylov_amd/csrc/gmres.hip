@@ -1437,8 +1437,7 @@ void gm_qr_step(kry_gmres *s, const double *pin, int P, int col, int step) {
   KRY_HIP(hipGetLastError());
   if (!s->comm) return;
   inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
-  ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
-  KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  comm_allreduce(s->comm, s->gbuf, s->total_k + 2, st);
   hipLaunchKernelGGL(gm_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                      (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
   KRY_HIP(hipGetLastError());

@@ -664,8 +664,7 @@ void mr_run_typed(kry_minres *s, int max_steps) {
       if (mru_launch(s, w, p, s->W[f], s->W[f ^ 1], pnew, partA, PA, step, i)) {
         if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
           inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
-          ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
-          KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+          comm_allreduce(s->comm, s->gbuf, s->total_k + 2, st);
           hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                              (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
           KRY_HIP(hipGetLastError());
@@ -685,8 +684,7 @@ void mr_run_typed(kry_minres *s, int max_steps) {
     KRY_HIP(hipGetLastError());
     if (s->comm) {  // one collective per iteration: residual norms + non-invariant count
       inject_peer_fault(s->gbuf, s->total_k + 2, step, st);
-      ncclResult_t nr = ncclAllReduce(s->gbuf, s->gbuf, s->total_k + 2, ncclDouble, ncclSum, s->comm->comm, st);
-      KRY_REQUIRE(nr == ncclSuccess, KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      comm_allreduce(s->comm, s->gbuf, s->total_k + 2, st);
       hipLaunchKernelGGL(mr_global_check, dim3(1), dim3(kBlock), 0, st, (const double *)s->gbuf,
                          (const double *)s->gcrit, s->total_k, s->hist, s->ctrl, step);
       KRY_HIP(hipGetLastError());

@@ -1,23 +1,44 @@
 // Pieces shared by the CG / GMRES / MINRES device loops.
 #pragma once
 
+#include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstring>
+#include <mutex>
 
 #include <rccl/rccl.h>
 
 #include "device.hpp"
 
+// One rank's RCCL communicator. Several host threads may hold one (the
+// devices=[...] driver aborts every device's communicator from the thread
+// that failed while the others are inside their solver loops), so: `aborted`
+// is atomic, and every collective ENQUEUE and the abort itself run under
+// `mu` (not the stream syncs that follow an enqueue: an abort must be able to
+// release a rank blocked in one). After an abort `comm` is null.
 struct kry_comm {
   kry_ctx *ctx = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   double *dbuf = nullptr;  // scratch for host allreduces
   int dbuf_len = 0;
-  bool aborted = false;  // kry_comm_abort ran: destroy skips ncclCommDestroy
+  std::atomic<bool> aborted{false};  // kry_comm_abort ran: destroy skips ncclCommDestroy
+  std::timed_mutex mu;
 };
 
 namespace kry {
+
+// In-place float64 sum over the communicator's ranks of `count` device
+// doubles, enqueued on `st` under the communicator's lock; KRY_ECOMM once the
+// communicator was aborted (by any thread).
+inline void comm_allreduce(kry_comm *c, double *buf, size_t count, hipStream_t st) {
+  std::lock_guard<std::timed_mutex> g(c->mu);
+  if (c->aborted.load(std::memory_order_acquire) || !c->comm)
+    throw Error{KRY_ECOMM, "the communicator was aborted"};
+  ncclResult_t nr = ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, st);
+  if (nr != ncclSuccess) throw Error{KRY_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr)};
+}
 
 // ------------------------------------------------ in-launch all-gathers
 // Persistent kernels (GMRES MGS, small-n CG) exchange one double per block

@@ -289,7 +289,7 @@ def bicgstab(A, b, Ml=None, Mr=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15
             success = True
             break
     xk = D.host_final(x)
-    return xk if success else None, Info(success, xk, k, resnorms)
+    return xk if success else None, Info(success, xk, k, resnorms, renumbered=prob.A.renumbered)
 
 
 def cgs(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None):
@@ -353,7 +353,7 @@ def cgs(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None,
             resnorms.append(D.cols(row))
             k += 1
     xk = D.host_final(x)
-    return xk if success else None, Info(success, xk, k, resnorms)
+    return xk if success else None, Info(success, xk, k, resnorms, renumbered=prob.A.renumbered)
 
 
 def cgr(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callback=None):
@@ -419,7 +419,7 @@ def cgr(A, b, M=None, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None,
             resnorms.append(D.cols(row))
             k += 1
     xk = D.host_final(x)
-    return xk if success else None, Info(success, xk, k, resnorms)
+    return xk if success else None, Info(success, xk, k, resnorms, renumbered=prob.A.renumbered)
 
 
 # gcr's basis grows by two n x k vectors per step; a chunk enqueued before its
@@ -492,4 +492,4 @@ def gcr(A, b, x0=None, inner=None, tol=1e-5, atol=1.0e-15, maxiter=None, callbac
             resnorms.append(D.cols(row))
             k += 1
     xk = D.host_final(x)
-    return xk if success else None, Info(success, xk, k, resnorms)
+    return xk if success else None, Info(success, xk, k, resnorms, renumbered=prob.A.renumbered)

@@ -169,19 +169,17 @@ def gmres(A, b, M=None, Ml=None, Mr=None, inner=None, ortho="mgs", x0=None, tol=
     ``ortho``: "mgs", "mgsK" (K MGS sweeps) or "householder" (Householder
     Arnoldi, arnoldi.py:33-104, one right-hand side, default inner, no M)."""
     if devices is not None:  # several GPUs of this process (krylov_amd.multi)
-        if inner is not None:
-            raise NotImplementedError("devices=[...] takes the Euclidean inner product")
         from .multi import solve
 
         return solve("gmres", A, b, devices, x0=x0, tol=tol, atol=atol, maxiter=maxiter, ortho=ortho,
-                     callback=callback, M=M, Ml=Ml, Mr=Mr)
+                     callback=callback, M=M, Ml=Ml, Mr=Mr, inner=inner)
     sweeps = _sweeps(ortho, inner, M, b)
     prob = Problem(A, b, x0, inner, M=M, Ml=Ml, Mr=Mr)
     maxiter = prob.A.shape[0] if maxiter is None else maxiter
     st = _GmresState(prob, maxiter, sweeps)
     host_out = HostOut((prob.n, prob.kpad), prob.dtype)  # pages faulted in while the device iterates
     success, xk, k, resnorms = _cycle(prob, st, maxiter, tol, atol, callback, host_out=host_out)
-    return xk if success else None, Info(success, xk, k, resnorms, num_operations=_num_operations(k))
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=_num_operations(k), renumbered=prob.A.renumbered)
 
 
 def _sweeps(ortho, inner, M, b):
@@ -350,7 +348,7 @@ def gmres_restarted(A, b, restart=30, x0=None, tol=1e-5, atol=1.0e-15, max_cycle
         x_cur = x_buf
         if success and xk is None:
             xk = prob.unpad_vec(x_buf.to_host(out=host_out.take()), prob.r0_dtype)
-        infos.append(Info(success, xk, k, resnorms, num_operations=_num_operations(k)))
+        infos.append(Info(success, xk, k, resnorms, num_operations=_num_operations(k), renumbered=prob.A.renumbered))
         x = xk
         if success:
             break

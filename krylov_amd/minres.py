@@ -161,4 +161,4 @@ def minres(A, b, M=None, Ml=None, Mr=None, inner=None, x0=None, tol=1e-5, atol=1
         "inner": 2 + 2 * k,
         "axpy": 4 + 8 * k,
     }
-    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations)
+    return xk if success else None, Info(success, xk, k, resnorms, num_operations=num_operations, renumbered=prob.A.renumbered)

@@ -23,11 +23,16 @@ the residual norms per iteration, xk gathered into X[:, 8g:8g+8]".
 
 ``A``: a scipy.sparse matrix or dense array (uploaded once per device, the
 uploads in parallel threads), or a list of ``CsrOperator``, one per device
-in ``devices`` order. Callbacks and preconditioners are not taken on this
-path (NotImplementedError), as on the multi-process sharded path. If one
-device's thread fails, every communicator is aborted (kry_comm_abort), so
-the others stop at their next collective instead of waiting for it, and
-that first error is raised.
+in ``devices`` order. ``M``/``Ml``/``Mr`` likewise (a host matrix is
+uploaded to every device; each device applies it to its own columns with the
+single-device kernels), and ``inner`` (None or WeightedInner). ``callback``
+is called once per step, from the first device's thread, with the gathered
+global iterate, exactly as the single-device solve calls it (cg.py:119-120,
+202-204; gmres.py:143-144, 226-228; minres.py:160-161, 230-232); every step
+then gathers x over the devices, so it is a debugging aid, not a fast path.
+If one device's thread fails, every communicator is aborted
+(kry_comm_abort), so the others stop at their next collective instead of
+waiting for it, and that first error is raised.
 """
 import threading
 
@@ -69,16 +74,27 @@ def _operators(A, devices):
     return ops
 
 
+def _per_device(name, op, devices):
+    """A preconditioner for each device: None, a host matrix (each device's
+    Problem uploads it), or one CsrOperator per device in devices order."""
+    from .sparse import CsrOperator
+
+    if isinstance(op, (list, tuple)):
+        if len(op) != len(devices) or not all(isinstance(a, CsrOperator) and a.device == d
+                                               for a, d in zip(op, devices)):
+            raise ValueError(f"{name} as a list: one CsrOperator per device, in devices order")
+        return list(op)
+    if isinstance(op, CsrOperator) and (len(devices) > 1 or op.device != devices[0]):
+        raise ValueError(f"devices=[...]: pass {name} as a host matrix (uploaded to every device) or one "
+                         "CsrOperator per device")
+    return [op] * len(devices)
+
+
 def solve(method, A, B, devices, x0=None, **kw):
     """The sharded solve of ``method`` ("cg", "gmres", "minres") over
     ``devices``: returns ``(xk or None, Info)`` with ``Info.xk`` the gathered
     global iterate and ``Info.resnorms`` the global history."""
-    if kw.get("callback") is not None:
-        raise NotImplementedError("callbacks are not supported with devices=[...]")
-    kw.pop("callback", None)
-    for name in ("M", "Ml", "Mr"):
-        if kw.pop(name, None) is not None:
-            raise NotImplementedError("preconditioners are not supported with devices=[...]")
+    callback = kw.pop("callback", None)
     devices = [int(d) for d in devices]
     if len(set(devices)) != len(devices) or not devices:
         raise ValueError(f"devices must be distinct device ids, got {devices}")
@@ -102,6 +118,22 @@ def solve(method, A, B, devices, x0=None, **kw):
         return np.ascontiguousarray(blk)
 
     ops = _operators(A, devices)
+    precs = {name: _per_device(name, kw.pop(name), devices) for name in ("M", "Ml", "Mr") if kw.get(name) is not None}
+    for name in ("M", "Ml", "Mr"):
+        kw.pop(name, None)
+    user_cb = None
+    if callback is not None:
+        def user_cb(x, second):
+            # the single-device call's shapes: b's shape for vectors, the
+            # reference's per-column array (a 0-d one for a 1-D b) for norms
+            x = x.reshape(B.shape)
+            second = np.asarray(second)
+            second = second.reshape(B.shape) if second.size == x.size else (
+                np.array(second.reshape(-1)[0]) if vec else second.reshape(B.shape[1:]))
+            callback(x, second)
+
+        def noop(*_a):
+            pass
     comms = ShardComm.all_devices(devices)
     fn = getattr(distributed, method)
     out = [None] * D
@@ -112,7 +144,10 @@ def solve(method, A, B, devices, x0=None, **kw):
 
     def run(g):
         try:
-            out[g] = fn(ops[g], local(B2, g), comms[g], x0=None if X0 is None else local(X0, g), kcs=kcs, **kw)
+            cb = None if user_cb is None else (user_cb if g == 0 else noop)
+            pg = {name: lst[g] for name, lst in precs.items()}
+            out[g] = fn(ops[g], local(B2, g), comms[g], x0=None if X0 is None else local(X0, g), kcs=kcs,
+                        callback=cb, **pg, **kw)
         except BaseException as e:  # noqa: BLE001 - re-raised below
             errs[g] = e
             # the other devices may be waiting in a collective this one will

@@ -62,9 +62,15 @@ class ShardLayout:
         return full
 
 
-def drive(engine, layout, allreduce, tol, atol, maxiter, inner_dtype, chunk=32):
+def drive(engine, layout, allreduce, tol, atol, maxiter, inner_dtype, chunk=32, hook=None):
     """The reference's outer loop over a sharded block (cg.py:150-234,
     gmres.py:179-234, minres.py:160-236 with the global stop rule).
+
+    ``hook(k, resnorm)``, if given, runs where the reference calls its
+    callback: once after the initial norms (k = 0; cg.py:119-120,
+    gmres.py:143-144, minres.py:160-161) and after every step (cg.py:202-204,
+    gmres.py:226-228, minres.py:230-232), with the global norms of the real
+    columns; the chunk is then one step, as on one device.
 
     ``engine`` is this rank's solver state:
       start_norms()      -> local kpad initial residual norms (float64)
@@ -84,6 +90,9 @@ def drive(engine, layout, allreduce, tol, atol, maxiter, inner_dtype, chunk=32):
     resnorms = [cast(rn0[real])]
     criterion = np.maximum(tol * resnorms[0], atol)
     engine.set_criterion(layout.criterion_full(criterion))
+    if hook is not None:
+        hook(0, resnorms[0])
+        chunk = 1
     k = 0
     success = False
     while True:
@@ -104,6 +113,8 @@ def drive(engine, layout, allreduce, tol, atol, maxiter, inner_dtype, chunk=32):
         for row in rows:
             resnorms.append(cast(np.asarray(row)[real]))
             k += 1
+        if hook is not None:
+            hook(k, resnorms[-1])
     return success, k, resnorms
 
 

@@ -30,9 +30,11 @@ class CsrOperator:
     renumbered operator, kry_csr_create_like); the device picks the
     renumbering on its own otherwise (reverse Cuthill-McKee for scattered
     matrices with a narrow level structure). Vectors always cross in the
-    caller's numbering."""
+    caller's numbering. ``ctx``: a ``device.Context`` to build it on instead
+    of the device's shared one (its own stream; e.g. two solves driven
+    concurrently on one GPU)."""
 
-    def __init__(self, A, device=None, like=None):
+    def __init__(self, A, device=None, like=None, ctx=None):
         if isinstance(A, CsrOperator):
             raise TypeError("already a CsrOperator")
         if scipy.sparse.issparse(A):
@@ -53,7 +55,7 @@ class CsrOperator:
         dt = np.dtype(csr.dtype)
         if dt not in (np.float32, np.float64):
             dt = np.dtype(np.float64)
-        self.ctx = get_context(device)
+        self.ctx = get_context(device) if ctx is None else ctx
         self.shape = csr.shape
         self.dtype = dt
         self.n = csr.shape[0]
@@ -149,7 +151,7 @@ class CsrOperator:
 # dtype), so an in-place change of the matrix is re-uploaded. It holds at most
 # _CACHE_MAX entries and drops an entry when its matrix is garbage-collected.
 _CACHE_MAX = 4
-_cache = {}  # (device, id(A)) -> (weakref(A), fingerprint, CsrOperator)
+_cache = {}  # (device, id(A), id(like) or None) -> (weakref(A), fingerprint, CsrOperator, weakref(like) or None)
 
 
 def _fingerprint(A):
@@ -176,16 +178,21 @@ def clear_operator_cache():
     _lib.empty_cache()
 
 
-def as_device_operator(A, device=None, like=None):
+def as_device_operator(A, device=None, like=None, ctx=None):
     """Return ``A`` as a CsrOperator (uploading scipy/dense inputs once).
     ``like``: the operator a preconditioner serves; when it is renumbered the
     preconditioner is built with its renumbering (a CsrOperator given as a
-    preconditioner must already carry it)."""
+    preconditioner must already carry it). ``ctx``: the context to upload on
+    (default: the device's shared one; another context is not cached)."""
     import os
 
     lk = like if (like is not None and like.renumbered) else None
     if isinstance(A, CsrOperator):
+        if ctx is not None and A.ctx is not ctx:
+            raise ValueError("the operator lives on another context than the solve")
         return A
+    if ctx is not None and ctx is not get_context(ctx.device):
+        return CsrOperator(A, like=lk, ctx=ctx)
     if os.environ.get("KRYLOV_CSR_CACHE", "1") == "0":
         return CsrOperator(A, device=device, like=lk)
     dev = get_context(device).device
@@ -194,15 +201,20 @@ def as_device_operator(A, device=None, like=None):
         return CsrOperator(A, device=device, like=lk)
     key = (dev, id(A), None if lk is None else id(lk))
     hit = _cache.get(key)
-    if hit is not None and hit[0]() is A and hit[1] == fp:
+    # the entry also holds a weakref to the operator it was built like: a new
+    # operator that reuses a dead one's id() must not get a preconditioner
+    # carrying the dead one's permutation
+    if (hit is not None and hit[0]() is A and hit[1] == fp
+            and (hit[3] is None if lk is None else (hit[3] is not None and hit[3]() is lk))):
         return hit[2]
     op = CsrOperator(A, device=dev, like=lk)
     try:
         ref = weakref.ref(A, lambda _r, key=key: _cache.pop(key, None))
+        lref = None if lk is None else weakref.ref(lk, lambda _r, key=key: _cache.pop(key, None))
     except TypeError:
         return op
     _cache.pop(key, None)
     while len(_cache) >= _CACHE_MAX:
         _cache.pop(next(iter(_cache)))
-    _cache[key] = (ref, fp, op)
+    _cache[key] = (ref, fp, op, lref)
     return op

@@ -659,3 +659,26 @@ def test_rs_plan_matches_restatement(case):
     assert got["slices"] == want["slices"] and got["slots"] == want["slots"]
     np.testing.assert_array_equal(got["widths"], want["widths"])
     np.testing.assert_array_equal(got["colrank"], want["colrank"])
+
+
+def test_build_id_matches_sources():
+    """The loaded library is built from the sources in the tree: its stamp
+    (kry_build_id, csrc/Makefile) is the sha256 over them, so a stale .so
+    (or a PMC summary stamped with another build, bench.py) is caught."""
+    import glob
+    import hashlib
+    import os
+
+    from krylov_amd import _lib
+
+    if _lib.HOST_ONLY:
+        pytest.skip("host-only build")
+    csrc = os.path.join(os.path.dirname(_lib.__file__), "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp"))
+                   + glob.glob(os.path.join(csrc, "*.cpp")), key=os.path.basename)
+    files.append(os.path.join(csrc, "..", "..", "include", "krylov_hip.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    assert _lib.build_id() == h.hexdigest()[:16]

@@ -68,9 +68,9 @@ def test_devices_argument_errors():
     with pytest.raises(ValueError):
         krylov_amd.cg(P, B, devices=[0, 0])
     with pytest.raises(NotImplementedError):
-        krylov_amd.cg(P, B, devices=[0], callback=lambda x, r: None)
-    with pytest.raises(NotImplementedError):
-        krylov_amd.gmres(P, B, devices=[0], M=np.eye(P.shape[0]))
+        krylov_amd.cg(P, B, devices=[0], return_arnoldi=True)
+    with pytest.raises(ValueError):  # a preconditioner list must match the devices
+        krylov_amd.gmres(P, B, devices=[0], M=[krylov_amd.CsrOperator(P, device=0)] * 2)
     with pytest.raises(ValueError):
         krylov_amd.cg(krylov_amd.CsrOperator(P), B, devices=[0])
     ops = [krylov_amd.CsrOperator(P, device=0)]

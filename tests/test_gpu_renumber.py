@@ -192,6 +192,9 @@ def test_renumbered_cg_converges_like_unrenumbered(perm104, op104, monkeypatch):
     x0, i0 = krylov_amd.cg(krylov_amd.CsrOperator(perm104), b, tol=1e-8)
     _, ref = K.cg(perm104, b, tol=1e-8)
     assert i1.success and i1.numsteps == i0.numsteps == ref.numsteps
+    # Info says which solve ran renumbered (its history matches the
+    # reference's only to the reference's own order spread)
+    assert i1.renumbered is True and i0.renumbered is False
     h1, h0, hr = (np.asarray(i.resnorms) for i in (i1, i0, ref))
     np.testing.assert_allclose(h1[:60], hr[:60], rtol=1e-10)
     np.testing.assert_allclose(h0[:60], hr[:60], rtol=1e-10)
@@ -322,3 +325,28 @@ def test_device_rcm_equals_host_order(case, perm104):
     assert info[0] == 1 and host is not None
     np.testing.assert_array_equal(perm, host[0])
     assert info[1] == host[1]
+
+
+def test_info_renumbered_flag_natural_order():
+    """A stencil in its natural order is not renumbered, and every driver's
+    Info says so (cg, gmres, minres, bicgstab, gmres_restarted)."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    A = krylov_amd.CsrOperator(problems.stencil15_3d(24))
+    assert not A.renumbered
+    b = np.ones(A.shape[0])
+    for fn in (krylov_amd.cg, krylov_amd.gmres, krylov_amd.minres, krylov_amd.bicgstab):
+        _, info = fn(A, b, tol=0.0, atol=0.0, maxiter=3)
+        assert info.renumbered is False, fn.__name__
+    _, infos = krylov_amd.gmres_restarted(A, b, restart=3, tol=0.0, atol=0.0, max_cycles=2)
+    assert all(i.renumbered is False for i in infos)
+
+
+def test_info_renumbered_flag_all_drivers(perm104, op104):
+    import krylov_amd
+
+    b = np.ones(perm104.shape[0])
+    for fn in (krylov_amd.cg, krylov_amd.gmres, krylov_amd.minres, krylov_amd.bicgstab):
+        _, info = fn(op104, b, tol=0.0, atol=0.0, maxiter=3)
+        assert info.renumbered is True, fn.__name__
