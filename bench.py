@@ -125,7 +125,7 @@ def gather_ceiling(label):
         return None
 
 
-def plan_launch(gpus, env, device_count):
+def plan_launch(gpus, env, device_count, launch="auto"):
     """How this process's ranks come about, decided before any GPU work:
 
     * ``torchrun``: ``WORLD_SIZE`` is set (python -m torch.distributed.run):
@@ -137,7 +137,10 @@ def plan_launch(gpus, env, device_count):
     * ``single``: one GPU (device KRYLOV_DEVICE, default 0).
 
     ``device_count()`` is called only to check that enough devices are
-    visible; too few raise SystemExit (non-zero), never a silent N = 1."""
+    visible; too few raise SystemExit (non-zero), never a silent N = 1.
+    ``launch="threads"`` takes the threaded path at any N (at N = 1: one
+    device, a one-rank ncclCommInitAll communicator attached - the path's
+    rehearsal on a one-GPU box)."""
     if gpus < 1:
         raise SystemExit(f"--gpus {gpus}: need at least one GPU")
     if "WORLD_SIZE" in env:
@@ -149,7 +152,7 @@ def plan_launch(gpus, env, device_count):
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {have} GPU(s) visible")
         note = None if gpus == world else f"--gpus {gpus} but WORLD_SIZE {world}; using WORLD_SIZE"
         return {"mode": "torchrun", "world": world, "rank": rank, "devices": [local], "ranks": [rank], "note": note}
-    if gpus > 1:
+    if gpus > 1 or launch == "threads":
         have = device_count()
         if have < gpus:
             raise SystemExit(f"--gpus {gpus} but only {have} GPU(s) visible")
@@ -974,13 +977,16 @@ def main():
                     help="also time cfg4 as a plain 8-RHS block CG (and cfg2 / cfg5 under --quick; the full run has them)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--full-out", default=None, help="also write the verbose JSON line (formulas, timings) here")
+    ap.add_argument("--launch", choices=["auto", "threads"], default="auto",
+                    help="auto: torchrun if WORLD_SIZE is set, else threads for --gpus > 1; threads: force the "
+                         "one-process threaded path (also at --gpus 1, a rehearsal with a 1-rank communicator)")
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed regions of --steps iterations each; the line reports their median (min and max beside)")
     args = ap.parse_args()
 
     from krylov_amd import _lib
 
-    plan = plan_launch(args.gpus, os.environ, _lib.device_count)
+    plan = plan_launch(args.gpus, os.environ, _lib.device_count, args.launch)
     if plan["note"]:
         print("note: " + plan["note"], file=sys.stderr)
     job = Job(plan)

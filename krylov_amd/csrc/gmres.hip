@@ -291,7 +291,7 @@ __device__ __forceinline__ void reduce_rows(const double *part, int P, int k, do
 // the granule words are zeroed once per chunk.
 constexpr int kGranWords = 2 * 2 * 256;  // two pass parities x two words x G <= 256 blocks
 // barrier words for `steps` chunk steps, then the (shared) granule words
-inline size_t bar_bytes(int steps) { return (size_t)steps * kBarWords * 4 + (size_t)kGranWords * 8; }
+inline size_t bar_bytes(int steps);
 template <typename V, int E>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V *__restrict__ w,
                                                             const V *__restrict__ Vb, size_t stride, int col,
@@ -414,6 +414,221 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
     if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
     reduce_rows<kMgsBlock, true>(slot, G, k, red);
     if (tid < k) alpha[tid] = red[tid];
+    __syncthreads();
+  }
+}
+
+// ------------------------------ persistent MGS with a two-vector lookahead
+// The same Arnoldi step as gm_mgsp_kernel with half the dependent grid
+// exchanges. The flattened MGS index list m = 0 .. np - 1 (vector
+// V_{m mod (col + 1)}, sweep m / (col + 1)) is split into groups {0} (alpha_0
+// from the SpMV's partials), {1, 2}, {3, 4}, ... (the last one single when
+// np - 1 is odd). Pass t subtracts group t, whose alphas are known,
+//   w -= alpha_a V_a;  w -= alpha_b V_b            (arnoldi.py:162, in order)
+// and forms the partials of group t + 1 = {a', b'} in the same sweep over w:
+//   c_a = <V_a', w>,  c_b = <V_b', w>,  g = <V_b', V_a'>
+// so ONE exchange gives alpha_a' = c_a and
+//   alpha_b' = <V_b', w - alpha_a' V_a'> = c_b - alpha_a' g
+// which is MGS in exact arithmetic (arnoldi.py:159-162); in floating point
+// alpha_b' moves by ~eps |alpha_a' g|, with g ~ eps for an orthonormal basis.
+// After the last group, <w, w> as before. Group t + 1's vectors are
+// prefetched into registers during pass t's predecessor's exchange and are
+// the subtrahends of pass t + 1 (read from HBM once per step, as in
+// gm_mgsp_kernel). KRY_MGS_LOOKAHEAD=0 restores gm_mgsp_kernel.
+__device__ __forceinline__ int la_groups(int np) { return 1 + np / 2; }
+__device__ __forceinline__ int la_first(int t) { return t == 0 ? 0 : 2 * t - 1; }
+__device__ __forceinline__ int la_size(int t, int np) {
+  return t >= la_groups(np) ? 0 : (t == 0 ? 1 : (np - (2 * t - 1) >= 2 ? 2 : 1));
+}
+// granule words: two pass parities x three values x two words x G <= 256 blocks
+constexpr int kGranWordsLa = 2 * 3 * 2 * 256;
+inline size_t bar_bytes(int steps) {
+  return (size_t)steps * kBarWords * 4 + (size_t)(kGranWords > kGranWordsLa ? kGranWords : kGranWordsLa) * 8;
+}
+
+template <typename V, int E>
+__global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V *__restrict__ w,
+                                                             const V *__restrict__ Vb, size_t stride, int col,
+                                                             int sweeps, const double *__restrict__ part0, int P0,
+                                                             double *__restrict__ pbuf, double *__restrict__ h,
+                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
+                                                             int step, int fault_step) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int NV = E / W;
+  __shared__ double red[kMgsBlock * W];
+  __shared__ double alpha[2 * kMaxCols];  // the current group's alphas: [i * k + column]
+  __shared__ double xs[3];                // k == 1: the exchanged sums
+  __shared__ int flags[3];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // KRY_MGS_FAULT (tests)
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  auto abort_step = [&]() {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+  };
+  // the block's segment of every vector through a buffer descriptor (no
+  // per-granule address registers; out-of-range elements read as 0, so they
+  // add 0 to every partial, and their stores are dropped), laid out as in
+  // gm_mgsp_kernel: granule u of thread tid = elements (u B + tid) W ...
+  const int64_t seg = (int64_t)NV * kMgsBlock * W;
+  const int64_t e0 = (int64_t)blockIdx.x * seg;
+  int colv[W];  // the column of element v of every granule (strides are multiples of 1024 >= k)
+#pragma unroll
+  for (int v = 0; v < W; ++v) colv[v] = (tid * W + v) & (k - 1);
+  V wr[NV][W], sa[NV][W], sb[NV][W], ta[NV][W], tb[NV][W];
+  auto ld = [&](const V *src, V(&dst)[NV][W]) {
+    const BufSeg<V, kMgsBlock> sg(src, e0, N, seg);
+#pragma unroll
+    for (int u = 0; u < NV; ++u) sg.template load<W>(u, dst[u]);
+  };
+  const int np = sweeps * (col + 1);
+  const int ng = la_groups(np);
+  auto vec_of = [&](int m) -> const V * { return Vb + stride * (size_t)(m % (col + 1)); };
+  auto ld_group = [&](int t) {  // group t's vectors into ta, tb
+    const int sz = la_size(t, np);
+    if (sz >= 1) ld(vec_of(la_first(t)), ta);
+    if (sz == 2) ld(vec_of(la_first(t) + 1), tb);
+  };
+  ld(w, wr);
+  ld(Vb, sa);
+  ld_group(1);
+  reduce_rows<kMgsBlock, false>(part0, P0, k, red);  // alpha_0 = <V_0, w> from the SpMV's partials
+  if (tid < k) alpha[tid] = red[tid];
+  __syncthreads();
+  for (int t = 0; t < ng; ++t) {
+    const int sS = la_size(t, np), sT = la_size(t + 1, np);
+    const int m0 = la_first(t);
+    if (blockIdx.x == 0 && tid < k) {  // h[j] += alpha_j (arnoldi.py:160-161)
+      for (int i = 0; i < sS; ++i) {
+        const int m = m0 + i, j = m % (col + 1);
+        const V a = (V)alpha[i * k + tid];
+        const V prev = m <= col ? V(0) : (V)h[(int64_t)j * k + tid];
+        h[(int64_t)j * k + tid] = (double)(prev + a);
+      }
+    }
+    double acc[3][W];
+#pragma unroll
+    for (int n = 0; n < 3; ++n)
+#pragma unroll
+      for (int v = 0; v < W; ++v) acc[n][v] = 0.0;
+    V a1[W], a2[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      a1[v] = (V)alpha[colv[v]];
+      a2[v] = (V)alpha[k + colv[v]];
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        wr[u][v] = wr[u][v] - a1[v] * sa[u][v];
+        if (sS == 2) wr[u][v] = wr[u][v] - a2[v] * sb[u][v];
+        const double b = (double)wr[u][v];
+        if (sT == 0) {
+          acc[0][v] += dterm(b, b);
+        } else {
+          acc[0][v] += dterm((double)ta[u][v], b);
+          if (sT == 2) {
+            acc[1][v] += dterm((double)tb[u][v], b);
+            acc[2][v] += dterm((double)tb[u][v], (double)ta[u][v]);
+          }
+        }
+      }
+    }
+    if (sT) {  // group t + 1 becomes the next pass's subtrahends
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+          sa[u][v] = ta[u][v];
+          sb[u][v] = tb[u][v];
+        }
+    }
+    const int nval = sT == 2 ? 3 : 1;
+    double pv[3] = {0.0, 0.0, 0.0};  // k == 1: the block partials, in wave 0
+    if (k == 1) {
+      double t3[3];
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        t3[n] = acc[n][0];
+#pragma unroll
+        for (int v = 1; v < W; ++v) t3[n] += acc[n][v];
+      }
+      if (nval == 3) {
+        block_sumn_t0_dpp<3>(t3, red + kMgsBlock);
+      } else {
+        double t1[1] = {t3[0]};
+        block_sumn_t0_dpp<1>(t1, red + kMgsBlock);
+        t3[0] = t1[0];
+      }
+#pragma unroll
+      for (int n = 0; n < 3; ++n) pv[n] = t3[n];
+    }
+    if (t == ng - 1) {  // <w, w> partials for the QR kernel; w back to HBM
+      double *slot = pbuf + (size_t)6 * G * k;
+      if (k == 1) {
+        if (tid == 0) slot[blockIdx.x] = pv[0];
+      } else {
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < W; ++v) red[tid * W + v] = acc[0][v];
+        block_tree_reduce(red, kMgsBlock * W, k);
+        if (tid < k) slot[(int64_t)blockIdx.x * k + tid] = red[tid];
+      }
+      const BufSeg<V, kMgsBlock> ws(w, e0, N, seg);
+#pragma unroll
+      for (int u = 0; u < NV; ++u) ws.template store<W>(u, wr[u]);
+      return;
+    }
+    if (k == 1) {  // granule all-gather of the block partials
+      unsigned long long *gr = gran + (size_t)(t & 1) * 3 * 2 * G;
+      const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(t + 1);
+      if (tid == 0) {
+        if (nval == 3) publish_partials_n<3>(gr, G, tag, pv);
+        else publish_partials_n<1>(gr, G, tag, pv);
+      }
+      ld_group(t + 2);  // travels during the wait
+      // wave v sweeps value v's granules (one wave's poll state each, as in
+      // the one-value kernels)
+      if (tid < 64 * nval) {
+        const int v = tid >> 6;
+        const bool ok = sweep_partials_n<1>(gr + (size_t)2 * v * G, G, tag, bar, ctrl, xs + v, spin_limit);
+        if ((tid & 63) == 0) flags[v] = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!(flags[0] && (nval == 1 || (flags[1] && flags[2])))) return abort_step();
+      if (tid == 0) {
+        const V aa = (V)xs[0];
+        alpha[0] = xs[0];
+        if (nval == 3) alpha[1] = xs[1] - (double)aa * xs[2];
+      }
+      __syncthreads();
+      continue;
+    }
+    double *slot = pbuf + (size_t)(t & 1) * 3 * G * k;
+    for (int n = 0; n < nval; ++n) {
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < W; ++v) red[tid * W + v] = acc[n][v];
+      block_tree_reduce(red, kMgsBlock * W, k);
+      if (tid < k) st_agent(slot + ((int64_t)n * G + blockIdx.x) * k + tid, red[tid]);
+    }
+    mgs_arrive(bar, (unsigned)(t + 1));
+    ld_group(t + 2);
+    if (!mgs_wait(bar, (unsigned)(t + 1), ctrl, &flag, spin_limit)) return abort_step();
+    double xv[3] = {0.0, 0.0, 0.0};
+    for (int n = 0; n < nval; ++n) {
+      reduce_rows<kMgsBlock, true>(slot + (int64_t)n * G * k, G, k, red);
+      if (tid < k) xv[n] = red[tid];
+      __syncthreads();
+    }
+    if (tid < k) {
+      const V aa = (V)xv[0];
+      alpha[tid] = xv[0];
+      if (nval == 3) alpha[k + tid] = xv[1] - (double)aa * xv[2];
+    }
     __syncthreads();
   }
 }
@@ -1322,6 +1537,15 @@ template <int NV>
 constexpr int mgsl_u() {
   return NV >= 32 ? 2 : 4;
 }
+// the two-vector lookahead MGS (gm_mgsp2_kernel): default; KRY_MGS_LOOKAHEAD=0
+// restores the one-exchange-per-pass form
+inline bool mgs_lookahead() {
+  static const bool on = [] {
+    const char *e = getenv("KRY_MGS_LOOKAHEAD");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 template <typename V>
 bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int step) {
   const int64_t N = s->n * (int64_t)s->k;
@@ -1343,9 +1567,10 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
         return G <= ncu && G <= 256 && per_cu >= 1 && (int64_t)s->sweeps * (s->maxiter + 1) < 4095;
       };
       // (E = 32 doubles per thread would spill: float only)
-      if (fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
-      else if (fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
-      else if (sizeof(V) == 4 && fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
+      if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 8>, 8) : fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
+      else if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 16>, 16) : fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
+      else if (sizeof(V) == 4 && (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 32>, 32) : fits(gm_mgsp_kernel<V, 32>, 32)))
+        s->mgsp_E = 32;
       else if (!(e && atoi(e) == 1)) {  // KRY_MGS_PERSIST=1: the register-resident kernel only
         s->mgsp_large = true;
         if (fits(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>, 12 * W)) s->mgsp_E = 12 * W;
@@ -1411,6 +1636,10 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>(), false>); break;
       default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>(), false>); break;
     }
+  } else if (mgs_lookahead()) {
+    if (E == 8) go(gm_mgsp2_kernel<V, 8>);
+    else if (E == 16) go(gm_mgsp2_kernel<V, 16>);
+    else if constexpr (sizeof(V) == 4) go(gm_mgsp2_kernel<V, 32>);
   } else if (E == 8) {
     go(gm_mgsp_kernel<V, 8>);
   } else if (E == 16) {
@@ -1420,7 +1649,8 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   }
   KRY_HIP(hipGetLastError());
   s->mgsp_grid = s->mgsp_norm ? 1 : G;  // normalising: the exchanged sum, one row
-  s->mgsp_out = pbuf + (size_t)2 * G * s->k;
+  // the <w, w> partials: slot 2 of the one-value kernels, slot 6 of the lookahead's three-value parities
+  s->mgsp_out = pbuf + (size_t)((!s->mgsp_large && mgs_lookahead()) ? 6 : 2) * G * s->k;
   return true;
 }
 

@@ -265,6 +265,79 @@ __device__ inline bool sweep_partials(unsigned long long *gr, int G, unsigned ta
   return true;
 }
 
+// sweep_partials<false, true> for NVAL doubles per block (the lookahead MGS
+// kernels exchange <V_a, w>, <V_b, w> and <V_b, V_a> at once): value v of
+// block b is the granule pair gr[2 (v G + b)], gr[2 (v G + b) + 1], read with
+// one 16-B load; the exchange completes when every value's tags match. Each
+// value is summed in sweep_partials' order (lane l: blocks l, l + 64, ...,
+// then wave_sum_dpp), so NVAL = 1 gives its bits; out[v] in lane 0.
+template <int NVAL>
+__device__ inline bool sweep_partials_n(unsigned long long *gr, int G, unsigned tag, unsigned *bar, Ctrl *ctrl,
+                                        double *out, unsigned spin_limit = kSpinLimit) {
+  const int lane = threadIdx.x & 63;  // any one wave
+  const __amdgpu_buffer_rsrc_t rs = granule_rsrc(gr, NVAL * G);
+  granule_u4 g[NVAL][4];
+  bool got[NVAL][4];
+#pragma unroll
+  for (int v = 0; v < NVAL; ++v)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      got[v][i] = lane + 64 * i >= G;
+      g[v][i] = granule_u4{0u, 0u, 0u, 0u};
+    }
+  unsigned spins = 0;
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    asm volatile("" ::: "memory");  // a fresh poll every round: the loads are not hoisted
+#pragma unroll
+    for (int v = 0; v < NVAL; ++v)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (!got[v][i]) g[v][i] = poll_granule(rs, v * G + lane + 64 * i);
+    bool ok = true;
+#pragma unroll
+    for (int v = 0; v < NVAL; ++v)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!got[v][i]) got[v][i] = g[v][i].y == tag && g[v][i].w == tag;
+        ok = ok && got[v][i];
+      }
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    ++spins;
+    if ((spins & 255u) == 0) {
+      if (__hip_atomic_load(bar + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+      if (spin_expired(t0, spin_limit)) {
+        if (lane == 0) {
+          __hip_atomic_store(bar + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ctrl->status, (int32_t)KRY_EDEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return false;
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NVAL; ++v) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = lane + 64 * i;
+      if (b < G)
+        s += __longlong_as_double((long long)(((unsigned long long)g[v][i].z << 32) | (unsigned long long)g[v][i].x));
+    }
+    s = wave_sum_dpp(s);
+    if (lane == 0) out[v] = s;
+  }
+  return true;
+}
+
+// Publish NVAL doubles of this block (sweep_partials_n's layout); one lane.
+template <int NVAL>
+__device__ __forceinline__ void publish_partials_n(unsigned long long *gr, int G, unsigned tag, const double *v) {
+#pragma unroll
+  for (int n = 0; n < NVAL; ++n) publish_partial(gr + 2 * ((size_t)n * G + blockIdx.x), tag, v[n]);
+}
+
 // Deterministic block sum for one column: each wave sums by a fixed xor
 // butterfly (lane 0's value is used), one barrier, then wave 0 adds the wave
 // sums by a fixed butterfly over lanes 0..nwaves-1 (blockDim <= 1024). The result is
@@ -294,6 +367,23 @@ __device__ __forceinline__ double block_sum1_t0_dpp(double v, double *wsum) {
   double s = 0.0;
   if (wv == 0) s = wave_sum_dpp(lane < (int)(blockDim.x >> 6) ? wsum[lane] : 0.0);
   return s;
+}
+// block_sum1_t0_dpp for NVAL values at once (one barrier); wsum holds
+// NVAL * 16 doubles. Each value's bits are block_sum1_t0_dpp's; valid in
+// every lane of wave 0.
+template <int NVAL>
+__device__ __forceinline__ void block_sumn_t0_dpp(double (&v)[NVAL], double *wsum) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int n = 0; n < NVAL; ++n) {
+    v[n] = wave_sum_dpp(v[n]);
+    if (lane == 0) wsum[n * 16 + wv] = v[n];
+  }
+  __syncthreads();
+  if (wv == 0) {
+#pragma unroll
+    for (int n = 0; n < NVAL; ++n) v[n] = wave_sum_dpp(lane < (int)(blockDim.x >> 6) ? wsum[n * 16 + lane] : 0.0);
+  }
 }
 __device__ __forceinline__ void block_sum1(double v, double *wsum, double *out) {
   const double s = block_sum1_t0(v, wsum);

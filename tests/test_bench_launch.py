@@ -97,3 +97,8 @@ def test_bench_gpus_2_without_devices_fails_loudly():
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
     assert '"value"' not in r.stdout
+
+
+def test_threads_launch_forced_at_one_gpu():
+    p = bench.plan_launch(1, {}, _count(1), "threads")
+    assert p["mode"] == "threads" and p["world"] == 1 and p["devices"] == [0]

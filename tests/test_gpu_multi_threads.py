@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 def _bits(a, b):
     a, b = np.asarray(a), np.asarray(b)
     assert a.shape == b.shape and a.dtype == b.dtype, (a.shape, b.shape, a.dtype, b.dtype)
-    np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+    np.testing.assert_array_equal(a.reshape(-1).view(np.uint8), b.reshape(-1).view(np.uint8))
 
 
 def _threads(fns, timeout=120):

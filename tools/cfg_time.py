@@ -25,7 +25,7 @@ elif cfg == "gmres_metric":
     print(cfg, bench.run_gmres(problems.stencil15_3d(m), f"metric {m}^3 GMRES(30)"), flush=True)
 elif cfg == "metric":
     A = problems.stencil15_3d(216)
-    r = bench.run_cg_bench(A, np.ones(A.shape[0]), 200, 20, 1, 0, 0, None)
+    r = bench.run_cg_bench(A, lambda _r: np.ones(A.shape[0]), 200, 20, bench.Job.single())
     print(cfg, {"it_per_s": 200 / r["elapsed"], "spmv_ms": 1e3 * r["spmv_avg_s"]}, flush=True)
 elif cfg == "gmres_cfg3":
     print(cfg, bench.run_gmres(), flush=True)
