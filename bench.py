@@ -716,32 +716,7 @@ def run_minres_cfg5(steps=100):
     return out
 
 
-PMC_SUMMARY = "r03b_pmc_traffic.json"
 GATHER_CEILING = "r04_gather_ceiling.json"
-
-
-def pmc_traffic(n, nnz, kernel):
-    """HBM bytes per launch of a CG SpMV kernel from the committed PMC summary
-    (tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE passes, read side
-    calibrated on a same-width stream of known size), if it was taken on this
-    workload and this kernel. PMC needs its own rocprofv3 runs, so it cannot be
-    live here."""
-    path = os.path.join(REPO, "profiles", PMC_SUMMARY)
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except OSError:
-        return {}
-    if d.get("n") != n or d.get("nnz") != nnz:
-        return {}
-    key = ("dia" if kernel.startswith("spmv_dia_kernel") else
-           "pair" if kernel.startswith("spmv_pair_kernel") else "sell")
-    k = d.get("kernels", {}).get(key)
-    if not k:
-        return {}
-    return {"traffic_bytes_per_launch": k["traffic_bytes_per_launch"],
-            "source": "profiles/%s[%s] (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, read side x%.3f calibrated)"
-                      % (PMC_SUMMARY, key, d["read_scale_from_calibration"])}
 
 
 def cpu_baseline(A_host, runs=5, target_run_s=3.0):
@@ -802,7 +777,7 @@ def run_spmv_general(A_host, steps):
             os.environ["KRY_SPMV_DIA"] = prev
     assert not res["layout"]["dia"]
     n, nnz = A_host.shape[0], int(A_host.nnz)
-    roof = roofline_of(res, n, nnz, pmc_traffic(n, nnz, spmv_kernel_desc(res["layout"], n)[0]))
+    roof = roofline_of(res, n, nnz)
     roof["cg_it_per_s"] = steps / res["elapsed"]
     roof["n"], roof["nnz"] = n, nnz
     return roof
@@ -831,16 +806,15 @@ def run_spmv_unstructured(A_host, steps):
     return roof
 
 
-TRAFFIC_INDEX = "r05_traffic_index.json"
+TRAFFIC_INDEX = "r06_traffic_index.json"
 FORMULAS = "profiles/bench_formulas.md"
 
 
 def traffic_index():
     """Per-leg HBM traffic per launch from the committed PMC summaries
     (profiles/<TRAFFIC_INDEX>, built by tools/traffic_index.py from the
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes named in it): {leg: {kernel
-    key: {"bytes": B, "src": file}}}. Each entry is kept only when it was
-    taken on the same matrix (n, nnz)."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_legs.sh): {leg:
+    {kernel key: {"bytes": B, "src": file, "build": stamp}}}."""
     try:
         with open(os.path.join(REPO, "profiles", TRAFFIC_INDEX)) as f:
             return json.load(f)
@@ -849,8 +823,14 @@ def traffic_index():
 
 
 def leg_traffic(idx, leg, key, n, nnz):
-    e = idx.get(leg, {}).get(key)
-    if not e or e.get("n") != n or e.get("nnz") != nnz:
+    """(bytes, source) of one leg's kernel, or (None, None) unless the entry
+    was taken on the same matrix (n, nnz) AND on the library build that is
+    loaded now (kry_build_id): a PMC of other code is not evidence for this
+    one, so the line then says traffic: null."""
+    from krylov_amd import _lib
+
+    e = idx.get(leg, {}).get(key) if isinstance(idx.get(leg), dict) else None
+    if not e or e.get("n") != n or e.get("nnz") != nnz or e.get("build") != _lib.build_id():
         return None, None
     return e["bytes"], e["src"]
 
@@ -870,9 +850,9 @@ def _short(kernel):
 def _kroof(r, traffic=None, src=None):
     """Compact form of one kernel roofline object."""
     out = {"kernel": _short(r["kernel"]), "ms": _r(r["ms_per_launch"]), "bytes": int(r["bytes_per_launch"]),
-           "frac": _r(r["frac"], 3), "traffic": int(traffic) if traffic else r.get("traffic")}
-    if out["traffic"] and (src or r.get("traffic_source")):
-        out["traffic_src"] = (src or r.get("traffic_source", "")).split(" ")[0]
+           "frac": _r(r["frac"], 3), "traffic": int(traffic) if traffic else None}
+    if out["traffic"] and src:
+        out["traffic_src"] = src.split(" ")[0]
     return out
 
 
@@ -1018,9 +998,11 @@ def main():
     rhs = res["rhs"]
     if args.workload == "cfg4":
         roof, it_roof = cfg4_rooflines(res, steps_timed)
+        t, src = leg_traffic(traffic_index(), "cfg4", "spmv", hn, hnnz)
+        roof["traffic"], roof["traffic_source"] = t, src
     else:
-        kname = spmv_kernel_desc(res["layout"], hn)[0]
-        roof = roofline_of(res, hn, hnnz, pmc_traffic(hn, hnnz, kname))
+        t, src = leg_traffic(traffic_index(), "metric_cg", "spmv", hn, hnnz)
+        roof = roofline_of(res, hn, hnnz, {"traffic_bytes_per_launch": t, "source": src} if t else None)
         # the iteration: the SpMV's image bytes + the one-launch update
         # (cg_upd_kernel: r, y, p read and written, Ap read = 7 n 8 B)
         it_b = roof["bytes_per_launch"] + 7 * hn * 8

@@ -1461,15 +1461,15 @@ static void launch_alpha(kry_cg *s, const double *partA, int PA, double *scratch
   KRY_HIP(hipGetLastError());
 }
 
-// Returns true when the chunk ran as one persistent launch.
-template <typename V, typename MV, typename I>
-bool cg_run_impl(kry_cg *s, int max_steps) {
-  hipStream_t st = s->ctx->stream;
+// Deferred yk updates on the block path (KRY_CG_YDEFER = D, 0 = off): the
+// ring of D p buffers is chosen and allocated once per solver, by
+// kry_cg_start (setup, not the iteration loop), and every buffer is written
+// once there (hipMemsetAsync): the first kernel to write a fresh multi-GB
+// allocation pays for mapping its pages (cfg4: a 2.2 ms first p pass against
+// ~0.39 ms, profiles/r05_cfg4_kernel_stats.csv), which then happens before
+// the solve's first iteration.
+static void cg_ydefer_setup(kry_cg *s) {
   const int k = s->k;
-  const int64_t N = s->n * (int64_t)k;
-  if (cgp_launch<V, MV, I>(s, max_steps)) return true;
-  double *partA = s->part, *partB = s->part + part_rows(k) * k;
-  // deferred yk updates on the block path (KRY_CG_YDEFER = D, 0 = off)
   if (s->ydefer < 0) {
     s->ydefer = 0;
     const char *e = getenv("KRY_CG_YDEFER");
@@ -1504,6 +1504,7 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       try {
         for (int q = 1; q <= D; ++q) s->pring[q] = dev_alloc(vb);
         s->alpha_ring = static_cast<double *>(dev_alloc((size_t)D * k * 8));
+        for (int q = 1; q <= D; ++q) KRY_HIP(hipMemsetAsync(s->pring[q], 0, vb, s->ctx->stream));
         s->ydefer = D;
         s->ydefer_bytes = (int64_t)D * (int64_t)vb + (int64_t)D * k * 8;
       } catch (const Error &err) {
@@ -1515,6 +1516,17 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       }
     }
   }
+}
+
+// Returns true when the chunk ran as one persistent launch.
+template <typename V, typename MV, typename I>
+bool cg_run_impl(kry_cg *s, int max_steps) {
+  hipStream_t st = s->ctx->stream;
+  const int k = s->k;
+  const int64_t N = s->n * (int64_t)k;
+  if (cgp_launch<V, MV, I>(s, max_steps)) return true;
+  double *partA = s->part, *partB = s->part + part_rows(k) * k;
+  cg_ydefer_setup(s);  // normally done by kry_cg_start already
   const int D = (!s->M && k <= 8) ? s->ydefer : 0;
   PRing<V> ring{};
   if (D) {
@@ -1740,6 +1752,7 @@ int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
   KRY_HIP(hipMemsetAsync(s->y, 0, vb, st));
   KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
   s->it = 0;
+  cg_ydefer_setup(s);
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
   // p0 = M_Ml_r0 (cg.py:138)
   KRY_HIP(hipMemcpyAsync(s->p, s->M ? s->z : s->r, vb, hipMemcpyDeviceToDevice, st));

@@ -71,6 +71,9 @@ struct kry_gmres {
   int mgsp_grid = 0;
   int mgsp_fallbacks = 0;  // chunks finished launch per pass after a persistent MGS timeout
   double *mgsp_out = nullptr;  // <w, w> partials of the last persistent pass
+  unsigned long long *mgs_tbuf = nullptr;  // KRY_MGS_TRACE phase sums (256 blocks x 4)
+  int64_t mgs_tpasses = 0;
+  int mgs_tgrid = 0;
   int chunk_cap = 0;
   int steps = 0;           // Arnoldi iterations done (arnoldi.iter)
   bool invariant = false;
@@ -298,12 +301,25 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
                                                             int sweeps, const double *__restrict__ part0, int P0,
                                                             double *__restrict__ pbuf, double *__restrict__ h,
                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
-                                                            int step, int fault_step) {
+                                                            int step, int fault_step,
+                                                            unsigned long long *tbuf = nullptr) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int NV = E / W;
   __shared__ double red[kMgsBlock * W];
   __shared__ double alpha[kMaxCols];
+  // optional phase trace (KRY_MGS_TRACE): thread 0's wall-clock split of the
+  // passes into compute (incl. the wait for the prefetched vectors), block
+  // reduction + publish, exchange wait
+  __shared__ unsigned long long tacc[4];
+  auto tmark = [&](int ph) {
+    if (tbuf && threadIdx.x == 0) {
+      const unsigned long long now = wall_clock64();
+      if (ph >= 0) tacc[ph] += now - tacc[3];
+      tacc[3] = now;
+    }
+  };
+  if (tbuf && threadIdx.x == 0) tacc[0] = tacc[1] = tacc[2] = 0;
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int G = gridDim.x;
@@ -338,6 +354,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
   reduce_rows<kMgsBlock, false>(part0, P0, k, red);
   if (tid < k) alpha[tid] = red[tid];
   __syncthreads();
+  tmark(-1);
   for (int p = 0; p < np; ++p) {
     const int j = p % (col + 1);
     const bool first_sweep = p <= col;
@@ -364,6 +381,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
         }
       }
     }
+    tmark(0);
     if (q) {  // V_{j+1} becomes the next pass's subtrahend
 #pragma unroll
       for (int u = 0; u < NV; ++u)
@@ -391,12 +409,16 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
       }
 #pragma unroll
       for (int u = 0; u < NV; ++u) VIO<V>::store(w, (base + (int64_t)u * kMgsBlock + tid) * W, N, wr[u]);
+      tmark(1);
+      if (tbuf && tid == 0)
+        for (int q3 = 0; q3 < 3; ++q3) tbuf[blockIdx.x * 4 + q3] += tacc[q3];
       return;
     }
     if (k == 1) {  // granule all-gather of the block partials
       unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
       const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
       if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
+      tmark(1);
       if (const V *q2 = next_of(p + 1)) ld(q2, vn);
       if (tid < 64) {
         const bool ok = sweep_partials<false, true>(gr, G, tag, bar, ctrl, alpha, spin_limit);
@@ -404,6 +426,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
       }
       __syncthreads();
       if (!flag) return abort_step();
+      tmark(2);
       continue;
     }
     if (tid < k) st_agent(slot + (int64_t)blockIdx.x * k + tid, red[tid]);
@@ -452,10 +475,23 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
                                                              int sweeps, const double *__restrict__ part0, int P0,
                                                              double *__restrict__ pbuf, double *__restrict__ h,
                                                              unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
-                                                             int step, int fault_step) {
+                                                             int step, int fault_step,
+                                                             unsigned long long *tbuf = nullptr) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   constexpr int NV = E / W;
+  __shared__ unsigned long long tacc[4];  // phase trace (KRY_MGS_TRACE), as gm_mgsp_kernel's
+  auto tmark = [&](int ph) {
+    if (tbuf && threadIdx.x == 0) {
+      const unsigned long long now = wall_clock64();
+      if (ph >= 0) tacc[ph] += now - tacc[3];
+      tacc[3] = now;
+    }
+  };
+  if (tbuf && threadIdx.x == 0) tacc[0] = tacc[1] = tacc[2] = 0;
+  // the current pass's subtrahends, per-thread storage (each thread reads back
+  // only what it wrote: no barrier): registers hold w and the partners only
+  __shared__ __attribute__((aligned(16))) V sub[2][NV][kMgsBlock * W];
   __shared__ double red[kMgsBlock * W];
   __shared__ double alpha[2 * kMaxCols];  // the current group's alphas: [i * k + column]
   __shared__ double xs[3];                // k == 1: the exchanged sums
@@ -477,7 +513,19 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
   int colv[W];  // the column of element v of every granule (strides are multiples of 1024 >= k)
 #pragma unroll
   for (int v = 0; v < W; ++v) colv[v] = (tid * W + v) & (k - 1);
-  V wr[NV][W], sa[NV][W], sb[NV][W], ta[NV][W], tb[NV][W];
+  V wr[NV][W], ta[NV][W], tb[NV][W];
+  typedef V vec_t __attribute__((ext_vector_type(W)));
+  auto sub_ld = [&](int i, int u, V(&o)[W]) {
+    const vec_t t = *reinterpret_cast<const vec_t *>(&sub[i][u][tid * W]);
+#pragma unroll
+    for (int v = 0; v < W; ++v) o[v] = t[v];
+  };
+  auto sub_st = [&](int i, int u, const V(&o)[W]) {
+    vec_t t;
+#pragma unroll
+    for (int v = 0; v < W; ++v) t[v] = o[v];
+    *reinterpret_cast<vec_t *>(&sub[i][u][tid * W]) = t;
+  };
   auto ld = [&](const V *src, V(&dst)[NV][W]) {
     const BufSeg<V, kMgsBlock> sg(src, e0, N, seg);
 #pragma unroll
@@ -492,11 +540,14 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
     if (sz == 2) ld(vec_of(la_first(t) + 1), tb);
   };
   ld(w, wr);
-  ld(Vb, sa);
+  ld(Vb, ta);  // V_0, the first pass's subtrahend
+#pragma unroll
+  for (int u = 0; u < NV; ++u) sub_st(0, u, ta[u]);
   ld_group(1);
   reduce_rows<kMgsBlock, false>(part0, P0, k, red);  // alpha_0 = <V_0, w> from the SpMV's partials
   if (tid < k) alpha[tid] = red[tid];
   __syncthreads();
+  tmark(-1);
   for (int t = 0; t < ng; ++t) {
     const int sS = la_size(t, np), sT = la_size(t + 1, np);
     const int m0 = la_first(t);
@@ -521,10 +572,13 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
     }
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
+      V sa[W], sb[W];
+      sub_ld(0, u, sa);
+      if (sS == 2) sub_ld(1, u, sb);
 #pragma unroll
       for (int v = 0; v < W; ++v) {
-        wr[u][v] = wr[u][v] - a1[v] * sa[u][v];
-        if (sS == 2) wr[u][v] = wr[u][v] - a2[v] * sb[u][v];
+        wr[u][v] = wr[u][v] - a1[v] * sa[v];
+        if (sS == 2) wr[u][v] = wr[u][v] - a2[v] * sb[v];
         const double b = (double)wr[u][v];
         if (sT == 0) {
           acc[0][v] += dterm(b, b);
@@ -537,14 +591,13 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
         }
       }
     }
+    tmark(0);
     if (sT) {  // group t + 1 becomes the next pass's subtrahends
 #pragma unroll
-      for (int u = 0; u < NV; ++u)
-#pragma unroll
-        for (int v = 0; v < W; ++v) {
-          sa[u][v] = ta[u][v];
-          sb[u][v] = tb[u][v];
-        }
+      for (int u = 0; u < NV; ++u) {
+        sub_st(0, u, ta[u]);
+        if (sT == 2) sub_st(1, u, tb[u]);
+      }
     }
     const int nval = sT == 2 ? 3 : 1;
     double pv[3] = {0.0, 0.0, 0.0};  // k == 1: the block partials, in wave 0
@@ -580,6 +633,9 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
       const BufSeg<V, kMgsBlock> ws(w, e0, N, seg);
 #pragma unroll
       for (int u = 0; u < NV; ++u) ws.template store<W>(u, wr[u]);
+      tmark(1);
+      if (tbuf && tid == 0)
+        for (int q3 = 0; q3 < 3; ++q3) tbuf[blockIdx.x * 4 + q3] += tacc[q3];
       return;
     }
     if (k == 1) {  // granule all-gather of the block partials
@@ -589,6 +645,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
         if (nval == 3) publish_partials_n<3>(gr, G, tag, pv);
         else publish_partials_n<1>(gr, G, tag, pv);
       }
+      tmark(1);
       ld_group(t + 2);  // travels during the wait
       // wave v sweeps value v's granules (one wave's poll state each, as in
       // the one-value kernels)
@@ -605,6 +662,7 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp2_kernel(int64_t N, int k, V
         if (nval == 3) alpha[1] = xs[1] - (double)aa * xs[2];
       }
       __syncthreads();
+      tmark(2);
       continue;
     }
     double *slot = pbuf + (size_t)(t & 1) * 3 * G * k;
@@ -893,6 +951,279 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsl_kernel(int64_t N, int k, V 
     if (!mgs_wait(bar, (unsigned)(p + 1), ctrl, &flag, spin_limit)) return abort_step();
     reduce_rows<kMgsBlock, true>(slot, G, k, red);
     if (tid < k) alpha[tid] = red[tid];
+    __syncthreads();
+  }
+}
+
+// ----------------------- streamed persistent MGS with the two-vector lookahead
+// gm_mgsl_kernel's streaming (w in registers, the basis streamed in chunks of
+// one granule per vector, chunk c + 1 loaded while chunk c is used, chunk 0
+// of the next pass loaded before the exchange) with gm_mgsp2_kernel's groups:
+// pass t streams its two subtrahends (group t) and its two partners (group
+// t + 1) and performs ONE exchange of <V_a', w>, <V_b', w>, <V_b', V_a'>. The
+// first KU granule rows of each partner are kept in LDS for its second read
+// as a subtrahend in the next pass (per-thread storage, no barrier), as the
+// one-vector kernel keeps its partner's. After the last group: the <w, w>
+// exchange and V_{k+1} = w / guard(h[k+1]) from the registers, as there.
+template <typename V, int NV, bool NT>
+__global__ __launch_bounds__(kMgsBlock) void gm_mgsl2_kernel(int64_t N, int k, V *__restrict__ w,
+                                                             const V *__restrict__ Vb, size_t stride, int col,
+                                                             int sweeps, const double *__restrict__ part0, int P0,
+                                                             double *__restrict__ pbuf, double *__restrict__ h,
+                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
+                                                             int step, int fault_step, V *__restrict__ vnext) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int KEEP = W == 2 ? 9 : 8;  // granule rows kept per partner (two partners: ~147 KiB)
+  constexpr int KU = NV < KEEP ? NV : KEEP;
+  __shared__ __attribute__((aligned(16))) V keep[2][KU][kMgsBlock * W];
+  __shared__ double red[kMgsBlock * W];
+  __shared__ double alpha[2 * kMaxCols];
+  __shared__ double xs[3];
+  __shared__ int flags[3];
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  const bool fault_here = fault_step >= 0 && (fault_step & 0xffff) == step && (int)blockIdx.x == G - 1;
+  const bool fault_final = (fault_step >> 16) == 1;
+  if (fault_here && !fault_final) return;
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  auto abort_step = [&]() {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+  };
+  const int64_t seg = (int64_t)NV * kMgsBlock * W;
+  const int64_t e0 = (int64_t)blockIdx.x * seg;
+  int colv[W];
+#pragma unroll
+  for (int v = 0; v < W; ++v) colv[v] = (tid * W + v) & (k - 1);
+  typedef BufSeg<V, kMgsBlock> Seg;
+  const Seg ws(w, e0, N, seg);
+  V wr[NV][W];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) ws.template load<W>(u, wr[u]);
+  const int np = sweeps * (col + 1);
+  const int ng = la_groups(np);
+  auto vec_of = [&](int m) -> const V * { return Vb + stride * (size_t)(m % (col + 1)); };
+  typedef V vec_t __attribute__((ext_vector_type(W)));
+  auto keep_ld = [&](int s, int g, V(&o)[W]) {
+    const vec_t t = *reinterpret_cast<const vec_t *>(&keep[s][g][tid * W]);
+#pragma unroll
+    for (int v = 0; v < W; ++v) o[v] = t[v];
+  };
+  auto keep_st = [&](int s, int g, const V(&o)[W]) {
+    vec_t t;
+#pragma unroll
+    for (int v = 0; v < W; ++v) t[v] = o[v];
+    *reinterpret_cast<vec_t *>(&keep[s][g][tid * W]) = t;
+  };
+  // chunk buffers [parity][stream][element]: streams S_a, S_b, T_a, T_b
+  V cb[2][4][W];
+  // chunk c of pass t's streams into cb[par] (the subtrahends only beyond the kept rows)
+  auto ld_chunk = [&](int t, int c, int par) {
+    const int sS = la_size(t, np), sT = la_size(t + 1, np);
+    const int m0 = la_first(t), m1 = la_first(t + 1);
+    if (c >= KU) {
+      Seg(vec_of(m0), e0, N, seg).template load<W, NT ? 2 : 0>(c, cb[par][0]);
+      if (sS == 2) Seg(vec_of(m0 + 1), e0, N, seg).template load<W, NT ? 2 : 0>(c, cb[par][1]);
+    }
+    if (sT >= 1) Seg(vec_of(m1), e0, N, seg).template load<W>(c, cb[par][2]);
+    if (sT == 2) Seg(vec_of(m1 + 1), e0, N, seg).template load<W>(c, cb[par][3]);
+  };
+  {
+    const Seg s0(Vb, e0, N, seg);
+#pragma unroll
+    for (int g = 0; g < KU; ++g) {  // V_0's kept rows
+      V t[W];
+      s0.template load<W>(g, t);
+      keep_st(0, g, t);
+    }
+    ld_chunk(0, 0, 0);
+  }
+  reduce_rows<kMgsBlock, false>(part0, P0, k, red);  // alpha_0 = <V_0, w> from the SpMV's partials
+  if (tid < k) alpha[tid] = red[tid];
+  __syncthreads();
+  for (int t = 0; t < ng; ++t) {
+    const int sS = la_size(t, np), sT = la_size(t + 1, np);
+    const int m0 = la_first(t);
+    if (blockIdx.x == 0 && tid < k) {  // h[j] += alpha_j (arnoldi.py:160-161)
+      for (int i = 0; i < sS; ++i) {
+        const int m = m0 + i, j = m % (col + 1);
+        const V a = (V)alpha[i * k + tid];
+        const V prev = m <= col ? V(0) : (V)h[(int64_t)j * k + tid];
+        h[(int64_t)j * k + tid] = (double)(prev + a);
+      }
+    }
+    V a1[W], a2[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      a1[v] = (V)alpha[colv[v]];
+      a2[v] = (V)alpha[k + colv[v]];
+    }
+    double acc[3][W];
+#pragma unroll
+    for (int n = 0; n < 3; ++n)
+#pragma unroll
+      for (int v = 0; v < W; ++v) acc[n][v] = 0.0;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int b = c & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < NV) ld_chunk(t, c + 1, b ^ 1);
+      V sa[W], sb[W];
+      if (c < KU) {
+        keep_ld(0, c, sa);
+        if (sS == 2) keep_ld(1, c, sb);
+        if (sT >= 1) keep_st(0, c, cb[b][2]);  // the next pass's subtrahends
+        if (sT == 2) keep_st(1, c, cb[b][3]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+          sa[v] = cb[b][0][v];
+          sb[v] = cb[b][1][v];
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        wr[c][v] = wr[c][v] - a1[v] * sa[v];
+        if (sS == 2) wr[c][v] = wr[c][v] - a2[v] * sb[v];
+        const double x = (double)wr[c][v];
+        if (sT == 0) {
+          acc[0][v] += dterm(x, x);
+        } else {
+          acc[0][v] += dterm((double)cb[b][2][v], x);
+          if (sT == 2) {
+            acc[1][v] += dterm((double)cb[b][3][v], x);
+            acc[2][v] += dterm((double)cb[b][3][v], (double)cb[b][2][v]);
+          }
+        }
+        asm volatile("" : "+v"(acc[0][v]));  // the accumulation in program order (see gm_mgsl_kernel)
+      }
+    }
+    const int nval = sT == 2 ? 3 : 1;
+    double pv[3] = {0.0, 0.0, 0.0};
+    if (k == 1) {
+      double t3[3];
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        t3[n] = acc[n][0];
+#pragma unroll
+        for (int v = 1; v < W; ++v) t3[n] += acc[n][v];
+      }
+      if (nval == 3) {
+        block_sumn_t0_dpp<3>(t3, red + kMgsBlock);
+      } else {
+        double t1[1] = {t3[0]};
+        block_sumn_t0_dpp<1>(t1, red + kMgsBlock);
+        t3[0] = t1[0];
+      }
+#pragma unroll
+      for (int n = 0; n < 3; ++n) pv[n] = t3[n];
+    }
+    if (t == ng - 1) {
+      double *tot = pbuf + (size_t)6 * G * k;
+      if (vnext == nullptr) {  // <w, w> partials for the QR kernel; w back to HBM
+        if (k == 1) {
+          if (tid == 0) tot[blockIdx.x] = pv[0];
+        } else {
+          __syncthreads();
+#pragma unroll
+          for (int v = 0; v < W; ++v) red[tid * W + v] = acc[0][v];
+          block_tree_reduce(red, kMgsBlock * W, k);
+          if (tid < k) tot[(int64_t)blockIdx.x * k + tid] = red[tid];
+        }
+#pragma unroll
+        for (int u = 0; u < NV; ++u) ws.template store<W>(u, wr[u]);
+        return;
+      }
+      // the <w, w> exchange, h[k+1] and its guard as the QR kernel forms
+      // them, and V_{k+1} = w / guard(h[k+1]) from the registers
+      // (arnoldi.py:185,191-196); the QR kernel reads the sum as one row
+      if (fault_here) return;  // KRY_MGS_FAULT_FINAL: never joins the normalising exchange
+      if (k == 1) {
+        unsigned long long *gr = gran + (size_t)(t & 1) * 3 * 2 * G;
+        const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(t + 1);
+        if (tid == 0) publish_partials_n<1>(gr, G, tag, pv);
+        if (tid < 64) {
+          const bool ok = sweep_partials_n<1>(gr, G, tag, bar, ctrl, xs, spin_limit);
+          if (tid == 0) {
+            flag = ok ? 1 : 0;
+            alpha[0] = xs[0];
+          }
+        }
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(flag)) return abort_step();
+      } else {
+        double *xsl = pbuf + (size_t)(t & 1) * 3 * G * k;
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < W; ++v) red[tid * W + v] = acc[0][v];
+        block_tree_reduce(red, kMgsBlock * W, k);
+        if (tid < k) st_agent(xsl + (int64_t)blockIdx.x * k + tid, red[tid]);
+        mgs_arrive(bar, (unsigned)(t + 1));
+        if (!mgs_wait(bar, (unsigned)(t + 1), ctrl, &flag, spin_limit)) return abort_step();
+        reduce_rows<kMgsBlock, true>(xsl, G, k, red);
+        if (tid < k) alpha[tid] = red[tid];
+        __syncthreads();
+      }
+      if (blockIdx.x == 0 && tid < k) tot[tid] = alpha[tid];
+      V hs[W];
+#pragma unroll
+      for (int v = 0; v < W; ++v) hs[v] = safe<V>(sqrt((V)alpha[colv[v]]));
+      const Seg vs(vnext, e0, N, seg);
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        V o[W];
+#pragma unroll
+        for (int v = 0; v < W; ++v) o[v] = wr[u][v] / hs[v];
+        vs.template store<W>(u, o);
+      }
+      return;
+    }
+    if (k == 1) {  // granule all-gather of the block partials, one wave per value
+      unsigned long long *gr = gran + (size_t)(t & 1) * 3 * 2 * G;
+      const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(t + 1);
+      if (tid == 0) {
+        if (nval == 3) publish_partials_n<3>(gr, G, tag, pv);
+        else publish_partials_n<1>(gr, G, tag, pv);
+      }
+      ld_chunk(t + 1, 0, 0);  // chunk 0 of the next pass travels during the wait
+      if (tid < 64 * nval) {
+        const int v = tid >> 6;
+        const bool ok = sweep_partials_n<1>(gr + (size_t)2 * v * G, G, tag, bar, ctrl, xs + v, spin_limit);
+        if ((tid & 63) == 0) flags[v] = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!(flags[0] && (nval == 1 || (flags[1] && flags[2])))) return abort_step();
+      if (tid == 0) {
+        const V aa = (V)xs[0];
+        alpha[0] = xs[0];
+        if (nval == 3) alpha[1] = xs[1] - (double)aa * xs[2];
+      }
+      __syncthreads();
+      continue;
+    }
+    double *slot = pbuf + (size_t)(t & 1) * 3 * G * k;
+    for (int n = 0; n < nval; ++n) {
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < W; ++v) red[tid * W + v] = acc[n][v];
+      block_tree_reduce(red, kMgsBlock * W, k);
+      if (tid < k) st_agent(slot + ((int64_t)n * G + blockIdx.x) * k + tid, red[tid]);
+    }
+    mgs_arrive(bar, (unsigned)(t + 1));
+    ld_chunk(t + 1, 0, 0);
+    if (!mgs_wait(bar, (unsigned)(t + 1), ctrl, &flag, spin_limit)) return abort_step();
+    double xv[3] = {0.0, 0.0, 0.0};
+    for (int n = 0; n < nval; ++n) {
+      reduce_rows<kMgsBlock, true>(slot + (int64_t)n * G * k, G, k, red);
+      if (tid < k) xv[n] = red[tid];
+      __syncthreads();
+    }
+    if (tid < k) {
+      const V aa = (V)xv[0];
+      alpha[tid] = xv[0];
+      if (nval == 3) alpha[k + tid] = xv[1] - (double)aa * xv[2];
+    }
     __syncthreads();
   }
 }
@@ -1537,12 +1868,24 @@ template <int NV>
 constexpr int mgsl_u() {
   return NV >= 32 ? 2 : 4;
 }
-// the two-vector lookahead MGS (gm_mgsp2_kernel): default; KRY_MGS_LOOKAHEAD=0
-// restores the one-exchange-per-pass form
+// The two-vector lookahead MGS (gm_mgsp2_kernel / gm_mgsl2_kernel) is
+// opt-in: KRY_MGS_LOOKAHEAD=1 (register-resident kernel), KRY_MGSL_LOOKAHEAD=1
+// (streamed kernel). Both measured slower than the one-exchange-per-pass
+// forms on one box, alternating processes (profiles/r06_mgs_lookahead_ab.txt):
+// cfg3 0.100 against 0.082 ms per step, the metric 0.405 against 0.356 ms
+// (its two partners share the LDS room one partner had, so it re-reads more
+// of the basis).
 inline bool mgs_lookahead() {
   static const bool on = [] {
     const char *e = getenv("KRY_MGS_LOOKAHEAD");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+inline bool mgsl_lookahead() {
+  static const bool on = [] {
+    const char *e = getenv("KRY_MGSL_LOOKAHEAD");
+    return e && atoi(e) == 1;
   }();
   return on;
 }
@@ -1569,15 +1912,26 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       // (E = 32 doubles per thread would spill: float only)
       if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 8>, 8) : fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
       else if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 16>, 16) : fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
-      else if (sizeof(V) == 4 && (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 32>, 32) : fits(gm_mgsp_kernel<V, 32>, 32)))
-        s->mgsp_E = 32;
-      else if (!(e && atoi(e) == 1)) {  // KRY_MGS_PERSIST=1: the register-resident kernel only
+      else if constexpr (sizeof(V) == 4) {
+        if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 32>, 32) : fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
+      }
+      if (s->mgsp_E == 0 && !(e && atoi(e) == 1)) {  // KRY_MGS_PERSIST=1: the register-resident kernel only
         s->mgsp_large = true;
-        if (fits(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>, 12 * W)) s->mgsp_E = 12 * W;
-        else if (fits(gm_mgsl_kernel<V, 16, mgsl_u<16>(), true>, 16 * W)) s->mgsp_E = 16 * W;
-        else if (fits(gm_mgsl_kernel<V, 24, mgsl_u<24>(), true>, 24 * W)) s->mgsp_E = 24 * W;
-        else if (fits(gm_mgsl_kernel<V, 32, mgsl_u<32>(), true>, 32 * W)) s->mgsp_E = 32 * W;
-        else if (fits(gm_mgsl_kernel<V, 40, mgsl_u<40>(), true>, 40 * W)) s->mgsp_E = 40 * W;
+        const bool la = mgsl_lookahead();
+        if (la ? fits(gm_mgsl2_kernel<V, 12, true>, 12 * W) : fits(gm_mgsl_kernel<V, 12, mgsl_u<12>(), true>, 12 * W))
+          s->mgsp_E = 12 * W;
+        else if (la ? fits(gm_mgsl2_kernel<V, 16, true>, 16 * W)
+                    : fits(gm_mgsl_kernel<V, 16, mgsl_u<16>(), true>, 16 * W))
+          s->mgsp_E = 16 * W;
+        else if (la ? fits(gm_mgsl2_kernel<V, 24, true>, 24 * W)
+                    : fits(gm_mgsl_kernel<V, 24, mgsl_u<24>(), true>, 24 * W))
+          s->mgsp_E = 24 * W;
+        else if (la ? fits(gm_mgsl2_kernel<V, 32, true>, 32 * W)
+                    : fits(gm_mgsl_kernel<V, 32, mgsl_u<32>(), true>, 32 * W))
+          s->mgsp_E = 32 * W;
+        else if (la ? fits(gm_mgsl2_kernel<V, 40, true>, 40 * W)
+                    : fits(gm_mgsl_kernel<V, 40, mgsl_u<40>(), true>, 40 * W))
+          s->mgsp_E = 40 * W;
         else s->mgsp_large = false;
       }
     }
@@ -1594,9 +1948,20 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   const char *fe = getenv("KRY_MGS_FAULT");  // fault injection (tests): chunk step at which a block drops out
   const char *ff = getenv("KRY_MGS_FAULT_FINAL");  // ... at the streamed kernel's final exchange instead
   const int fault_step = fe ? (atoi(fe) | ((ff && atoi(ff) == 1) ? (1 << 16) : 0)) : -1;
+  // KRY_MGS_TRACE: per-block phase sums of the register-resident kernels,
+  // accumulated over the solver's launches and printed at its destroy
+  static const bool trace = getenv("KRY_MGS_TRACE") != nullptr;
+  if (trace && !s->mgs_tbuf) {
+    KRY_HIP(hipMalloc(&s->mgs_tbuf, 256 * 4 * 8));
+    KRY_HIP(hipMemsetAsync(s->mgs_tbuf, 0, 256 * 4 * 8, st));
+  }
+  if (trace) {
+    s->mgs_tpasses += (int64_t)(mgs_lookahead() ? (1 + s->sweeps * (col + 1) / 2) : s->sweeps * (col + 1));
+    s->mgs_tgrid = G;
+  }
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(G), dim3(kMgsBlock), 0, st, N, s->k, w, (const V *)s->V, s->vstride, col, s->sweeps,
-                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step);
+                       pin, Pin, pbuf, s->h, bar, gran, s->ctrl, step, fault_step, s->mgs_tbuf);
   };
   // the streamed kernel also normalises: V_{col+1} = w / guard(h[col+1])
   V *vnext = basis<V>(s->V, s->vstride, col + 1);
@@ -1615,7 +1980,16 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   }();
   bool u4 = false;
   if constexpr (sizeof(V) == 8) u4 = s->mgsp_large && mgsl_nt && mgsl_u_env == 4 && E / W >= 32;
-  if (u4) {
+  const bool la = s->mgsp_large ? mgsl_lookahead() : mgs_lookahead();
+  if (s->mgsp_large && la) {
+    switch (E / W) {
+      case 12: gol(gm_mgsl2_kernel<V, 12, true>); break;
+      case 16: gol(gm_mgsl2_kernel<V, 16, true>); break;
+      case 24: gol(gm_mgsl2_kernel<V, 24, true>); break;
+      case 32: gol(gm_mgsl2_kernel<V, 32, true>); break;
+      default: gol(gm_mgsl2_kernel<V, 40, true>); break;
+    }
+  } else if (u4) {
     if constexpr (sizeof(V) == 8) {
       if (E / W == 32) gol(gm_mgsl_kernel<V, 32, 4, true>);
       else gol(gm_mgsl_kernel<V, 40, 4, true>);
@@ -1636,7 +2010,7 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>(), false>); break;
       default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>(), false>); break;
     }
-  } else if (mgs_lookahead()) {
+  } else if (la) {
     if (E == 8) go(gm_mgsp2_kernel<V, 8>);
     else if (E == 16) go(gm_mgsp2_kernel<V, 16>);
     else if constexpr (sizeof(V) == 4) go(gm_mgsp2_kernel<V, 32>);
@@ -1650,7 +2024,7 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
   KRY_HIP(hipGetLastError());
   s->mgsp_grid = s->mgsp_norm ? 1 : G;  // normalising: the exchanged sum, one row
   // the <w, w> partials: slot 2 of the one-value kernels, slot 6 of the lookahead's three-value parities
-  s->mgsp_out = pbuf + (size_t)((!s->mgsp_large && mgs_lookahead()) ? 6 : 2) * G * s->k;
+  s->mgsp_out = pbuf + (size_t)(la ? 6 : 2) * G * s->k;
   return true;
 }
 
@@ -1938,6 +2312,20 @@ int kry_gmres_destroy(kry_gmres *s) {
   if (!s) return KRY_OK;
   (void)hipSetDevice(s->ctx->device);
   (void)hipStreamSynchronize(s->ctx->stream);
+  if (s->mgs_tbuf) {  // KRY_MGS_TRACE: mean over blocks of the per-pass phase times
+    unsigned long long h[256 * 4];
+    if (hipMemcpy(h, s->mgs_tbuf, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess && s->mgs_tgrid > 0) {
+      double sum[3] = {0, 0, 0};
+      for (int b = 0; b < s->mgs_tgrid; ++b)
+        for (int q = 0; q < 3; ++q) sum[q] += (double)h[b * 4 + q];
+      const double np = (double)(s->mgs_tpasses > 0 ? s->mgs_tpasses : 1);
+      fprintf(stderr, "mgs trace G=%d passes=%lld (us/pass, mean over blocks): compute %.2f reduce+publish %.2f xwait %.2f\n",
+              s->mgs_tgrid, (long long)s->mgs_tpasses, sum[0] * 0.01 / s->mgs_tgrid / np,
+              sum[1] * 0.01 / s->mgs_tgrid / np, sum[2] * 0.01 / s->mgs_tgrid / np);
+    }
+    (void)hipFree(s->mgs_tbuf);
+    s->mgs_tbuf = nullptr;
+  }
   gm_free(s);
   delete s;
   KRY_API_END

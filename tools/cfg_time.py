@@ -1,6 +1,7 @@
-"""One secondary BASELINE config on its own, for a kernel trace:
-`python tools/cfg_time.py metric|cfg4|cfg5|cfg2|gmres_cfg3 [steps]` or `gmres_metric [m]` (run under
-`rocprofv3 --kernel-trace --stats` to split an iteration by kernel)."""
+"""One bench leg on its own, for a kernel trace or a PMC pass:
+`python tools/cfg_time.py metric|general|unstructured|cfg4|cfg5|cfg2|gmres_cfg3|bicgstab_cfg3 [steps]` or
+`gmres_metric [m]` (run under `rocprofv3 --kernel-trace --stats` to split an iteration by kernel, or under
+tools/pmc_legs.sh for the traffic index)."""
 import os
 import sys
 
@@ -29,3 +30,12 @@ elif cfg == "metric":
     print(cfg, {"it_per_s": 200 / r["elapsed"], "spmv_ms": 1e3 * r["spmv_avg_s"]}, flush=True)
 elif cfg == "gmres_cfg3":
     print(cfg, bench.run_gmres(), flush=True)
+elif cfg == "general":  # the metric matrix on the paired-row image (KRY_SPMV_DIA=0), bench's spmv_general
+    r = bench.run_spmv_general(problems.stencil15_3d(216), steps)
+    print(cfg, {"it_per_s": r["cg_it_per_s"], "spmv_ms": r["spmv_ms"]}, flush=True)
+elif cfg == "unstructured":  # the permuted metric (renumbered, rank-sorted image), bench's spmv_unstructured
+    r = bench.run_spmv_unstructured(problems.stencil15_3d(216), steps)
+    print(cfg, {"it_per_s": r["cg_it_per_s"], "spmv_ms": r["ms_per_launch"]}, flush=True)
+elif cfg == "bicgstab_cfg3":
+    r = bench.run_bicgstab(problems.random_nonsym(2_000_000), steps)
+    print(cfg, {"it_per_s": r["it_per_s"], "spmv_ms": r["roofline"]["ms_per_launch"]}, flush=True)

@@ -14,7 +14,7 @@ from krylov_amd import problems  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 A = problems.stencil15_3d(216)
-r = bench.run_cg_bench(A, np.ones(A.shape[0]), steps, 0, 1, 0, 0, None, roofline_launches=1)
+r = bench.run_cg_bench(A, lambda _r: np.ones(A.shape[0]), steps, 0, bench.Job.single(), roofline_launches=1)
 print("dia", r["layout"]["dia"], "spmv_ms", 1e3 * r["spmv_avg_s"], flush=True)
 g = bench.run_spmv_general(A, steps)
 print("general", g["kernel"].split(" ")[0], "spmv_ms", g["spmv_ms"], flush=True)
