@@ -47,6 +47,14 @@ struct kry_cg {
   Ctrl *ctrl = nullptr;
   int chunk_cap = 0;
   int64_t it = 0;
+  // deferred yk (ydefer = D > 0): the ring is indexed by the GLOBAL step
+  // (p_g in pring[g % (D + 1)], alpha_g in alpha_ring[g % D]) across run
+  // calls, so a chunk's end costs nothing: y holds every update below yfb,
+  // the in-kernel flushes fall every D steps from yfb, and the ones pending
+  // at a chunk's end are applied only when the host needs y (cg_ydefer_flush:
+  // kry_cg_get x, kry_cg_residual). it_base: the global step of a run's step 0
+  int64_t yfb = 0;
+  int64_t it_base = 0;
   bool started = false;
   // multi-GPU
   kry_comm *comm = nullptr;
@@ -355,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
                                                            const V *__restrict__ r, const double *__restrict__ part,
                                                            int P, double *scal, double *alpha_ring, double *hist,
                                                            Ctrl *ctrl, int step, double *gbuf, int col_offset,
-                                                           int total_k) {
+                                                           int total_k, int64_t gstep, int64_t fb) {
   if (halted(ctrl, step)) return;
   constexpr int W = Vec16<V>::W;
   __shared__ double red[kBlock];
@@ -364,7 +372,8 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const bool flush = (step + 1) % D == 0;
+  // gstep: this step's global index; flushes fall every D steps from fb
+  const bool flush = (gstep + 1 - fb) % D == 0;
   const int nf = flush ? D : 0;
   reduce_partials(part, P, k, red);
   if (tid < k) {
@@ -373,12 +382,12 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
     const S om = rr / safe<S>(old);
     sh_om[tid] = (double)om;
     const double a = scal[S_ALPHA * k + tid];
-    for (int q = 0; q + 1 < nf; ++q) sh_a[q][tid] = alpha_ring[(int64_t)((step - nf + 1 + q) % D) * k + tid];
+    for (int q = 0; q + 1 < nf; ++q) sh_a[q][tid] = alpha_ring[((gstep - nf + 1 + q) % D) * k + tid];
     if (nf) sh_a[nf - 1][tid] = a;
     const S nrm = sqrt(rr);
     rn[tid] = (double)nrm;
     if (g == 0) {
-      alpha_ring[(int64_t)(step % D) * k + tid] = a;
+      alpha_ring[(gstep % D) * k + tid] = a;
       scal[S_RHO_PREV * k + tid] = (double)old;
       scal[S_RHO * k + tid] = (double)rr;
       scal[S_OMEGA * k + tid] = (double)om;
@@ -386,8 +395,8 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
     }
   }
   __syncthreads();
-  const V *pi = ring.s[step % (D + 1)];
-  V *pn = ring.s[(step + 1) % (D + 1)];
+  const V *pi = ring.s[gstep % (D + 1)];
+  V *pn = ring.s[(gstep + 1) % (D + 1)];
   const int64_t ngrp = (N + W - 1) / W;
   const int64_t per = ((ngrp + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
   const int64_t v0 = per * g;
@@ -402,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
       VIO<V>::load_nt(y, e, N, yv);
       for (int q = 0; q < nf; ++q) {
         V pj[W];
-        if (q + 1 < nf) VIO<V>::load_nt(ring.s[(step - nf + 1 + q) % (D + 1)], e, N, pj);
+        if (q + 1 < nf) VIO<V>::load_nt(ring.s[(gstep - nf + 1 + q) % (D + 1)], e, N, pj);
 #pragma unroll
         for (int u = 0; u < W; ++u) {
           const V a = (V)sh_a[q][(int)((e + u) & (k - 1))];
@@ -432,59 +441,22 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
   }
 }
 
-// The end of a chunk on the deferred path: m = min(stop_at, steps) steps ran;
-// the updates of steps (m / D) D .. m - 1 are still pending (yk += alpha_j
-// p_j in order), and p_m sits in ring buffer m % (D + 1), copied to p
-// (pring[0]) for the next chunk. Not halted by ctrl (it reads it).
-template <typename V>
-struct OpCgYFlush {
-  V *y;
-  PRing<V> ring;
-  int D;
-  const double *alpha_ring;
-  const Ctrl *ctrl;
-  int steps, k;
-  __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
-    constexpr int W = Vec16<V>::W;
-    const int m = ctrl->stop_at < steps ? ctrl->stop_at : steps;
-    const int j0 = m / D * D;
-    if (j0 < m) {
-      V yv[W];
-      VIO<V>::load_nt(y, e, N, yv);
-      for (int j = j0; j < m; ++j) {
-        V pj[W];
-        VIO<V>::load(ring.s[j % (D + 1)], e, N, pj);
-#pragma unroll
-        for (int u = 0; u < W; ++u) {
-          const V a = (V)alpha_ring[(int64_t)(j % D) * k + (int)((e + u) & (k - 1))];
-          const V t1 = a * pj[u];
-          yv[u] = yv[u] + t1;
-        }
-      }
-      VIO<V>::store_nt(y, e, N, yv);
-    }
-    if (m % (D + 1) != 0) {
-      V pv[W];
-      VIO<V>::load(ring.s[m % (D + 1)], e, N, pv);
-      VIO<V>::store(ring.s[0], e, N, pv);
-    }
-  }
-};
-
-// yk += alpha_j p_j for j = j0 .. j1 - 1 in order (cg.py:196): the deferred
-// updates of a flushing step of the one-launch update path.
+// yk += alpha_j p_j for global steps j = j0 .. j1 - 1 in order (cg.py:196):
+// the deferred updates of a flushing step of the one-launch update path, and
+// those pending when the host needs y (cg_ydefer_flush).
 template <typename V>
 struct OpCgYSteps {
   V *y;
   PRing<V> ring;
   int D;
   const double *alpha_ring;
-  int j0, j1, k;
+  int64_t j0, j1;
+  int k;
   __device__ __forceinline__ void operator()(int64_t e, int64_t N, double (&)[Vec16<V>::W]) const {
     constexpr int W = Vec16<V>::W;
     V yv[W];
     VIO<V>::load_nt(y, e, N, yv);
-    for (int j = j0; j < j1; ++j) {
+    for (int64_t j = j0; j < j1; ++j) {
       V pj[W];
       VIO<V>::load_nt(ring.s[j % (D + 1)], e, N, pj);
 #pragma unroll
@@ -648,7 +620,7 @@ __global__ __launch_bounds__(kUpdBlock) void cg_upd_kernel(int64_t N, V *__restr
   }
   if (blockIdx.x == 0) {
     if (tid == 0) {
-      if (DEF) alpha_ring[step % D] = (double)alpha;
+      if (DEF) alpha_ring[0] = (double)alpha;  // the host passes this step's slot
       scal[S_ALPHA] = (double)alpha;
       scal[S_RHO_OLD] = (double)rho;
       scal[S_RHO_PREV] = (double)rho;
@@ -1400,9 +1372,10 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf, 
   const char *fl = getenv("KRY_CGU_FAULT_LATE");  // ... or joins late (decide_exchange tests)
   if (fault_step >= 0 && fl) fault_step |= (atoi(fl) & 0x7fff) << 16;
   V *y = static_cast<V *>(s->y), *r = static_cast<V *>(s->r);
-  V *p = D ? ring.s[step % (D + 1)] : static_cast<V *>(s->p);
-  V *pout = D ? ring.s[(step + 1) % (D + 1)] : p;
-  double *alpha_ring = s->alpha_ring;
+  const int64_t gstep = s->it_base + step;
+  V *p = D ? ring.s[gstep % (D + 1)] : static_cast<V *>(s->p);
+  V *pout = D ? ring.s[(gstep + 1) % (D + 1)] : p;
+  double *alpha_ring = D ? s->alpha_ring + gstep % D : s->alpha_ring;  // this step's slot
   int Dv = D ? D : 1;
   const V *Ap = static_cast<const V *>(s->Ap);
   double *scal = s->scal, *hist = s->hist;
@@ -1423,9 +1396,9 @@ bool cgu_launch(kry_cg *s, const double *partA, int PA, int step, double *gbuf, 
     ProfScope ps(s->ctx, PROF_UPDATE);
     le = hipLaunchKernel(kern(nv, D != 0), dim3(G), dim3(kUpdBlock), args, 0, st);
   }
-  if (le == hipSuccess && D && (step + 1) % D == 0) {  // the D deferred yk updates of steps step - D + 1 .. step
+  if (le == hipSuccess && D && (gstep + 1 - s->yfb) % D == 0) {  // the D deferred updates of steps gstep - D + 1 .. gstep
     ProfScope ps(s->ctx, PROF_OTHER);
-    launch_elementwise<V>(N, 1, OpCgYSteps<V>{y, ring, D, s->alpha_ring, step - D + 1, step + 1, 1}, nullptr, ctrl,
+    launch_elementwise<V>(N, 1, OpCgYSteps<V>{y, ring, D, s->alpha_ring, gstep - D + 1, gstep + 1, 1}, nullptr, ctrl,
                           step, st);
   }
   if (le != hipSuccess) {
@@ -1534,7 +1507,8 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
     for (int q = 1; q <= D; ++q) ring.s[q] = static_cast<V *>(s->pring[q]);
   }
   for (int step = 0; step < max_steps; ++step) {
-    V *p = D ? ring.s[step % (D + 1)] : static_cast<V *>(s->p);
+    const int64_t gstep = s->it_base + step;
+    V *p = D ? ring.s[gstep % (D + 1)] : static_cast<V *>(s->p);
     int PA, PB;
     {
       ProfScope ps(s->ctx, PROF_SPMV);
@@ -1567,11 +1541,11 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
         if (s->scalar_f32)
           hipLaunchKernelGGL((cg_pdefer_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
                              ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
-                             step, gb, s->col_offset, s->total_k);
+                             step, gb, s->col_offset, s->total_k, gstep, s->yfb);
         else
           hipLaunchKernelGGL((cg_pdefer_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
                              ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
-                             step, gb, s->col_offset, s->total_k);
+                             step, gb, s->col_offset, s->total_k, gstep, s->yfb);
       } else if (s->scalar_f32)
         hipLaunchKernelGGL((cg_yp_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
                            static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,
@@ -1623,13 +1597,24 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       KRY_HIP(hipGetLastError());
     }
   }
-  if (D) {  // the pending yk updates, and p_m back into p (skipped when no step ran)
-    ProfScope ps(s->ctx, PROF_OTHER);
-    launch_elementwise<V>(N, k,
-                          OpCgYFlush<V>{static_cast<V *>(s->y), ring, D, s->alpha_ring, s->ctrl, max_steps, k},
-                          nullptr, s->ctrl, 0, st);
-  }
-  return false;
+  return false;  // (deferred yk: the updates pending now wait for cg_ydefer_flush)
+}
+
+// The deferred yk updates still pending (global steps yfb .. it - 1), applied
+// in step order when the host needs y: then y is bitwise what one update per
+// step gives. Nothing to do off the deferred path.
+template <typename V>
+void cg_ydefer_flush(kry_cg *s) {
+  const int D = (!s->M && s->k <= 8) ? s->ydefer : 0;
+  if (D <= 0 || s->yfb >= s->it) return;
+  PRing<V> ring{};
+  ring.s[0] = static_cast<V *>(s->p);
+  for (int q = 1; q <= D; ++q) ring.s[q] = static_cast<V *>(s->pring[q]);
+  ProfScope ps(s->ctx, PROF_OTHER);
+  launch_elementwise<V>(s->n * (int64_t)s->k, s->k, OpCgYSteps<V>{static_cast<V *>(s->y), ring, D, s->alpha_ring, s->yfb,
+                                                                s->it, s->k},
+                        nullptr, nullptr, 0, s->ctx->stream);
+  s->yfb = s->it;
 }
 
 template <typename V, typename MV, typename I>
@@ -1637,6 +1622,7 @@ void cg_residual_impl(kry_cg *s, double *norm2) {
   hipStream_t st = s->ctx->stream;
   const int k = s->k;
   const int64_t N = s->n * (int64_t)k;
+  cg_ydefer_flush<V>(s);
   launch_elementwise<V>(N, k, OpXk<V>{static_cast<const V *>(s->x0), static_cast<const V *>(s->y), static_cast<V *>(s->xk)},
                         nullptr, nullptr, 0, st);
   // explicit ||M Ml (b - A xk)||: t and z are free between iterations
@@ -1752,6 +1738,8 @@ int kry_cg_start(kry_cg *s, kry_vec *b, kry_vec *x0, kry_vec *w, double *rho0) {
   KRY_HIP(hipMemsetAsync(s->y, 0, vb, st));
   KRY_HIP(hipMemsetAsync(s->xk, 0, vb, st));
   s->it = 0;
+  s->yfb = 0;
+  s->it_base = 0;
   cg_ydefer_setup(s);
   dispatch_vmi(s->dtype, s->A->dtype, s->A->itype, [&](auto v0, auto m0, auto i0) { cg_start_impl<decltype(v0), decltype(m0), decltype(i0)>(s); });
   // p0 = M_Ml_r0 (cg.py:138)
@@ -1798,6 +1786,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     return {read_chunk(s->ctx, st, s->ctrl, s->hist, steps, hk, rows, c), persistent};
   };
   auto run_chunk = [&](Ctrl *c) { return run_steps(max_steps, resnorms, c); };
+  s->it_base = s->it;
   Ctrl c;
   auto [done, persistent] = run_chunk(&c);
   bool upd = s->upd_used;
@@ -1835,6 +1824,7 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
     s->upd_nv = 0;
     ++s->upd_fallbacks;
     const int first = done;
+    s->it_base = s->it + first;
     auto [more, pers2] = run_steps(max_steps - first, resnorms + (size_t)first * hk, &c);
     (void)pers2;
     done = first + more;
@@ -1843,6 +1833,8 @@ int kry_cg_run(kry_cg *s, int32_t max_steps, int32_t *steps_done, double *resnor
   s->cgp_last = persistent;
   s->upd_last = upd;
   s->it += done;
+  if (s->ydefer > 0 && !s->M && s->k <= 8 && !persistent)  // the in-kernel flushes of this run
+    s->yfb += (s->it - s->yfb) / s->ydefer * s->ydefer;
   *steps_done = done;
   KRY_API_END
 }
@@ -1902,6 +1894,8 @@ int kry_cg_get(kry_cg *s, int which, void *host) {
   hipStream_t st = s->ctx->stream;
   const int64_t N = s->n * (int64_t)s->k;
   if (which == 0) {
+    if (s->dtype == KRY_F64) cg_ydefer_flush<double>(s);
+    else cg_ydefer_flush<float>(s);
     if (s->dtype == KRY_F64)
       launch_elementwise<double>(N, s->k, OpXk<double>{static_cast<const double *>(s->x0), static_cast<const double *>(s->y), static_cast<double *>(s->xk)},
                                  nullptr, nullptr, 0, st);

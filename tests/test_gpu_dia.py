@@ -253,8 +253,9 @@ def test_dia_block_cg_matches_lane_group_and_oracle(golden, monkeypatch):
 @pytest.mark.parametrize("case", ["poisson2d_300_f64", "lap3d_f32", "poisson_weighted", "banded_general", "Ml"])
 def test_block_cg_deferred_y_bitwise(case, D, monkeypatch):
     """Block CG with yk += alpha p deferred and applied D steps at a time
-    (cg_pdefer_kernel, p cycling through D + 1 buffers, OpCgYFlush at each
-    chunk's end) against one update per step (KRY_CG_YDEFER=0): the same
+    (cg_pdefer_kernel, p cycling through D + 1 buffers indexed by the global
+    step across chunks; the updates pending at a chunk's end applied when the
+    host reads y, cg_ydefer_flush) against one update per step (KRY_CG_YDEFER=0): the same
     roundings in the same order, so the history, the iterate and the step
     count are bitwise equal, for chunks of 1, 7, 32, 1 and 19 steps (ends
     that fall before, on and after a flush), a solve stopping in the middle
@@ -392,11 +393,11 @@ def _hip_free_bytes():
 
 
 def test_block_cg_ring_depth_follows_free_memory(monkeypatch):
-    """The default ring is sized by what is free when the solver first runs
-    (a quarter of it, and at most 10 GB): with a balloon allocated next to
-    the solver so that about 2.5 GB stay free, the 144 MB block gets D = 3
-    (3 x 144 MB fit 625 MB, 7 x 144 MB do not) and still iterates bitwise as
-    one update per step."""
+    """The default ring is sized by what is free when the solver starts
+    (kry_cg_start: a quarter of it, and at most 10 GB): with a balloon
+    allocated next to the solver so that about 2.5 GB stay free, the 144 MB
+    block gets D = 3 (3 x 144 MB fit 625 MB, 7 x 144 MB do not) and still
+    iterates bitwise as one update per step."""
     import krylov_amd
     from krylov_amd import _helpers, problems
     from krylov_amd.cg import _CGState
@@ -407,19 +408,22 @@ def test_block_cg_ring_depth_follows_free_memory(monkeypatch):
     B = np.random.default_rng(7).standard_normal((P.shape[0], 8))
     A = krylov_amd.CsrOperator(P)
 
-    def solve():
+    def solve(start=True):
         st = _CGState(_helpers.Problem(A, B, None, None))
-        st.start()
-        st.set_criterion(np.zeros(8))
+        if start:
+            st.start()
+            st.set_criterion(np.zeros(8))
         return st
 
-    st = solve()
+    st = solve(start=False)
     krylov_amd.empty_cache()
     keep = int(2.5 * 2**30)
     free = _hip_free_bytes()
     assert free > keep + 2**30
     balloon = DeviceVector(A.ctx, (free - keep) // 8, 1, np.float64)
     try:
+        st.start()
+        st.set_criterion(np.zeros(8))
         h = st.run(12)
         D, _ = st.defer_info()
         assert D == 3

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Kernel trace of one secondary config (tools/cfg_time.py CFG STEPS) under
 # rocprofv3 --kernel-trace --stats; output gpurun_out/prof_CFG/.
-#   tools/prof_cfg.sh CFG [STEPS]
+#   [PROF_TAG=t] tools/prof_cfg.sh CFG [STEPS]   (PROF_TAG: a suffix for the output directory)
 CFG=$1; STEPS=${2:-20}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$CFG
+OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$CFG${PROF_TAG:+_$PROF_TAG}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- \
