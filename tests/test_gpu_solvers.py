@@ -516,7 +516,8 @@ def test_restarted_gmres_variants_match_oracle_chaining(case):
     preconditioner (criterion 1e-8 ||Ml b|| / ||Ml (b - A x_c)||), with a
     WeightedInner (both norms in <., .>_w, device kry_dot) and with a callback
     (the host download of each cycle's x_in), against the same x0-chaining of
-    the oracle (restart 15)."""
+    the oracle (restart 15), and, for every case but the callback, against the
+    reference's own chain (tests/golden/make_restart_variants.py) at 1e-10."""
     import krylov_amd
     from oracle import krylov_ref as K
     from tests import solver_cases
@@ -564,6 +565,20 @@ def test_restarted_gmres_variants_match_oracle_chaining(case):
     ref = np.array(hist)
     assert got.shape == ref.shape
     np.testing.assert_allclose(got[:-1], ref[:-1], rtol=1e-9)
+    if case != "callback":
+        # the reference's own chain (tests/golden/restart_variants.npz, made by
+        # running the reference: parity pinned, not only the oracle's)
+        import os
+
+        d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "restart_variants.npz"))
+        assert [i.numsteps for i in infos] == d[f"{case}_steps"].tolist()
+        rref = d[f"{case}_hist"]
+        assert got.shape == rref.shape
+        np.testing.assert_allclose(got[:-1], rref[:-1], rtol=1e-10)
+        xr = d[f"{case}_x"]
+        np.testing.assert_allclose(x, xr, rtol=0, atol=1e-9 * np.abs(xr).max())
+        print(f"\nrestart {case}: {len(infos)} cycles, history max rel vs the reference "
+              f"{np.max(np.abs(got[:-1] - rref[:-1]) / np.abs(rref[:-1])):.2e}")
     if case == "callback":
         assert len(calls) == len(ocalls) > 0
         for (gx, gr), (ox, orr) in zip(calls, ocalls):

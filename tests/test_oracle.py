@@ -225,3 +225,28 @@ def test_oracle_fullsize_cfg3_restart_chain():
     np.testing.assert_allclose(hist, F["cfg3_gmres30_restart_hist"], rtol=1e-12, atol=0)
     idx = np.sort(np.random.default_rng(12345).choice(R.shape[0], int(F["nsample"]), replace=False))
     np.testing.assert_allclose(x[idx], F["cfg3_gmres30_restart_xsample"], rtol=1e-11, atol=0)
+
+
+@pytest.mark.parametrize("case", ["Mr", "block3", "householder", "x0", "Ml", "weighted"])
+def test_oracle_restart_variants_match_reference(case):
+    """The oracle's x0-chained GMRES(15) with Mr / a block / Householder / x0
+    / Ml / a weighted inner against the reference's own chain
+    (tests/golden/restart_variants.npz, make_restart_variants.py)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_restart_variants import case_setup, chain
+
+    from oracle import krylov_ref as K
+    from tests import solver_cases
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "restart_variants.npz"))
+    q = solver_cases.inputs()
+    b, x0, kw, norm = case_setup(case, q)
+    if "inner_w" in kw:
+        w = kw.pop("inner_w")
+        kw["inner"] = lambda x, y: np.dot(x.T, w * y)
+    hist, steps, x = chain(K.gmres, q["R"], b, x0, kw, norm)
+    np.testing.assert_array_equal(steps, d[f"{case}_steps"])
+    np.testing.assert_allclose(hist, d[f"{case}_hist"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(x, d[f"{case}_x"], rtol=0, atol=1e-10 * np.abs(d[f"{case}_x"]).max())
