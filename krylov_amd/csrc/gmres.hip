@@ -441,6 +441,234 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp_kernel(int64_t N, int k, V 
   }
 }
 
+// ------------------------ persistent MGS, next vector two passes ahead (k = 1)
+// gm_mgsp_kernel's passes, exchanges and sums (bitwise the same results), with
+// the partner of pass p + 1 already on chip when pass p's exchange ends: each
+// wave copies its rows of the partner of pass p + 2 into LDS with
+// buffer_load ... lds (no VGPRs) during pass p's exchange, so the copy has a
+// whole pass to land instead of the exchange's few microseconds, and reads
+// them into registers at the start of pass p + 1 after a counted vmcnt wait
+// for the older copy only. Wave 0, which polls the exchange, issues its copy
+// after the exchange (its polls would otherwise wait behind it: vmcnt counts
+// in order). The barriers that may have a copy in flight are raw s_barriers
+// with lgkmcnt waits only: __syncthreads would drain every copy.
+// a workgroup barrier that leaves vector-memory copies in flight
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// The same copy issued from inline asm: the compiler then does not know the
+// LDS is written by a pending vector-memory op, and does not put vmcnt(0)
+// before the kernel's LDS reads (its tracking cannot tell the copy's rows
+// from alpha / red); the kernel waits for the copies itself, with counted
+// vmcnt. desc: {base lo, base hi, bytes, 0x00020000} (no stride), lds: the
+// wave's LDS byte address (m0), voff: the lane's byte offset, soff: the
+// granule's.
+typedef int sdesc4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_dma16_asm(sdesc4 desc, unsigned lds, int voff, int soff) {
+  int keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(desc), "s"(lds), "s"(soff)
+      : "memory");
+}
+// this thread's 16 B at LDS byte address `lds` into o (ds_read_b128; the
+// lgkmcnt wait inside, as the compiler does not track asm LDS reads)
+template <typename V, int W>
+__device__ __forceinline__ void lds_rd16_asm(unsigned lds, V (&o)[W]) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i t;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(lds) : "memory");
+  if constexpr (W == 2) {
+    const double2 d = __builtin_bit_cast(double2, t);
+    o[0] = d.x;
+    o[1] = d.y;
+  } else {
+    const float4 f = __builtin_bit_cast(float4, t);
+    o[0] = f.x;
+    o[1] = f.y;
+    o[2] = f.z;
+    o[3] = f.w;
+  }
+}
+template <typename V, int E>
+__global__ __launch_bounds__(kMgsBlock) void gm_mgsp3_kernel(int64_t N, int k, V *__restrict__ w,
+                                                             const V *__restrict__ Vb, size_t stride, int col,
+                                                             int sweeps, const double *__restrict__ part0, int P0,
+                                                             double *__restrict__ pbuf, double *__restrict__ h,
+                                                             unsigned *bar, unsigned long long *gran, Ctrl *ctrl,
+                                                             int step, int fault_step,
+                                                             unsigned long long *tbuf = nullptr) {
+  if (halted(ctrl, step)) return;
+  constexpr int W = Vec16<V>::W;
+  constexpr int NV = E / W;
+  __shared__ __attribute__((aligned(16))) V nb[2][NV][kMgsBlock * W];  // partners two passes ahead
+  __shared__ double red[kMgsBlock * W];
+  __shared__ double alpha[kMaxCols];
+  __shared__ unsigned long long tacc[4];  // phase trace (KRY_MGS_TRACE), as gm_mgsp_kernel's
+  auto tmark = [&](int ph) {
+    if (tbuf && threadIdx.x == 0) {
+      const unsigned long long now = wall_clock64();
+      if (ph >= 0) tacc[ph] += now - tacc[3];
+      tacc[3] = now;
+    }
+  };
+  if (tbuf && threadIdx.x == 0) tacc[0] = tacc[1] = tacc[2] = 0;
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  if (fault_step == step && (int)blockIdx.x == G - 1) return;  // KRY_MGS_FAULT (tests)
+  const unsigned spin_limit = fault_step >= 0 ? kSpinLimitFault : kSpinLimit;
+  auto abort_step = [&]() {
+    if (tid == 0) atomicMin(&ctrl->stop_at, step);
+  };
+  const int64_t base = (int64_t)blockIdx.x * NV * kMgsBlock;
+  V wr[NV][W], vc[NV][W], vn[NV][W];
+  auto ld = [&](const V *src, V(&dst)[NV][W]) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) VIO<V>::load(src, (base + (int64_t)u * kMgsBlock + tid) * W, N, dst[u]);
+  };
+  const int wave0 = tid & ~63;
+  // LDS byte addresses (the low 32 bits of a generic LDS address are the offset)
+  const unsigned nb0 = (unsigned)(uintptr_t)&nb[0][0][0];
+  constexpr unsigned kRow = kMgsBlock * W * sizeof(V), kBuf = NV * kRow;
+  auto dma = [&](const V *src, int buf) {  // this wave's rows of src into nb[buf] (out of range: 0)
+    const int64_t e0 = base * W;
+    const int64_t rem = N - e0, seg = (int64_t)NV * kMgsBlock * W;
+    const int64_t cnt = rem < seg ? (rem > 0 ? rem : 0) : seg;
+    const uint64_t a = reinterpret_cast<uint64_t>(src + e0);
+    sdesc4 d;
+    d.x = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    d.y = (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    d.z = __builtin_amdgcn_readfirstlane((int)(cnt * (int64_t)sizeof(V)));
+    d.w = 0x00020000;
+    const unsigned l0 = (unsigned)__builtin_amdgcn_readfirstlane(nb0 + buf * kBuf + wave0 * W * sizeof(V));
+#pragma unroll
+    for (int u = 0; u < NV; ++u)
+      lds_dma16_asm(d, __builtin_amdgcn_readfirstlane(l0 + u * kRow), tid * 16,
+                    __builtin_amdgcn_readfirstlane(u * kMgsBlock * 16));
+  };
+  auto nb_ld = [&](int buf) {  // this thread's rows of nb[buf] into vn
+#pragma unroll
+    for (int u = 0; u < NV; ++u) lds_rd16_asm<V, W>(nb0 + buf * kBuf + u * kRow + tid * W * sizeof(V), vn[u]);
+  };
+  const int np = sweeps * (col + 1);
+  auto next_of = [&](int p) -> const V * {  // the vector of pass p's inner product (null = w)
+    if (p >= np) return nullptr;
+    const int j = p % (col + 1), sw = p / (col + 1);
+    if (j < col) return Vb + stride * (size_t)(j + 1);
+    if (sw + 1 < sweeps) return Vb;
+    return nullptr;
+  };
+  // h[j] += alpha_j of pass p (arnoldi.py:160-161), block 0; issued where
+  // no copy of this wave is in flight (its load would wait behind them)
+  auto h_update = [&](int p) {
+    if (blockIdx.x == 0 && tid < k) {
+      const int j = p % (col + 1);
+      const V a = (V)alpha[tid];
+      const V prev = p <= col ? V(0) : (V)h[(int64_t)j * k + tid];
+      h[(int64_t)j * k + tid] = (double)(prev + a);
+    }
+  };
+  ld(w, wr);
+  ld(Vb, vc);
+  reduce_rows<kMgsBlock, false>(part0, P0, k, red);  // alpha_0 = <V_0, w> from the SpMV's partials
+  if (tid < k) alpha[tid] = red[tid];
+  __syncthreads();
+  h_update(0);
+  // w, V_0 and h in: only copies from here on. (s_waitcnt encodings on gfx9:
+  // vmcnt in bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8; the builtin, not
+  // inline asm, so the compiler's own wait tracking sees it)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (const V *q0 = next_of(0)) dma(q0, 0);  // the partners of passes 0 and 1
+  if (const V *q1 = next_of(1)) dma(q1, 1);
+  tmark(-1);
+  for (int p = 0; p < np; ++p) {
+    const V *q = next_of(p);
+    if (q) {
+      // this pass's partner was copied during an earlier exchange; the copy
+      // of the next pass's (NV instructions, issued since, if any) may stay
+      // in flight
+      static_assert(NV < 16, "vmcnt(NV) in the low field");
+      if (next_of(p + 1)) __builtin_amdgcn_s_waitcnt(0x0F70 | NV);
+      else __builtin_amdgcn_s_waitcnt(0x0F70);
+      nb_ld(p & 1);
+    }
+    double acc[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc[v] = 0.0;
+    const V al = (V)alpha[0];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int64_t e = (base + (int64_t)u * kMgsBlock + tid) * W;
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const V t = al * vc[u][v];
+        wr[u][v] = wr[u][v] - t;  // Av -= alpha * V[j] (arnoldi.py:162)
+        if (e + v < N) {
+          const double a = q ? (double)vn[u][v] : (double)wr[u][v];
+          const double b = (double)wr[u][v];
+          acc[v] += dterm(a, b);
+        }
+      }
+    }
+    tmark(0);
+    if (q) {  // V_{j+1} becomes the next pass's subtrahend
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+#pragma unroll
+        for (int v = 0; v < W; ++v) vc[u][v] = vn[u][v];
+    }
+    // block sum as block_sum1_t0_dpp (same tree, same bits) over a raw barrier
+    double part1 = 0.0;
+    {
+      double t = acc[0];
+#pragma unroll
+      for (int v = 1; v < W; ++v) t += acc[v];
+      t = wave_sum_dpp(t);
+      const int lane = tid & 63, wv = tid >> 6;
+      if (lane == 0) red[kMgsBlock + wv] = t;
+      raw_barrier();
+      if (wv == 0) part1 = wave_sum_dpp(lane < kMgsBlock / 64 ? red[kMgsBlock + lane] : 0.0);
+    }
+    if (p == np - 1) {  // <w, w> partials for the QR kernel; w back to HBM
+      double *slot = pbuf + (size_t)2 * G;
+      if (tid == 0) slot[blockIdx.x] = part1;
+#pragma unroll
+      for (int u = 0; u < NV; ++u) VIO<V>::store(w, (base + (int64_t)u * kMgsBlock + tid) * W, N, wr[u]);
+      tmark(1);
+      if (tbuf && tid == 0)
+        for (int q3 = 0; q3 < 3; ++q3) tbuf[blockIdx.x * 4 + q3] += tacc[q3];
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      return;
+    }
+    unsigned long long *gr = gran + (size_t)(p & 1) * 2 * G;
+    const unsigned tag = ((unsigned)(step + 1) << 12) | (unsigned)(p + 1);
+    if (tid == 0) publish_partial(gr + 2 * blockIdx.x, tag, part1);
+    tmark(1);
+    const V *q2 = next_of(p + 2);
+    if (q2 && tid >= 64) dma(q2, p & 1);  // the partner of pass p + 2 (nb[p & 1] held pass p's, now in vn / vc)
+    if (tid < 64) {
+      const bool ok = sweep_partials<false, true>(gr, G, tag, bar, ctrl, alpha, spin_limit);
+      if (tid == 0) flag = ok ? 1 : 0;
+    }
+    raw_barrier();
+    if (!flag) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // no copy left in flight when the block leaves
+      return abort_step();
+    }
+    if (tid < 64) {
+      h_update(p + 1);  // (wave 0 has no copy in flight here)
+      if (q2) dma(q2, p & 1);  // wave 0's rows, after its polls
+    }
+    tmark(2);
+  }
+}
+
 // ------------------------------ persistent MGS with a two-vector lookahead
 // The same Arnoldi step as gm_mgsp_kernel with half the dependent grid
 // exchanges. The flattened MGS index list m = 0 .. np - 1 (vector
@@ -1882,6 +2110,15 @@ inline bool mgs_lookahead() {
   }();
   return on;
 }
+// the register-resident MGS at k = 1 with the partner copied two passes
+// ahead into LDS (gm_mgsp3_kernel): default; KRY_MGS_PF2=0 restores
+// gm_mgsp_kernel (bitwise the same results). cfg3 GMRES(30): MGS 0.084 ->
+// 0.079 ms per step, 2,867 -> 2,920 it/s, same box, alternating processes
+// (profiles/r06_mgs_pf2_ab.txt)
+inline bool mgs_pf2() {
+  const char *e = getenv("KRY_MGS_PF2");  // read per launch: the tests switch it within one process
+  return !(e && atoi(e) == 0);
+}
 inline bool mgsl_lookahead() {
   static const bool on = [] {
     const char *e = getenv("KRY_MGSL_LOOKAHEAD");
@@ -1910,8 +2147,13 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
         return G <= ncu && G <= 256 && per_cu >= 1 && (int64_t)s->sweeps * (s->maxiter + 1) < 4095;
       };
       // (E = 32 doubles per thread would spill: float only)
-      if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 8>, 8) : fits(gm_mgsp_kernel<V, 8>, 8)) s->mgsp_E = 8;
-      else if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 16>, 16) : fits(gm_mgsp_kernel<V, 16>, 16)) s->mgsp_E = 16;
+      const bool pf2 = !mgs_lookahead() && s->k == 1 && mgs_pf2();
+      if (pf2 ? fits(gm_mgsp3_kernel<V, 8>, 8)
+              : (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 8>, 8) : fits(gm_mgsp_kernel<V, 8>, 8)))
+        s->mgsp_E = 8;
+      else if (pf2 ? fits(gm_mgsp3_kernel<V, 16>, 16)
+                   : (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 16>, 16) : fits(gm_mgsp_kernel<V, 16>, 16)))
+        s->mgsp_E = 16;
       else if constexpr (sizeof(V) == 4) {
         if (mgs_lookahead() ? fits(gm_mgsp2_kernel<V, 32>, 32) : fits(gm_mgsp_kernel<V, 32>, 32)) s->mgsp_E = 32;
       }
@@ -2010,6 +2252,10 @@ bool mgsp_launch(kry_gmres *s, V *w, const double *pin, int Pin, int col, int st
       case 32: gol(gm_mgsl_kernel<V, 32, mgsl_u<32>(), false>); break;
       default: gol(gm_mgsl_kernel<V, 40, mgsl_u<40>(), false>); break;
     }
+  } else if (!la && s->k == 1 && mgs_pf2()) {
+    if (E == 8) go(gm_mgsp3_kernel<V, 8>);
+    else if (E == 16) go(gm_mgsp3_kernel<V, 16>);
+    else if constexpr (sizeof(V) == 4) go(gm_mgsp3_kernel<V, 32>);
   } else if (la) {
     if (E == 8) go(gm_mgsp2_kernel<V, 8>);
     else if (E == 16) go(gm_mgsp2_kernel<V, 16>);

@@ -88,3 +88,25 @@ def test_streamed_mgs_timeout_falls_back(poisson1800, monkeypatch):
     np.testing.assert_allclose(f[:-1], c[:-1], rtol=1e-11)
     np.testing.assert_allclose(faulted.xk, clean.xk, rtol=0, atol=1e-10 * np.abs(clean.xk).max())
     assert _state_path(A, b, 1) == (False, 1)
+
+
+def test_mgs_partner_two_passes_ahead_is_bitwise(monkeypatch):
+    """gm_mgsp3_kernel (k = 1: the partner of pass p + 1 copied into LDS two
+    passes ahead, buffer_load ... lds) performs gm_mgsp_kernel's passes and
+    sums in the same order: the GMRES history, Hessenberg and iterate are
+    bitwise those of KRY_MGS_PF2=0, for mgs and mgs2, and at a size whose
+    last block is ragged (the copies' out-of-range rows read 0)."""
+    import krylov_amd
+    from krylov_amd import problems
+
+    for n, ortho in ((200_000, "mgs"), (200_000, "mgs2"), (123_457, "mgs")):
+        R = problems.random_nonsym(n)
+        b = np.random.default_rng(3).standard_normal(n)
+        monkeypatch.setenv("KRY_MGS_PF2", "1")
+        A1 = krylov_amd.CsrOperator(R)
+        assert _state_path(A1, b, 1 if ortho == "mgs" else 2) == (True, 0)
+        _, i1 = krylov_amd.gmres(A1, b, ortho=ortho, maxiter=30, tol=0.0)
+        monkeypatch.setenv("KRY_MGS_PF2", "0")
+        _, i0 = krylov_amd.gmres(krylov_amd.CsrOperator(R), b, ortho=ortho, maxiter=30, tol=0.0)
+        np.testing.assert_array_equal(np.asarray(i1.resnorms).view(np.uint8), np.asarray(i0.resnorms).view(np.uint8))
+        np.testing.assert_array_equal(np.asarray(i1.xk).view(np.uint8), np.asarray(i0.xk).view(np.uint8))

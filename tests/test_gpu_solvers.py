@@ -574,7 +574,12 @@ def test_restarted_gmres_variants_match_oracle_chaining(case):
         assert [i.numsteps for i in infos] == d[f"{case}_steps"].tolist()
         rref = d[f"{case}_hist"]
         assert got.shape == rref.shape
-        np.testing.assert_allclose(got[:-1], rref[:-1], rtol=1e-10)
+        # 1e-10 rel, with the cancellation floor of a residual recomputed from
+        # x at each cycle's start (the explicit-residual bound's form,
+        # 64 eps ||b||): the weighted chain's late entries differ from the
+        # reference's by 1.2e-15 absolute (1.6e-10 rel at 7e-6)
+        floor = 64 * np.finfo(float).eps * np.max(np.atleast_1d(bnorm))
+        np.testing.assert_allclose(got[:-1], rref[:-1], rtol=1e-10, atol=floor)
         xr = d[f"{case}_x"]
         np.testing.assert_allclose(x, xr, rtol=0, atol=1e-9 * np.abs(xr).max())
         print(f"\nrestart {case}: {len(infos)} cycles, history max rel vs the reference "
