@@ -476,25 +476,6 @@ __device__ __forceinline__ void lds_dma16_asm(sdesc4 desc, unsigned lds, int vof
       : "v"(voff), "s"(desc), "s"(lds), "s"(soff)
       : "memory");
 }
-// this thread's 16 B at LDS byte address `lds` into o (ds_read_b128; the
-// lgkmcnt wait inside, as the compiler does not track asm LDS reads)
-template <typename V, int W>
-__device__ __forceinline__ void lds_rd16_asm(unsigned lds, V (&o)[W]) {
-  typedef int v4i __attribute__((ext_vector_type(4)));
-  v4i t;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(lds) : "memory");
-  if constexpr (W == 2) {
-    const double2 d = __builtin_bit_cast(double2, t);
-    o[0] = d.x;
-    o[1] = d.y;
-  } else {
-    const float4 f = __builtin_bit_cast(float4, t);
-    o[0] = f.x;
-    o[1] = f.y;
-    o[2] = f.z;
-    o[3] = f.w;
-  }
-}
 template <typename V, int E>
 __global__ __launch_bounds__(kMgsBlock) void gm_mgsp3_kernel(int64_t N, int k, V *__restrict__ w,
                                                              const V *__restrict__ Vb, size_t stride, int col,
@@ -552,9 +533,15 @@ __global__ __launch_bounds__(kMgsBlock) void gm_mgsp3_kernel(int64_t N, int k, V
       lds_dma16_asm(d, __builtin_amdgcn_readfirstlane(l0 + u * kRow), tid * 16,
                     __builtin_amdgcn_readfirstlane(u * kMgsBlock * 16));
   };
-  auto nb_ld = [&](int buf) {  // this thread's rows of nb[buf] into vn
+  auto nb_ld = [&](int buf) {  // this thread's rows of nb[buf] into vn (after the counted wait below)
+    asm volatile("" ::: "memory");  // the reads stay below the wait
+    typedef V vec_t __attribute__((ext_vector_type(W)));
 #pragma unroll
-    for (int u = 0; u < NV; ++u) lds_rd16_asm<V, W>(nb0 + buf * kBuf + u * kRow + tid * W * sizeof(V), vn[u]);
+    for (int u = 0; u < NV; ++u) {
+      const vec_t t = *reinterpret_cast<const vec_t *>(&nb[buf][u][tid * W]);
+#pragma unroll
+      for (int v = 0; v < W; ++v) vn[u][v] = t[v];
+    }
   };
   const int np = sweeps * (col + 1);
   auto next_of = [&](int p) -> const V * {  // the vector of pass p's inner product (null = w)
