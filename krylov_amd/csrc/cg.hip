@@ -358,7 +358,7 @@ struct PRing {
   V *s[kCgYDeferMax + 1];
 };
 
-template <typename V, typename S>
+template <typename V, typename S, bool FLUSH>
 __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *__restrict__ y, PRing<V> ring, int D,
                                                            const V *__restrict__ r, const double *__restrict__ part,
                                                            int P, double *scal, double *alpha_ring, double *hist,
@@ -372,9 +372,9 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
   __shared__ int flag;
   const int tid = threadIdx.x;
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  // gstep: this step's global index; flushes fall every D steps from fb
-  const bool flush = (gstep + 1 - fb) % D == 0;
-  const int nf = flush ? D : 0;
+  // gstep: this step's global index; flushes fall every D steps from fb (the
+  // host picks FLUSH by the same rule, so the common step carries no flush code)
+  const int nf = FLUSH ? D : 0;
   reduce_partials(part, P, k, red);
   if (tid < k) {
     const S rr = (S)red[tid];
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void cg_pdefer_kernel(int64_t N, int k, V *
     V pv[W], rv[W];
     VIO<V>::load(pi, e, N, pv);
     VIO<V>::load(r, e, N, rv);
-    if (flush) {
+    if constexpr (FLUSH) {
       V yv[W];
       VIO<V>::load_nt(y, e, N, yv);
       for (int q = 0; q < nf; ++q) {
@@ -1538,14 +1538,19 @@ bool cg_run_impl(kry_cg *s, int max_steps) {
       constexpr int W = Vec16<V>::W;
       const int G = grid_for((N + W - 1) / W, kBlock * 2);
       if (D) {
-        if (s->scalar_f32)
-          hipLaunchKernelGGL((cg_pdefer_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
-                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
-                             step, gb, s->col_offset, s->total_k, gstep, s->yfb);
-        else
-          hipLaunchKernelGGL((cg_pdefer_kernel<V, double>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y),
-                             ring, D, static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl,
-                             step, gb, s->col_offset, s->total_k, gstep, s->yfb);
+        const bool flush = (gstep + 1 - s->yfb) % D == 0;  // the kernel's rule (cg_pdefer_kernel)
+        auto go = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), ring, D,
+                             static_cast<const V *>(s->r), partB, PB, s->scal, s->alpha_ring, s->hist, s->ctrl, step,
+                             gb, s->col_offset, s->total_k, gstep, s->yfb);
+        };
+        if (s->scalar_f32) {
+          if (flush) go(cg_pdefer_kernel<V, float, true>);
+          else go(cg_pdefer_kernel<V, float, false>);
+        } else {
+          if (flush) go(cg_pdefer_kernel<V, double, true>);
+          else go(cg_pdefer_kernel<V, double, false>);
+        }
       } else if (s->scalar_f32)
         hipLaunchKernelGGL((cg_yp_kernel<V, float>), dim3(G), dim3(kBlock), 0, st, N, k, static_cast<V *>(s->y), p,
                            static_cast<const V *>(s->r), partB, PB, s->scal, s->hist, s->ctrl, step, gb,

@@ -12,7 +12,21 @@
 //   mix     every thread streams and gathers, interleaved, indices from the
 //           hash (independent of the stream)
 //   dep     every thread streams and gathers with the index taken from the
-//           streamed column word (the SpMV's dependence)
+//           streamed column word (the SpMV's dependence; the memset stream
+//           makes every index the same, so this is the stream alone)
+//   l2s     the stream's loads over a 1 MB L2-resident region (same bytes)
+//   l2split split, with the stream waves reading that L2-resident region: if
+//           this overlaps where split does not, what the two share is the
+//           time an HBM miss holds the CU's load path, not the load path
+//   sstream every 128-B line of the stream touched by one scalar load
+//           (s_load_dword, wave-uniform addresses: the scalar cache's path to
+//           L2, not the vector one): can scalar loads fill L2 ahead?
+//   ssplit  split, with the stream waves using those scalar loads
+//   cusplit roles by compute unit (HW_ID cu_id == 0: stream, else gather),
+//           each role draining its own pool of 64-KB stream chunks / 32 K
+//           gathers through an atomic counter: do stream CUs and gather CUs
+//           overlap? (a prefetch-CU design would need them to)
+//   custeal as cusplit, then each block helps drain the other pool
 //
 // If split/mix run at ~max(gather, stream), a kernel that moves the stream
 // off the gathering waves can beat the serial sum; if they run at the sum,
@@ -38,7 +52,10 @@ typedef int i4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGrid = 1024, kBlock = 256;
 constexpr int64_t kWin = 262144;                 // 2 MB of fp64
-constexpr int64_t kStreamB = 480LL << 20;        // column + value stream
+#ifndef STREAM_MB
+#define STREAM_MB 480
+#endif
+constexpr int64_t kStreamB = (int64_t)STREAM_MB << 20;  // column + value stream (-DSTREAM_MB=...)
 constexpr int64_t kQuads = kStreamB / 16;         // 16-B units
 constexpr int64_t kGathers = 40000000;
 
@@ -47,7 +64,7 @@ __device__ __forceinline__ uint32_t xs(uint32_t h) {
   return h;
 }
 
-// role: 0 gather only, 1 stream only, 2 split, 3 mix, 4 dep
+// role: 0 gather only, 1 stream only, 2 split, 3 mix, 4 dep, 5 l2s, 6 l2split, 7 sstream, 8 ssplit
 template <int ROLE>
 __global__ __launch_bounds__(kBlock) void probe(const i4 *__restrict__ s, const double *__restrict__ x,
                                                 double *__restrict__ out) {
@@ -56,11 +73,13 @@ __global__ __launch_bounds__(kBlock) void probe(const i4 *__restrict__ s, const 
   uint32_t h = (blockIdx.x * 256u + tid) * 2654435761u + 12345u;
   double acc = 0.0;
   int isum = 0;
-  bool do_g = ROLE == 0 || ROLE == 3 || (ROLE == 2 && wave < 2);
-  bool do_s = ROLE == 1 || ROLE == 3 || ROLE == 4 || (ROLE == 2 && wave >= 2);
+  constexpr bool SPLIT = ROLE == 2 || ROLE == 6 || ROLE == 8;
+  constexpr int64_t kMask = (ROLE == 5 || ROLE == 6) ? (1 << 16) - 1 : -1;  // l2s / l2split: 1 MB of quads
+  bool do_g = ROLE == 0 || ROLE == 3 || (SPLIT && wave < 2);
+  bool do_s = ROLE == 1 || ROLE == 3 || ROLE == 4 || ROLE == 5 || ROLE == 7 || (SPLIT && wave >= 2);
   if (ROLE == 4) do_g = false;
   // per-thread shares; split doubles each role's share (half the threads)
-  const int64_t gshare = (kGathers / nthr + 7) / 8 * (ROLE == 2 ? 2 : 1);   // rounds of 8
+  const int64_t gshare = (kGathers / nthr + 7) / 8 * (SPLIT ? 2 : 1);   // rounds of 8
   if (ROLE == 3) {
     // interleave: one stream quad and ~ (gathers / quads) gathers per step
     const int64_t per = kQuads / nthr;
@@ -108,15 +127,34 @@ __global__ __launch_bounds__(kBlock) void probe(const i4 *__restrict__ s, const 
         for (int g = 0; g < 8; ++g) acc += v[g];
       }
     }
-    if (do_s) {
-      const int64_t sthr = ROLE == 2 ? nthr / 2 : nthr;
-      const int64_t t0 = ROLE == 2 ? (int64_t)blockIdx.x * (kBlock / 2) + (tid - 128) : (int64_t)blockIdx.x * kBlock + tid;
+    if (do_s && (ROLE == 7 || ROLE == 8)) {
+      // one scalar dword load per 128-B line (enough to bring the line into
+      // L2), 15 in flight per wave (the lgkm counter's range)
+      const int64_t nwaves = ROLE == 8 ? (int64_t)kGrid * 2 : (int64_t)kGrid * 4;
+      const int64_t w0 = ROLE == 8 ? (int64_t)blockIdx.x * 2 + (wave - 2) : (int64_t)blockIdx.x * 4 + wave;
+      const int64_t nlines = kStreamB / 128;
+      const int *base = reinterpret_cast<const int *>(s);
+      int sacc = 0;
+      for (int64_t l = __builtin_amdgcn_readfirstlane((int)w0); l < nlines; l += 15 * nwaves) {
+        int v[15];
+#pragma unroll
+        for (int u = 0; u < 15; ++u) {
+          const int64_t ll = l + u * nwaves;
+          v[u] = base[(ll < nlines ? ll : 0) * 32];
+        }
+#pragma unroll
+        for (int u = 0; u < 15; ++u) sacc ^= v[u];
+      }
+      isum += sacc;
+    } else if (do_s) {
+      const int64_t sthr = SPLIT ? nthr / 2 : nthr;
+      const int64_t t0 = SPLIT ? (int64_t)blockIdx.x * (kBlock / 2) + (tid - 128) : (int64_t)blockIdx.x * kBlock + tid;
       for (int64_t q = t0; q < kQuads; q += 4 * sthr) {
         i4 c[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int64_t qq = q + u * sthr;
-          c[u] = qq < kQuads ? __builtin_nontemporal_load(s + qq) : i4{0, 0, 0, 0};
+          c[u] = qq < kQuads ? __builtin_nontemporal_load(s + (qq & kMask)) : i4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) isum += c[u].x ^ c[u].y ^ c[u].z ^ c[u].w;
@@ -124,6 +162,52 @@ __global__ __launch_bounds__(kBlock) void probe(const i4 *__restrict__ s, const 
     }
   }
   if (acc == 1234.5678 || isum == 0x7fffabcd) out[0] = acc + isum;  // keeps the loads
+}
+
+// pooled roles (cusplit / custeal): ctr[0] stream chunks, ctr[1] gather chunks,
+// ctr[2] blocks that took the stream role
+template <bool STEAL>
+__global__ __launch_bounds__(kBlock) void pooled(const i4 *__restrict__ s, const double *__restrict__ x,
+                                                 double *__restrict__ out, unsigned *ctr) {
+  __shared__ unsigned claim;
+  const int tid = threadIdx.x;
+  const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_REG_HW_ID, all 32 bits
+  const bool streamer = ((hwid >> 8) & 15) == 0;
+  if (streamer && tid == 0) atomicAdd(&ctr[2], 1u);
+  constexpr unsigned kSChunks = (unsigned)(kQuads / 4096), kGChunks = (unsigned)(kGathers / 32768);
+  uint32_t h = (blockIdx.x * 256u + tid) * 2654435761u + 12345u;
+  double acc = 0.0;
+  int isum = 0;
+  for (int pass = 0; pass < (STEAL ? 2 : 1); ++pass) {
+    const bool do_stream = (pass == 0) == streamer;
+    for (;;) {
+      __syncthreads();
+      if (tid == 0) claim = atomicAdd(&ctr[do_stream ? 0 : 1], 1u);
+      __syncthreads();
+      const unsigned c = claim;
+      if (c >= (do_stream ? kSChunks : kGChunks)) break;
+      if (do_stream) {
+        const i4 *p = s + (int64_t)c * 4096 + tid;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          i4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(p + (b * 4 + u) * 256);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) isum += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+      } else {
+        for (int r = 0; r < 16; ++r) {
+          double v[8];
+#pragma unroll
+          for (int g = 0; g < 8; ++g) { h = xs(h); v[g] = x[h % (uint32_t)kWin]; }
+#pragma unroll
+          for (int g = 0; g < 8; ++g) acc += v[g];
+        }
+      }
+    }
+  }
+  if (acc == 1234.5678 || isum == 0x7fffabcd) out[0] = acc + isum;
 }
 
 int main(int argc, char **argv) {
@@ -138,9 +222,10 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char *names[5] = {"gather", "stream", "split", "mix", "dep"};
-  void (*ks[5])(const i4 *, const double *, double *) = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>};
-  for (int m = 0; m < 5; ++m) {
+  const char *names[9] = {"gather", "stream", "split", "mix", "dep", "l2s", "l2split", "sstream", "ssplit"};
+  void (*ks[9])(const i4 *, const double *, double *) = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>,
+                                                         probe<5>, probe<6>, probe<7>, probe<8>};
+  for (int m = 0; m < 9; ++m) {
     float best = 1e30f, tot = 0.f;
     for (int r = 0; r < reps + 2; ++r) {
       CK(hipEventRecord(e0, 0));
@@ -153,6 +238,27 @@ int main(int argc, char **argv) {
     }
     printf("{\"mode\": \"%s\", \"ms_mean\": %.4f, \"ms_min\": %.4f}\n", names[m], tot / reps, best);
   }
+  unsigned *ctr;
+  CK(hipMalloc(&ctr, 64));
+  for (int m = 0; m < 2; ++m) {
+    float best = 1e30f, tot = 0.f;
+    unsigned h[4] = {0, 0, 0, 0};
+    for (int r = 0; r < reps + 2; ++r) {
+      CK(hipMemset(ctr, 0, 64));
+      CK(hipEventRecord(e0, 0));
+      if (m == 0) hipLaunchKernelGGL(pooled<false>, dim3(kGrid), dim3(kBlock), 0, 0, s, x, out, ctr);
+      else hipLaunchKernelGGL(pooled<true>, dim3(kGrid), dim3(kBlock), 0, 0, s, x, out, ctr);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (r >= 2) { tot += ms; best = ms < best ? ms : best; }
+      CK(hipMemcpy(h, ctr, 16, hipMemcpyDeviceToHost));
+    }
+    printf("{\"mode\": \"%s\", \"ms_mean\": %.4f, \"ms_min\": %.4f, \"stream_blocks\": %u}\n",
+           m ? "custeal" : "cusplit", tot / reps, best, h[2]);
+  }
+  CK(hipFree(ctr));
   CK(hipFree(s));
   CK(hipFree(x));
   CK(hipFree(out));
