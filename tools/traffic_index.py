@@ -29,7 +29,7 @@ CFG5 = (8_000_000, 55_760_000)
 # leg of the index -> (summary file, (n, nnz), {key: (kernel-name prefix, note)})
 LEGS = {
     "metric_cg": ("metric", METRIC, {"spmv": ("void kry::spmv_dia_kernel<double, double, 16, kry::SrcPlain", None),
-                                     "update": ("void kry::cg_upd_kernel", None)}),
+                                     "update": ("cg_upd_kernel", None)}),
     "spmv_general": ("general", METRIC, {"spmv": ("void kry::spmv_pair_kernel", None)}),
     "spmv_unstructured": ("unstructured", METRIC, {"spmv": ("void kry::spmv_rs1_kernel", None)}),
     "gmres": ("gmres_cfg3", CFG3, {"spmv": ("void kry::spmv_cbp_kernel", None),
@@ -38,7 +38,7 @@ LEGS = {
     "gmres_metric": ("gmres_metric", METRIC, {"spmv": ("void kry::spmv_dia_kernel", None),
                                               "mgs": ("gm_mgsl", "mean over the launches of a GMRES(30) cycle")}),
     "cfg4": ("cfg4", CFG4, {"spmv": ("void kry::spmv_dia_blk_kernel", None),
-                            "ppass": ("void kry::cg_pdefer_kernel", None)}),
+                            "ppass": ("cg_pdefer_kernel", None)}),
     "cfg5": ("cfg5", CFG5, {"spmv": ("void kry::spmv_dia_kernel", None), "update": ("mr_upd_kernel", None)}),
 }
 
@@ -85,7 +85,7 @@ def main():
     if os.path.exists(path):
         with open(path) as f:
             summ = json.load(f)
-        b, disp, full = kernel_bytes(summ, "void kry::cg_persist_kernel")
+        b, disp, full = kernel_bytes(summ, "cg_persist_kernel")
         iters = 210  # tools/cfg_time.py cfg2: 10 warm-up + 200 timed iterations
         idx["cfg2"] = {"iteration": {"n": CFG2[0], "nnz": CFG2[1], "bytes": b * disp / iters, "kernel": full[:120],
                                      "src": "profiles/r06_pmc_legs/cfg2.json", "build": build,
