@@ -109,3 +109,22 @@ def test_committed_traffic_index_is_of_the_shipped_library():
     for leg, ks in idx.items():
         if leg != "build":
             assert all(v["build"] == idx["build"] for v in ks.values()), leg
+
+
+def test_traffic_index_covers_every_leg_kernel():
+    """Every (leg, kernel) tools/traffic_index.py names resolves in the
+    committed PMC summaries, so no leg prints traffic: null for a kernel-name
+    mismatch (round 6: anonymous-namespace kernels were missed by a
+    'void kry::' prefix)."""
+    import importlib.util
+    import os
+
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("traffic_index", os.path.join(here, "tools", "traffic_index.py"))
+    ti = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ti)
+    idx = bench.traffic_index()
+    for leg, (_fname, _shape, keys) in ti.LEGS.items():
+        for key in keys:
+            assert key in idx.get(leg, {}), (leg, key)
+    assert "iteration" in idx["cfg2"]
