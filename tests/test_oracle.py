@@ -250,3 +250,53 @@ def test_oracle_restart_variants_match_reference(case):
     np.testing.assert_array_equal(steps, d[f"{case}_steps"])
     np.testing.assert_allclose(hist, d[f"{case}_hist"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(x, d[f"{case}_x"], rtol=0, atol=1e-10 * np.abs(d[f"{case}_x"]).max())
+
+
+def _extra():
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "extra.npz"))
+
+
+def _extra_ref_cases(solver):
+    from tests import gpu_helpers as H
+
+    if solver in ("bicgstab", "cgs"):
+        return [H.spd_dense((5,)), H.spd_sparse((5,)), H.spd_dense((5, 1)), H.spd_dense((5, 3)),
+                H.spd_rhs_0((5,)), H.spd_rhs_0sol0(), H.symmetric_indefinite(), H.real_unsymmetric()]
+    return [H.spd_dense((5,)), H.spd_sparse((5,)), H.spd_sparse((5, 1)), H.spd_sparse((5, 3)),
+            H.spd_rhs_0((5,)), H.spd_rhs_0sol0(), H.symmetric_indefinite()]
+
+
+@pytest.mark.parametrize("solver", ["bicgstab", "cgs", "cgr", "gcr"])
+def test_oracle_extra_solvers_match_reference(solver):
+    """The oracle's bicgstab / cgs / cgr / gcr against the reference's own
+    runs (tests/golden/extra.npz, make_extra.py): random nonsymmetric n = 5000
+    (Poisson 40^2 for cgr) to 1e-9, and the real cases of the reference's
+    tests/test_<solver>.py: same steps, histories and iterates to 1e-12."""
+    d = _extra()
+    A = problems.poisson2d(40) if solver == "cgr" else problems.random_nonsym(5000)
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    _, info = getattr(K, solver)(A, b, tol=1e-9, maxiter=150)
+    assert info.numsteps == int(d[f"{solver}_rand_numsteps"]) and info.success == bool(d[f"{solver}_rand_success"])
+    np.testing.assert_allclose(np.asarray(info.resnorms, dtype=np.float64), d[f"{solver}_rand_resnorms"],
+                               rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(info.xk, d[f"{solver}_rand_x"], rtol=1e-12, atol=1e-14)
+    for i, (A, b) in enumerate(_extra_ref_cases(solver)):
+        _, info = getattr(K, solver)(A, b, tol=1.0e-7, maxiter=10)
+        assert info.numsteps == int(d[f"{solver}_ref{i}_numsteps"]), i
+        np.testing.assert_allclose(np.asarray(info.resnorms, dtype=np.float64), d[f"{solver}_ref{i}_resnorms"],
+                                   rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(np.asarray(info.xk, dtype=np.float64), d[f"{solver}_ref{i}_x"], rtol=1e-12,
+                                   atol=1e-14)
+
+
+@pytest.mark.parametrize("solver", ["bicgstab", "cgs"])
+def test_oracle_fullsize_cfg3_extra(solver):
+    """The oracle's bicgstab / cgs on the BASELINE cfg3 matrix, 20 steps,
+    against the reference's own run (extra.npz cfg3_*)."""
+    d = _extra()
+    R = problems.random_nonsym(2_000_000)
+    _, info = getattr(K, solver)(R, np.ones(R.shape[0]), tol=0.0, maxiter=20)
+    assert info.numsteps == int(d[f"cfg3_{solver}_numsteps"])
+    np.testing.assert_allclose(np.asarray(info.resnorms, dtype=np.float64), d[f"cfg3_{solver}_resnorms"],
+                               rtol=1e-11, atol=0)
+    np.testing.assert_allclose(info.xk[d["cfg3_sample_idx"]], d[f"cfg3_{solver}_xsample"], rtol=1e-10, atol=0)
